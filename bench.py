@@ -1,0 +1,224 @@
+"""Benchmark: CTR training examples/sec of the fused HIP step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu-baseline]
+
+N>1 is launched by the driver as `python -m torch.distributed.run --nproc-per-node N ...`:
+one process per GPU, RCCL over xGMI, data parallel with replicated tables (weak scaling:
+every rank trains its own B-example batches; value = all ranks' examples / max time).
+
+Workload (default c3 = BASELINE configs[2], the north-star target shape): DeepFM, 26
+fields, 10M-id vocabulary, embed_dim 64, batch 8192 per GPU, synthetic Criteo-shape ids
+(skewed field cardinalities, Zipf(1.1) within fields) and planted-FM labels, inputs
+resident in HBM, reference semantics (dense Adam, lr 1e-3, wd 1e-5, dropout 0.2).
+c2 = configs[1]: FM, 1M vocab, dim 16, batch 4096.
+
+The JSON line carries `roofline` for the dominant kernel (the dense Adam pass over the
+table, adam_embedding_vec, timed per launch with HIP events on its stream inside the
+timed region) and `cpu_baseline` (the oracle = torch-CPU restatement of the reference,
+timed on this host's cores on a bounded sample of the same workload, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "CTR train examples/sec at 1/2/4/8 MI355X; HBM GB/s on embedding gather/scatter"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+CONFIGS = {
+    "c3": dict(kind="DeepFM", V=10_000_000, F=26, K=64, B=8192,
+               workload="C3 DeepFM (FM + MLP 1664-300-200-1), Criteo-shape 26 fields, "
+                        "10M vocab, embed_dim 64, batch 8192/GPU"),
+    "c2": dict(kind="FM", V=1_000_000, F=26, K=16, B=4096,
+               workload="C2 FM, Criteo-shape 26 fields, 1M vocab, embed_dim 16, batch 4096/GPU"),
+}
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def adam_bytes(V, K, U):
+    """Algorithmic bytes of one dense-Adam pass over E[V,K] + w[V]:
+    read+write p, m, v for every element (24 B), the rowmap read (4 B/row), and for the
+    U rows present in the batch their gradient row (4K B), linear grad (4 B) and the
+    rowmap reset (4 B)."""
+    return 24 * V * (K + 1) + 4 * V + U * (4 * K + 8)
+
+
+def gather_bytes(S, K, B, deep):
+    """fm_forward: int64 ids (8 B/slot), the gathered row (4K B) and linear weight (4 B)
+    per slot, the per-example sums written (4K B/example), and for DeepFM the flat MLP
+    input written (4K B/slot)."""
+    return S * (8 + 4 * K + 4) + B * 4 * K + (S * 4 * K if deep else 0) + B * 16
+
+
+def scatter_bytes(S, K, U, deep):
+    """fm_embedding_grad: per slot its plan entries (12 B) and example terms (4 B gz +
+    4K B sum_e), for DeepFM the MLP-input gradient row (4K B); per unique row the table
+    row read, the gradient row written (4K B each) and the linear grad (4 B)."""
+    return S * (12 + 4 + 4 * K + (4 * K if deep else 0)) + U * (8 * K + 8)
+
+
+def cpu_baseline(cfg, batches, max_seconds=25.0):
+    """The oracle (torch-CPU restatement, pinned to the reference) on this host."""
+    from oracle import ctr_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    params = O.init_params(cfg["kind"], cfg["V"], cfg["F"], cfg["K"], seed=1)
+    opt = O.make_optimizer(params, 1e-3, 1e-5)
+    init_s = time.perf_counter() - t0
+    xs = [torch.from_numpy(x) for x, _ in batches]
+    ys = [torch.from_numpy(y) for _, y in batches]
+    O.train_step(cfg["kind"], params, opt, xs[0], ys[0])  # warm-up (allocates dense grads)
+    n, t = 0, 0.0
+    while n < 1 or (t < max_seconds and n < 10):
+        s = time.perf_counter()
+        O.train_step(cfg["kind"], params, opt, xs[n % len(xs)], ys[n % len(ys)])
+        t += time.perf_counter() - s
+        n += 1
+        if t > max_seconds / 2 and n >= 3:
+            break
+    eps = n * cfg["B"] / t
+    return {"value": eps, "unit": "examples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} timed steps (+1 warm-up) of the same workload and batches on the "
+                      f"host CPU, oracle/ctr_oracle.py train_step (torch-CPU ops as the "
+                      f"reference: dense nn.Embedding grads, torch.optim.Adam); "
+                      f"{t / n * 1e3:.0f} ms/step; param init {init_s:.1f} s untimed"}
+
+
+def load_traffic(config: str, kernel: str):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes with the gfx950 corrections, profiles/)."""
+    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        k = d.get(config, {}).get(kernel)
+        if k and k.get("hbm_bytes_per_launch"):
+            return float(k["hbm_bytes_per_launch"]), p.name
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--batches", type=int, default=4, help="distinct synthetic batches cycled")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rl_ctr_prediction_amd import DeepFM, FM, FusedCTRTrainer
+    from rl_ctr_prediction_amd.synthetic import CriteoSynth
+
+    cfg = CONFIGS[args.config]
+    V, F, K, B = cfg["V"], cfg["F"], cfg["K"], cfg["B"]
+    t0 = time.perf_counter()
+    torch.manual_seed(1)  # identical replicas on every rank
+    with torch.device(dev):
+        model = FM(V, K) if cfg["kind"] == "FM" else DeepFM(V, F, K)
+    model.train()
+    synth = CriteoSynth(V, F, seed=1)
+    host_batches = list(synth.batches(args.batches, B, rank=rank))
+    xs = [torch.from_numpy(x).to(dev) for x, _ in host_batches]
+    ys = [torch.from_numpy(y).to(dev) for _, y in host_batches]
+    trainer = FusedCTRTrainer(model, lr=1e-3, weight_decay=1e-5, seed=1234)
+    log(f"rank {rank}/{world}: {cfg['kind']} V={V} K={K} B={B} ready in {time.perf_counter() - t0:.1f}s")
+
+    for i in range(args.warmup):
+        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    trainer.timing = {"adam": [], "gather": [], "scatter": []}
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    timing = trainer.timing
+    trainer.timing = None
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    def avg_ms(pairs):
+        return float(np.mean([a.elapsed_time(b) for a, b in pairs])) if pairs else float("nan")
+
+    U = trainer._bufs.plan.num_unique_host()
+    S = B * F
+    adam_ms = avg_ms(timing["adam"])
+    gather_ms, scatter_ms = avg_ms(timing["gather"]), avg_ms(timing["scatter"])
+    deep = cfg["kind"] == "DeepFM"
+    a_bytes = adam_bytes(V, K, U)
+    achieved = a_bytes / (adam_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.config, "adam_embedding_vec")
+    value = world * B * args.steps / elapsed
+    result = {
+        "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (Criteo-shape ids: skewed field cardinalities, Zipf(1.1); "
+                "planted-FM labels, CTR~0.25); random-init weights",
+        "config": {"workload": cfg["workload"], "model": cfg["kind"], "global_batch": B * world,
+                   "fields": F, "vocab": V, "embed_dim": K,
+                   "parallelism": f"dp{world} (replicated tables, sparse grad all-gather)",
+                   "optimizer": "dense Adam lr=1e-3 wd=1e-5 (reference semantics)"},
+        "roofline": {"kernel": "adam_embedding_vec (dense Adam over E[V,K] + w[V])",
+                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": a_bytes, "avg_launch_ms": adam_ms},
+        "gather_scatter": {
+            "gather_kernel": "fm_forward_vec", "gather_ms": gather_ms,
+            "gather_GBps": gather_bytes(S, K, B, deep) / (gather_ms * 1e-3) / 1e9,
+            "scatter_kernels": "sparse plan (radix sort + scan) + fm_embedding_grad",
+            "scatter_ms": scatter_ms,
+            "scatter_GBps": scatter_bytes(S, K, U, deep) / (scatter_ms * 1e-3) / 1e9,
+            "unique_rows_per_batch": U, "slots_per_batch": S},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        result["cpu_baseline"] = cpu_baseline(cfg, host_batches)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,225 @@
+/*
+ * ctr_hip.h — C ABI of libctr_hip.so, the MI355X (gfx950) hot path of
+ * jqsl2012/RL_CTR_Prediction's CTR training step.
+ *
+ * Scope: the multi-field sparse->embedding gather, the FM
+ * interaction (sum-square trick) and linear term, the DeepFM MLP head, the log-loss
+ * (BCE after sigmoid) backward, the embedding scatter-add, the coupled-L2 Adam step,
+ * Feature_Embedding's pairwise inner products and the REINFORCE loss of PG_model.
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers and sizes, row-major, fp32 unless stated; index arrays are
+ *     int32 (CTR_IDX_I32) or int64 (CTR_IDX_I64, what the reference's LongTensor holds);
+ *   - all work is enqueued on `stream` (a hipStream_t; NULL = legacy default stream);
+ *     nothing synchronises, nothing allocates; scratch is caller-owned and sized by the
+ *     matching *_workspace_bytes() query;
+ *   - return CTR_OK (0) or a CTR_ERR_* code; ctr_last_error() then holds a thread-local
+ *     message. Out-of-range feature ids never fault: the kernel reads row 0 instead and
+ *     ORs CTR_EFLAG_INDEX into *err_flag (optional device int32), the analogue of
+ *     nn.Embedding's "index out of range" error, checked by the host when it chooses.
+ */
+#ifndef CTR_HIP_H
+#define CTR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* ctr_stream_t; /* hipStream_t */
+
+enum ctr_status {
+  CTR_OK = 0,
+  CTR_ERR_INVALID = 1,     /* argument out of contract */
+  CTR_ERR_HIP = 2,         /* HIP runtime / launch error */
+  CTR_ERR_WORKSPACE = 3,   /* scratch smaller than the *_workspace_bytes() answer */
+  CTR_ERR_UNSUPPORTED = 4  /* shape this build does not handle */
+};
+
+enum ctr_idx_type { CTR_IDX_I32 = 0, CTR_IDX_I64 = 1 };
+
+enum ctr_err_flag { CTR_EFLAG_INDEX = 1 };
+
+/* GEMM epilogues (ctr_gemm_f32). */
+enum ctr_epilogue {
+  CTR_EPI_NONE = 0,            /* C = A.B                                                  */
+  CTR_EPI_BIAS = 1,            /* C = A.B + bias[n]                                        */
+  CTR_EPI_BIAS_RELU = 2,       /* C = relu(A.B + bias[n])                                  */
+  CTR_EPI_BIAS_RELU_DROP = 3,  /* C = dropout(relu(A.B + bias[n]); p, seed, offset)        */
+  CTR_EPI_GRAD_MASK = 4        /* C = aux[m,n] > 0 ? (A.B) * scale : 0  (relu+dropout bwd) */
+};
+
+int ctr_abi_version(void);
+const char* ctr_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU); never initialises a context
+ * beyond hipGetDeviceCount. */
+int ctr_device_count(void);
+
+/* ---------------------------------------------------------------- A3: gather ---------
+ * out[i, :] = table[idx[i], :]  — nn.Embedding.forward.
+ * Replaces: p_model.py:47,303,320 and Feature_embedding.py:52 (self.feature_embedding(x)). */
+int ctr_embedding_gather(const float* table, int64_t V, int K, const void* idx, int idx_type,
+                         int64_t n, float* out, int32_t* err_flag, ctr_stream_t stream);
+
+/* ------------------------------------------------------ A1/A2/A4: FM forward ---------
+ * Fused gather + FM second order + linear term for B examples of F fields:
+ *   z[b]      = bias[0] + sum_f lin[x_bf] + 0.5 * sum_k ((sum_f E[x_bf,k])^2 - sum_f E[x_bf,k]^2)
+ *   sum_e     [B,K]   sum_f E[x_bf,:]      (optional; the backward needs it)
+ *   emb_out   [B,F*K] E[x_bf,:] flattened  (optional; DeepFM's MLP input)
+ * If labels != NULL the BCE-after-sigmoid head is fused (FM model):
+ *   p[b] = sigmoid(z[b]); loss_elem[b] = BCE(p, y) (log clamped at -100);
+ *   gz[b] = d(mean BCE)/dz with the reference's UNFUSED formula in ATen's operation order,
+ *           mean_div = the batch the mean runs over (B, or B_global under data parallel):
+ *           g_p = ((p-y)/max((1-p)p, 1e-12))/mean_div; gz = (g_p*(1-p))*p.
+ *   p, loss_elem, gz may then be non-NULL individually.
+ * Replaces: p_model.py:40-57 (FM.forward), 296-313 (DeepFM.to_fm), nn.BCELoss at
+ * all_main/pretrain_main.py:74,139. */
+int ctr_fm_forward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                   const float* emb, const float* lin, const float* bias,
+                   float* z, float* sum_e, float* emb_out,
+                   const float* labels, float mean_div,
+                   float* p, float* loss_elem, float* gz,
+                   int32_t* err_flag, ctr_stream_t stream);
+
+/* BCE after sigmoid on precomputed logits (same formulas as the fused FM head).
+ * Replaces: torch.sigmoid (p_model.py:55,324) + nn.BCELoss (pretrain_main.py:74). */
+int ctr_bce_sigmoid(const float* z, const float* labels, int64_t B, float mean_div,
+                    float* p, float* loss_elem, float* gz, ctr_stream_t stream);
+
+/* DeepFM output head: z[b] = z_fm[b] + h[b,:].w_out + b_out[0]; then the BCE head as above.
+ * dh_pre[b,j] = h[b,j] > 0 ? gz[b]*w_out[j]*drop_scale : 0  (grad through the last
+ * Linear, the Dropout and the ReLU that produced h; drop_scale = 1/(1-p) or 1 in eval).
+ * Replaces: p_model.py:322-324 (mlp[6] Linear(200,1) + sum + sigmoid), pretrain_main.py:74. */
+int ctr_deepfm_head(const float* h, int64_t B, int H, const float* w_out, const float* b_out,
+                    const float* z_fm, const float* labels, float mean_div, float drop_scale,
+                    float* z, float* p, float* loss_elem, float* gz, float* dh_pre,
+                    ctr_stream_t stream);
+
+/* -------------------------------------------------------- MLP: fp32 MFMA GEMM ---------
+ * C[M,N] = op(A)[M,K] . op(B)[K,N] with epilogue `epi` (enum ctr_epilogue).
+ * trans_a = 0: A stored [M,K] (lda >= K); 1: A stored [K,M] (lda >= M).
+ * trans_b = 0: B stored [K,N] (ldb >= N); 1: B stored [N,K] (ldb >= K)  (nn.Linear weight).
+ * Dropout keeps element (m,n) iff hash(seed, offset + m*N + n) >= p*2^32 and scales by
+ * 1/(1-p). `scale` is used by CTR_EPI_GRAD_MASK. Split-K (long K, few tiles) uses `ws`.
+ * Replaces: nn.Linear / ReLU / Dropout of DeepFM.mlp (p_model.py:276-293) and of
+ * PG_model.Net.mlp (PG_model.py:41-51), forward and autograd backward (dX and dW). */
+int64_t ctr_gemm_f32_workspace_bytes(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K);
+int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                 const float* A, int64_t lda, const float* B, int64_t ldb,
+                 float* C, int64_t ldc, int epi, const float* bias,
+                 const float* aux, int64_t ldaux, float scale,
+                 float drop_p, uint64_t seed, uint64_t offset,
+                 void* ws, int64_t ws_bytes, ctr_stream_t stream);
+
+/* Deterministic reductions (fixed order; identical bits run to run).
+ * ctr_sum_f32:    out[0] = scale * sum_i x[i]
+ * ctr_colsum_f32: out[n] = scale * sum_m (row_w ? row_w[m] : 1) * X[m,n]   (bias / dW of
+ *                 a 1-row Linear). */
+int64_t ctr_reduce_workspace_bytes(int64_t M, int64_t N);
+int ctr_sum_f32(const float* x, int64_t n, float scale, float* out, void* ws, int64_t ws_bytes,
+                ctr_stream_t stream);
+int ctr_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, const float* row_w,
+                   float scale, float* out, void* ws, int64_t ws_bytes, ctr_stream_t stream);
+
+/* ------------------------------------------------ A3: embedding scatter-add -----------
+ * A sparse plan groups the S = B*F slots (slot s = b*F + f) of a batch by feature id.
+ * All arrays are caller-owned device buffers of S int32 (seg_offsets: S+1, num_unique: 1):
+ *   sorted_slots  slot ids ordered by (row, slot) — a STABLE sort, so each row's slots keep
+ *                 the order embedding_dense_backward accumulates them in;
+ *   sorted_rows   the row of each sorted position;
+ *   pos_seg       the segment (unique-row ordinal) of each sorted position;
+ *   unique_rows   the distinct rows ascending, first *num_unique valid;
+ *   seg_offsets   row u owns sorted positions [seg_offsets[u], seg_offsets[u+1]).
+ * Index work: bit-exact (tests compare with numpy.unique). Replaces the grouping inside
+ * embedding_dense_backward (autograd through p_model.py:47,54,303,311,320). */
+typedef struct ctr_sparse_plan {
+  int64_t S;
+  int32_t* sorted_slots;
+  int32_t* sorted_rows;
+  int32_t* pos_seg;
+  int32_t* unique_rows;
+  int32_t* seg_offsets;
+  int32_t* num_unique;
+} ctr_sparse_plan;
+
+int64_t ctr_sparse_plan_workspace_bytes(int64_t S, int64_t V);
+int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
+                          void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
+
+/* Segmented row sums over a plan, deterministic: each row's slots are summed in slot
+ * order in chunks of 16 positions, chunk partials are then added in chunk order (hot
+ * rows spread over many waves; identical bits run to run and rank to rank).
+ *   ctr_fm_embedding_grad (FM / DeepFM backward, slot s = b*F + f):
+ *     grad_rows[u,:] = sum_{s in row u} ((gz[b]*sum_e[b,:] - gz[b]*E[row,:]) + dx[s,:])
+ *     grad_lin[u]    = sum_{s in row u} gz[b]
+ *     dx (the MLP input gradient, [B, F*K]) is NULL for FM.
+ *   ctr_segment_sum_rows (generic; multi-GPU exchange): out[u,:] = sum vals[s,:],
+ *     out_lin[u] = sum vals_lin[s] (both optional-lin).
+ * If rowmap != NULL also rowmap[row_u] = u (ctr_adam_embedding consumes and resets it).
+ * Replaces: FM/DeepFM backward through p_model.py:47-54 / 303-311 / 320-322 and
+ * embedding_dense_backward. */
+int64_t ctr_segment_workspace_bytes(int64_t S, int K);
+int ctr_fm_embedding_grad(const ctr_sparse_plan* plan, int F, int K, const float* emb,
+                          const float* gz, const float* sum_e, const float* dx,
+                          float* grad_rows, float* grad_lin, int32_t* rowmap, void* ws,
+                          int64_t ws_bytes, ctr_stream_t stream);
+int ctr_segment_sum_rows(const ctr_sparse_plan* plan, int K, const float* vals,
+                         const float* vals_lin, float* out, float* out_lin, int32_t* rowmap,
+                         void* ws, int64_t ws_bytes, ctr_stream_t stream);
+
+/* Dense gradient for the autograd (drop-in) path: dense[V,K] (and dense_lin[V], optional)
+ * must be zero on entry; dense[row_u,:] = grad_rows[u,:]. */
+int ctr_rows_to_dense(const ctr_sparse_plan* plan, int K, const float* grad_rows,
+                      const float* grad_lin, float* dense, float* dense_lin,
+                      ctr_stream_t stream);
+
+/* ---------------------------------------------------------------- A5: Adam -----------
+ * torch.optim.Adam(lr, betas, eps, weight_decay) with coupled L2, one step, for EVERY
+ * element (dense semantics). Host-computed step scalars (as torch computes them):
+ *   step_size = lr / (1 - beta1^t),  bc2_sqrt = sqrt(1 - beta2^t).
+ * Per element: g += wd*p; m += (1-beta1)*(g-m); v = v*beta2 + (1-beta2)*g*g;
+ *              p += -step_size * (m / (sqrt(v)/bc2_sqrt + eps)).
+ * ctr_adam_dense:     g is a dense gradient (MLP, bias).
+ * ctr_adam_embedding: the embedding table E[V,K] and the linear table w[V] in one pass;
+ *   the gradient of row r is grad_rows[rowmap[r]] when rowmap[r] >= 0, else 0; rowmap
+ *   entries read >= 0 are reset to -1. lin/m_lin/v_lin may be NULL (Feature tables w/o
+ *   a linear term). Replaces: torch.optim.Adam.step at all_main/pretrain_main.py:78,153. */
+int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n, double step_size,
+                   double bc2_sqrt, double beta1, double beta2, double eps, double weight_decay,
+                   ctr_stream_t stream);
+int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                       float* v_lin, int64_t V, int K, int32_t* rowmap,
+                       const float* grad_rows, const float* grad_lin, double step_size,
+                       double bc2_sqrt, double beta1, double beta2, double eps,
+                       double weight_decay, ctr_stream_t stream);
+
+/* ------------------------------------------------ A7: Feature_Embedding -------------
+ * out[b] = [ <E[x_bi],E[x_bj]> for i<j in row-major pair order ] ++ flat(E[x_b]),
+ * out is [B, F(F-1)/2 + F*K]. Replaces: Feature_embedding.py:51-59. */
+int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int F, int K,
+                                  int64_t V, const float* emb, float* out, int32_t* err_flag,
+                                  ctr_stream_t stream);
+
+/* ------------------------------------------------------ A8: REINFORCE (PG) -----------
+ * ctr_softmax_rows: out[b,:] = softmax(x[b,:]) (PG_model.py:56).
+ * ctr_pg_discount_norm: discounted return of an episode, reverse recurrence
+ *   d[i] = r[i] + gamma*d[i+1] in fp64, then (d - mean)/std (population std), written as
+ *   fp64 `out` and fp32 `out_f32`; stats[0..1] = mean, std (fp64, std before division).
+ *   Replaces PG_model.py:139-154.
+ * ctr_pg_loss_grad: loss = sum_b(-log probs[b, act_b - 1]) * mean(vt) (PG_model.py:104-107,
+ *   actions 1-based) and the gradient w.r.t. the softmax LOGITS (softmax backward fused),
+ *   scaled by grad_scale. loss_out is a device scalar. */
+int ctr_softmax_rows(const float* x, int64_t B, int A, float* out, ctr_stream_t stream);
+int64_t ctr_pg_workspace_bytes(int64_t n);
+int ctr_pg_discount_norm(const float* r, int64_t n, double gamma, double* out, float* out_f32,
+                         double* stats, void* ws, int64_t ws_bytes, ctr_stream_t stream);
+int ctr_pg_loss_grad(const float* probs, const int64_t* acts, const float* vt, int64_t B,
+                     int A, float grad_scale, float* loss_out, float* dlogits, void* ws,
+                     int64_t ws_bytes, ctr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CTR_HIP_H */

@@ -1,0 +1,203 @@
+"""CPU oracle for the CTR hot path — TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's `cpu_baseline` leg may import this
+module, and only as the checker / the timed CPU baseline. The product path
+(rl_ctr_prediction_amd) never imports it and has no CPU fallback.
+
+A from-scratch restatement of jqsl2012/RL_CTR_Prediction's algorithms on torch-CPU
+(the reference's own runtime) + numpy, written functionally from SURVEY.md §8a:
+
+  fm_forward          p_model.py:40-57       (FM.forward)
+  deepfm_forward      p_model.py:296-324     (DeepFM.to_fm + forward, MLP 276-293)
+  bce                 all_main/pretrain_main.py:74,139 (nn.BCELoss, mean)
+  train_step          all_main/pretrain_main.py:67-83 (fwd, BCE, zero_grad, backward, Adam)
+  feature_embedding   Feature_embedding.py:51-59
+  pg_*                PG_model.py:104-154 (loss_func, choose_action, discount_and_norm)
+  sparse_plan         the grouping inside embedding_dense_backward (numpy, bit-exact ints)
+  pretrain_run        all_main/pretrain_main.py:119-202 (per-epoch Adam, no shuffle, AUC)
+
+Parity is PINNED: tests/test_oracle.py checks every function here against the golden
+vectors in tests/golden/, produced by importing the reference itself
+(tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as Fn
+
+# ---------------------------------------------------------------- parameters --------
+FM_KEYS = ("bias", "linear.weight", "feature_embedding.weight")
+DEEPFM_KEYS = FM_KEYS + ("mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bias",
+                         "mlp.6.weight", "mlp.6.bias")
+
+
+def init_params(kind: str, V: int, F: int, K: int, seed: int | None = None) -> dict:
+    """Parameters with the reference modules' default initialisers, created in the
+    reference's order: N(0,1) embeddings (nn.Embedding), zero bias, nn.Linear's
+    kaiming-uniform weights / uniform biases."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    p = {"linear.weight": torch.nn.Embedding(V, 1).weight.data,
+         "bias": torch.zeros(1),
+         "feature_embedding.weight": torch.nn.Embedding(V, K).weight.data}
+    if kind == "DeepFM":
+        dims = [F * K, 300, 200, 1]
+        for i, name in zip(range(3), ("mlp.0", "mlp.3", "mlp.6")):
+            lin = torch.nn.Linear(dims[i], dims[i + 1])
+            p[f"{name}.weight"] = lin.weight.data
+            p[f"{name}.bias"] = lin.bias.data
+    return {k: v.clone().requires_grad_(True) for k, v in p.items()}
+
+
+# ------------------------------------------------------------------ forward ---------
+def fm_logit(params: dict, x: torch.Tensor) -> torch.Tensor:
+    """bias + sum_f w[x_f] + 0.5 * sum_k((sum_f e_fk)^2 - sum_f e_fk^2), shape [B,1]."""
+    e = Fn.embedding(x, params["feature_embedding.weight"])            # [B,F,K]
+    square_of_sum = e.sum(dim=1) ** 2
+    sum_of_square = (e ** 2).sum(dim=1)
+    inter = (square_of_sum - sum_of_square).sum(dim=1, keepdim=True)
+    lin = Fn.embedding(x, params["linear.weight"]).sum(dim=1)            # [B,1]
+    return params["bias"] + lin + inter * 0.5
+
+
+def fm_forward(params: dict, x: torch.Tensor) -> torch.Tensor:
+    return torch.sigmoid(fm_logit(params, x))
+
+
+def mlp(params: dict, h: torch.Tensor, drop_p: float, training: bool) -> torch.Tensor:
+    for name in ("mlp.0", "mlp.3"):
+        h = Fn.relu(Fn.linear(h, params[f"{name}.weight"], params[f"{name}.bias"]))
+        h = Fn.dropout(h, p=drop_p, training=training)
+    return Fn.linear(h, params["mlp.6.weight"], params["mlp.6.bias"])
+
+
+def deepfm_forward(params: dict, x: torch.Tensor, drop_p: float = 0.2,
+                   training: bool = True) -> torch.Tensor:
+    B, F = x.shape
+    e = Fn.embedding(x, params["feature_embedding.weight"])
+    deep = mlp(params, e.reshape(B, -1), drop_p, training)
+    return torch.sigmoid(fm_logit(params, x) + deep)
+
+
+def forward(kind: str, params: dict, x, drop_p=0.2, training=True):
+    return fm_forward(params, x) if kind == "FM" else deepfm_forward(params, x, drop_p, training)
+
+
+def bce(p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    return Fn.binary_cross_entropy(p, y)
+
+
+# ---------------------------------------------------------------- training ---------
+def make_optimizer(params: dict, lr: float, weight_decay: float):
+    """torch.optim.Adam over the parameters (reference: all_main/pretrain_main.py:153),
+    in state_dict order so the optimiser state lines up with the reference's."""
+    return torch.optim.Adam(list(params.values()), lr=lr, weight_decay=weight_decay)
+
+
+def train_step(kind: str, params: dict, opt, x: torch.Tensor, y: torch.Tensor,
+               drop_p: float = 0.2) -> float:
+    """One reference step: forward, BCE, zero_grad, backward (dense embedding grads),
+    Adam.step, loss.item()  (all_main/pretrain_main.py:72-79)."""
+    p = forward(kind, params, x, drop_p, True)
+    loss = bce(p, y.reshape(-1, 1).float())
+    for t in params.values():
+        t.grad = None
+    loss.backward()
+    opt.step()
+    return loss.item()
+
+
+def grads(kind: str, params: dict, x, y, drop_p=0.0) -> tuple[float, torch.Tensor, dict]:
+    p = forward(kind, params, x, drop_p, True)
+    loss = bce(p, y.reshape(-1, 1).float())
+    for t in params.values():
+        t.grad = None
+    loss.backward()
+    return loss.item(), p.detach(), {k: v.grad.clone() for k, v in params.items()}
+
+
+# ------------------------------------------------------------ scatter grouping -------
+def sparse_plan(x: np.ndarray):
+    """Stable grouping of slots by id: (sorted_slots, sorted_rows, pos_seg, unique_rows,
+    seg_offsets) — what ctr_sparse_plan_build must reproduce bit-exactly."""
+    flat = np.asarray(x).reshape(-1).astype(np.int64)
+    order = np.argsort(flat, kind="stable")
+    rows = flat[order]
+    uniq, first, counts = np.unique(rows, return_index=True, return_counts=True)
+    offsets = np.concatenate([first, [flat.size]]).astype(np.int64)
+    pos_seg = np.repeat(np.arange(uniq.size), counts)
+    return order, rows, pos_seg, uniq, offsets
+
+
+# -------------------------------------------------------------- Feature_Embedding ----
+def feature_embedding(E: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    B, F = x.shape
+    e = Fn.embedding(x, E)
+    i, j = np.triu_indices(F, k=1)          # row-major pairs (i<j), Feature_embedding.py:40-43
+    inner = (e[:, i] * e[:, j]).sum(dim=2)
+    return torch.cat([inner, e.reshape(B, -1)], dim=1).detach()
+
+
+# -------------------------------------------------------------------- REINFORCE -----
+def pg_discount_and_norm(r: np.ndarray, gamma: float) -> np.ndarray:
+    """Reverse discounted return in float64, then (d - mean) / std (PG_model.py:139-154)."""
+    r = np.asarray(r, dtype=np.float32).reshape(-1)
+    d = np.zeros(r.shape + (1,), dtype=np.float64)
+    run = 0.0
+    for i in range(r.size - 1, -1, -1):
+        run = run * gamma + float(r[i])
+        d[i] = run
+    d -= np.mean(d)
+    std = np.std(d)
+    if std == 0:
+        raise FloatingPointError("divide by zero encountered in divide")
+    d /= std
+    return d
+
+
+def pg_loss(probs: torch.Tensor, acts: torch.Tensor, vt: torch.Tensor) -> torch.Tensor:
+    """sum_b(-log p[b, a_b-1]) * mean(vt)  (PG_model.py:104-107; acts are 1-based)."""
+    nlp = torch.sum(-torch.log(probs.gather(1, acts.reshape(-1, 1).long() - 1)))
+    return torch.mean(nlp * vt)
+
+
+def pg_choose_action(probs: torch.Tensor, action_nums: int) -> torch.Tensor:
+    """PG_model.py:110-121 on host probabilities (same CPU RNG calls, same order)."""
+    n = probs.shape[0]
+    random_seeds = torch.rand(n, 1)
+    max_action = torch.argsort(-probs)[:, 0] + 1
+    random_action = torch.randint(low=1, high=action_nums + 1, size=[n, 1])
+    return torch.where(random_seeds >= torch.max(probs, 1)[0].view(-1, 1),
+                       max_action.view(-1, 1), random_action)
+
+
+# --------------------------------------------------------------------- driver -------
+def pretrain_run(kind: str, train: np.ndarray, test: np.ndarray, V: int, K: int, epochs: int,
+                 lr: float, wd: float, batch: int, seed: int = 1, drop_p: float = 0.0):
+    """all_main/pretrain_main.main without files: Adam re-created every epoch, batches in
+    file order, train loss = mean of batch losses, AUC over the test split."""
+    from sklearn.metrics import roc_auc_score
+    F = train.shape[1] - 1
+    params = init_params(kind, V, F, K, seed=seed)
+    hist = []
+    xt = torch.from_numpy(test[:, 1:]).long()
+    yt = torch.from_numpy(test[:, 0]).float()
+    for _ in range(epochs):
+        opt = make_optimizer(params, lr, wd)
+        losses = []
+        for s in range(0, len(train), batch):
+            xb = torch.from_numpy(train[s:s + batch, 1:]).long()
+            yb = torch.from_numpy(train[s:s + batch, 0]).float()
+            losses.append(train_step(kind, params, opt, xb, yb, drop_p))
+        with torch.no_grad():
+            preds, vl = [], []
+            for s in range(0, len(test), batch):
+                p = forward(kind, params, xt[s:s + batch], drop_p, False)
+                vl.append(bce(p, yt[s:s + batch].reshape(-1, 1)).item())
+                preds.append(p.reshape(-1))
+            pr = torch.cat(preds).numpy()
+        hist.append(dict(train_loss=sum(losses) / len(losses),
+                         valid_auc=float(roc_auc_score(test[:, 0], pr)),
+                         valid_loss=sum(vl) / len(vl)))
+    return hist, params

@@ -1,0 +1,119 @@
+"""ctypes binding of libctr_hip.so (the C ABI declared in include/ctr_hip.h).
+
+This is the only way the package reaches the GPU: there is no CPU or eager-PyTorch
+fallback for any op on the hot path. If the library is missing, or was built for
+another architecture, every entry point raises instead of computing something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(os.environ.get("CTR_HIP_LIB", Path(__file__).resolve().parent / "libctr_hip.so"))
+
+CTR_OK = 0
+CTR_IDX_I32, CTR_IDX_I64 = 0, 1
+CTR_EFLAG_INDEX = 1
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RELU_DROP, EPI_GRAD_MASK = range(5)
+
+_vp, _i32, _i64, _f32, _f64, _u64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_double, C.c_uint64
+
+
+class SparsePlan(C.Structure):
+    """Mirror of ``ctr_sparse_plan`` (include/ctr_hip.h)."""
+    _fields_ = [("S", _i64), ("sorted_slots", _vp), ("sorted_rows", _vp), ("pos_seg", _vp),
+                ("unique_rows", _vp), ("seg_offsets", _vp), ("num_unique", _vp)]
+
+
+_plan_p = C.POINTER(SparsePlan)
+
+# name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
+# against the header.
+SIGNATURES = {
+    "ctr_abi_version": (_i32, []),
+    "ctr_last_error": (C.c_char_p, []),
+    "ctr_device_count": (_i32, []),
+    "ctr_embedding_gather": (_i32, [_vp, _i64, _i32, _vp, _i32, _i64, _vp, _vp, _vp]),
+    "ctr_fm_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                              _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
+    "ctr_bce_sigmoid": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp, _vp]),
+    "ctr_deepfm_head": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,
+                               _vp, _vp, _vp]),
+    "ctr_gemm_f32_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
+    "ctr_gemm_f32": (_i32, [_i32, _i32, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i32,
+                            _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _i64, _vp]),
+    "ctr_reduce_workspace_bytes": (_i64, [_i64, _i64]),
+    "ctr_sum_f32": (_i32, [_vp, _i64, _f32, _vp, _vp, _i64, _vp]),
+    "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),
+    "ctr_sparse_plan_workspace_bytes": (_i64, [_i64, _i64]),
+    "ctr_sparse_plan_build": (_i32, [_vp, _i32, _i64, _plan_p, _vp, _i64, _vp, _vp]),
+    "ctr_segment_workspace_bytes": (_i64, [_i64, _i32]),
+    "ctr_fm_embedding_grad": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _i64, _vp]),
+    "ctr_segment_sum_rows": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "ctr_rows_to_dense": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "ctr_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _f64, _f64, _f64, _f64, _vp]),
+    "ctr_adam_embedding": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _f64,
+                                  _f64, _f64, _f64, _f64, _f64, _vp]),
+    "ctr_feature_embedding_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp,
+                                             _vp]),
+    "ctr_softmax_rows": (_i32, [_vp, _i64, _i32, _vp, _vp]),
+    "ctr_pg_workspace_bytes": (_i64, [_i64]),
+    "ctr_pg_discount_norm": (_i32, [_vp, _i64, _f64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "ctr_pg_loss_grad": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp, _vp, _i64, _vp]),
+}
+
+
+class CtrHipError(RuntimeError):
+    pass
+
+
+class _Lib:
+    """Lazily loaded handle; attribute access returns a checked wrapper."""
+
+    def __init__(self) -> None:
+        self._dll = None
+
+    def load(self) -> C.CDLL:
+        if self._dll is None:
+            if not LIB_PATH.exists():
+                raise CtrHipError(
+                    f"{LIB_PATH} not found: build it with `python -m rl_ctr_prediction_amd.build_lib` "
+                    "(hipcc, gfx950). There is no CPU fallback for the HIP hot path.")
+            dll = C.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(dll, name)
+                fn.restype = res
+                fn.argtypes = args
+            self._dll = dll
+        return self._dll
+
+    def raw(self, name: str):
+        return getattr(self.load(), name)
+
+    def __getattr__(self, name: str):
+        if not name.startswith("ctr_"):
+            raise AttributeError(name)
+        fn = self.raw(name)
+        res = SIGNATURES[name][0]
+        if res is not _i32 or name in ("ctr_abi_version", "ctr_device_count"):
+            return fn
+
+        def checked(*args):
+            rc = fn(*args)
+            if rc != CTR_OK:
+                msg = self.load().ctr_last_error().decode(errors="replace")
+                raise CtrHipError(f"{name} failed (status {rc}): {msg}")
+            return rc
+
+        checked.__name__ = name
+        return checked
+
+
+lib = _Lib()
+
+
+def exported_symbols() -> list[str]:
+    """Names of every C-ABI entry point (used by the CPU test of the library)."""
+    return list(SIGNATURES)

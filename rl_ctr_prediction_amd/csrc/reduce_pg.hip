@@ -1,0 +1,293 @@
+// Deterministic reductions (loss mean, bias / 1-row-Linear gradients) and the REINFORCE
+// kernels of PG_model.PolicyGradient.
+//
+// Every reduction here has a fixed, size-determined order (grid sizes depend only on the
+// problem size; partials are added in block order), so results are identical bits run to
+// run and on every data-parallel rank.
+#include "ctr_common.h"
+
+namespace ctr {
+
+constexpr int kSumBlocks = 256;  // stage-1 blocks of ctr_sum_f32 (fixed => deterministic)
+
+__device__ __forceinline__ float block_sum_256(float v, float* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0) r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();
+  return r;  // valid in thread 0
+}
+
+__global__ __launch_bounds__(256) void sum_stage1(const float* __restrict__ x, int64_t n,
+                                                  int64_t per_block, float* __restrict__ part) {
+  __shared__ float sh[4];
+  const int64_t lo = blockIdx.x * per_block;
+  const int64_t hi = min(n, lo + per_block);
+  float acc = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += x[i];
+  const float r = block_sum_256(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(256) void sum_stage2(const float* __restrict__ part, int nparts,
+                                                  float scale, float* __restrict__ out) {
+  __shared__ float sh[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  const float r = block_sum_256(acc, sh);
+  if (threadIdx.x == 0) out[0] = r * scale;
+}
+
+// colsum: grid (ceil(N/64), RS); block = 64 columns x 4 row lanes.
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X, int64_t M,
+                                                     int64_t N, int64_t ldx,
+                                                     const float* __restrict__ w,
+                                                     int64_t rows_per_split,
+                                                     float* __restrict__ part) {
+  __shared__ float sh[4][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + cx;
+  const int64_t lo = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t hi = min(M, lo + rows_per_split);
+  float acc = 0.f;
+  if (n < N)
+    for (int64_t m = lo + ry; m < hi; m += 4) acc += (w ? w[m] * X[m * ldx + n] : X[m * ldx + n]);
+  sh[ry][cx] = acc;
+  __syncthreads();
+  if (ry == 0 && n < N) part[blockIdx.y * N + n] = (sh[0][cx] + sh[1][cx]) + (sh[2][cx] + sh[3][cx]);
+}
+
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int rs,
+                                                     int64_t N, float scale,
+                                                     float* __restrict__ out) {
+  for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
+       n += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < rs; ++r) s += part[(int64_t)r * N + n];
+    out[n] = s * scale;
+  }
+}
+
+static int colsum_splits(int64_t M) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 256), 64));
+}
+
+// ----------------------------------------------------------------- REINFORCE --------
+// torch.softmax(x, dim=1) for narrow rows (A = number of actions).
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ x, int64_t B,
+                                                           int A, float* __restrict__ out) {
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < B;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    const float* xb = x + b * A;
+    float mx = xb[0];
+    for (int j = 1; j < A; ++j) mx = fmaxf(mx, xb[j]);
+    float s = 0.f;
+    for (int j = 0; j < A; ++j) s += expf(xb[j] - mx);
+    for (int j = 0; j < A; ++j) out[b * A + j] = expf(xb[j] - mx) / s;
+  }
+}
+
+// PG_model.discount_and_norm_rewards (139-154), fp64 like the reference's numpy buffer:
+// d[i] = r[i] + gamma*d[i+1] (reverse), then d -= mean(d); d /= std(d) (population).
+// One block of 1024 threads: each thread owns a contiguous chunk; chunk affine maps are
+// chained from the right by thread 0 (<= 1024 fp64 FMAs), then each chunk is re-walked.
+__global__ __launch_bounds__(1024) void pg_discount_norm_kernel(const float* __restrict__ r,
+                                                                int64_t n, double gamma,
+                                                                double* __restrict__ out,
+                                                                float* __restrict__ out_f32,
+                                                                double* __restrict__ stats) {
+  __shared__ double s_sum[1024];
+  __shared__ double s_pow[1024];
+  __shared__ double s_red[16];
+  const int t = threadIdx.x, T = blockDim.x;
+  const int64_t cs = (n + T - 1) / T;
+  const int64_t lo = min(n, (int64_t)t * cs), hi = min(n, lo + cs);
+  double acc = 0.0, pw = 1.0;
+  for (int64_t i = hi - 1; i >= lo; --i) {
+    acc = acc * gamma + (double)r[i];
+    pw *= gamma;
+  }
+  s_sum[t] = acc;
+  s_pow[t] = pw;
+  __syncthreads();
+  if (t == 0) {  // carry[t] = value of d at position hi(t) (start of the next chunk)
+    double carry = 0.0;
+    for (int j = T - 1; j >= 0; --j) {
+      const double c_in = carry;
+      carry = s_sum[j] + s_pow[j] * carry;
+      s_sum[j] = c_in;
+    }
+  }
+  __syncthreads();
+  double run = s_sum[t];
+  double part = 0.0;
+  for (int64_t i = hi - 1; i >= lo; --i) {
+    run = run * gamma + (double)r[i];
+    out[i] = run;
+    part += run;
+  }
+  // mean
+  auto block_sum = [&](double v) -> double {
+    v = wave_sum_f64(v);
+    if ((t & 63) == 0) s_red[t >> 6] = v;
+    __syncthreads();
+    double tot = 0.0;
+    for (int w = 0; w < T / 64; ++w) tot += s_red[w];
+    __syncthreads();
+    return tot;
+  };
+  const double mean = block_sum(part) / (double)n;
+  double part2 = 0.0;
+  for (int64_t i = lo; i < hi; ++i) {
+    out[i] -= mean;
+    part2 += out[i];
+  }
+  // np.std of the centred buffer: its own mean, then sqrt(mean(|x - mean|^2))
+  const double mean2 = block_sum(part2) / (double)n;
+  double part3 = 0.0;
+  for (int64_t i = lo; i < hi; ++i) {
+    const double dv = out[i] - mean2;
+    part3 += dv * dv;
+  }
+  const double stdv = sqrt(block_sum(part3) / (double)n);
+  for (int64_t i = lo; i < hi; ++i) {
+    out[i] /= stdv;
+    if (out_f32) out_f32[i] = (float)out[i];
+  }
+  if (t == 0 && stats) {
+    stats[0] = mean;
+    stats[1] = stdv;
+  }
+}
+
+// PG_model.loss_func (104-107) + autograd through gather/log/softmax, one block:
+//   nlp = sum_b -log(p[b, a_b - 1]);  loss = mean(nlp * vt) ;
+//   c = d loss / d nlp = sum_i vt_i / n;  g[b,a] = -c / p[b,a];
+//   dlogit[b,j] = p[b,j] * (g[b,j] - g[b,a] * p[b,a])     (softmax backward)
+__global__ __launch_bounds__(1024) void pg_loss_grad_kernel(const float* __restrict__ p,
+                                                            const int64_t* __restrict__ acts,
+                                                            const float* __restrict__ vt,
+                                                            int64_t B, int A, float grad_scale,
+                                                            float* __restrict__ loss_out,
+                                                            float* __restrict__ dlogits) {
+  __shared__ float s_red[16];
+  const int t = threadIdx.x, T = blockDim.x;
+  auto block_sum = [&](float v) -> float {
+    v = wave_sum(v);
+    if ((t & 63) == 0) s_red[t >> 6] = v;
+    __syncthreads();
+    float tot = 0.f;
+    for (int w = 0; w < T / 64; ++w) tot += s_red[w];
+    __syncthreads();
+    return tot;
+  };
+  float nl = 0.f, sv = 0.f;
+  for (int64_t b = t; b < B; b += T) {
+    int64_t a = acts[b] - 1;
+    a = a < 0 ? 0 : (a >= A ? A - 1 : a);
+    nl += -logf(p[b * A + a]);
+    sv += vt[b];
+  }
+  const float nlp = block_sum(nl);
+  const float svt = block_sum(sv);
+  float lv = 0.f;
+  for (int64_t b = t; b < B; b += T) lv += nlp * vt[b];
+  const float loss = block_sum(lv) / (float)B;
+  if (t == 0 && loss_out) loss_out[0] = loss;
+  const float c = (svt / (float)B) * grad_scale;
+  if (!dlogits) return;
+  for (int64_t b = t; b < B; b += T) {
+    int64_t a = acts[b] - 1;
+    a = a < 0 ? 0 : (a >= A ? A - 1 : a);
+    const float pa = p[b * A + a];
+    const float ga = -c / pa;
+    const float dot = ga * pa;
+    for (int j = 0; j < A; ++j) {
+      const float gj = (j == a) ? ga : 0.f;
+      dlogits[b * A + j] = p[b * A + j] * (gj - dot);
+    }
+  }
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int64_t ctr_reduce_workspace_bytes(int64_t M, int64_t N) {
+  if (M < 0 || N < 0) return -1;
+  const int64_t a = (int64_t)kSumBlocks * 4;
+  const int64_t b = (int64_t)colsum_splits(M) * std::max<int64_t>(N, 1) * 4;
+  return align_up(std::max(a, b), 256);
+}
+
+extern "C" int ctr_sum_f32(const float* x, int64_t n, float scale, float* out, void* ws,
+                           int64_t ws_bytes, ctr_stream_t stream) {
+  CTR_REQUIRE(out && n >= 0 && (x || n == 0), "ctr_sum_f32: bad arguments");
+  CTR_REQUIRE(ws && ws_bytes >= (int64_t)kSumBlocks * 4, "ctr_sum_f32: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int64_t per = std::max<int64_t>(1, ceil_div(n, kSumBlocks));
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(sum_stage1, kSumBlocks, 256, 0, st, x, n, per, part);
+  CTR_LAUNCH_CHECK("sum_stage1");
+  hipLaunchKernelGGL(sum_stage2, 1, 256, 0, st, part, kSumBlocks, scale, out);
+  CTR_LAUNCH_CHECK("sum_stage2");
+  return CTR_OK;
+}
+
+extern "C" int ctr_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, const float* row_w,
+                              float scale, float* out, void* ws, int64_t ws_bytes,
+                              ctr_stream_t stream) {
+  CTR_REQUIRE(M >= 0 && N >= 0 && ldx >= N, "ctr_colsum_f32: bad sizes");
+  if (N == 0) return CTR_OK;
+  CTR_REQUIRE(out && (X || M == 0), "ctr_colsum_f32: null pointer");
+  const int rs = colsum_splits(M);
+  CTR_REQUIRE(ws && ws_bytes >= (int64_t)rs * N * 4, "ctr_colsum_f32: workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(ws);
+  const int64_t rps = std::max<int64_t>(1, ceil_div(M, rs));
+  hipLaunchKernelGGL(colsum_stage1, dim3((unsigned)ceil_div(N, 64), (unsigned)rs), 256, 0, st, X,
+                     M, N, ldx, row_w, rps, part);
+  CTR_LAUNCH_CHECK("colsum_stage1");
+  hipLaunchKernelGGL(colsum_stage2, (unsigned)std::min<int64_t>(ceil_div(N, 256), 1024), 256, 0,
+                     st, part, rs, N, scale, out);
+  CTR_LAUNCH_CHECK("colsum_stage2");
+  return CTR_OK;
+}
+
+extern "C" int ctr_softmax_rows(const float* x, int64_t B, int A, float* out, ctr_stream_t stream) {
+  CTR_REQUIRE(B >= 0 && A > 0 && (B == 0 || (x && out)), "ctr_softmax_rows: bad arguments");
+  if (B == 0) return CTR_OK;
+  hipLaunchKernelGGL(softmax_rows_kernel, (unsigned)std::min<int64_t>(ceil_div(B, 256), 4096), 256,
+                     0, as_stream(stream), x, B, A, out);
+  CTR_LAUNCH_CHECK("ctr_softmax_rows");
+  return CTR_OK;
+}
+
+extern "C" int64_t ctr_pg_workspace_bytes(int64_t n) { return n < 0 ? -1 : 0; }
+
+extern "C" int ctr_pg_discount_norm(const float* r, int64_t n, double gamma, double* out,
+                                    float* out_f32, double* stats, void* ws, int64_t ws_bytes,
+                                    ctr_stream_t stream) {
+  (void)ws;
+  (void)ws_bytes;
+  CTR_REQUIRE(n > 0 && r && out, "ctr_pg_discount_norm: bad arguments");
+  hipLaunchKernelGGL(pg_discount_norm_kernel, 1, 1024, 0, as_stream(stream), r, n, gamma, out,
+                     out_f32, stats);
+  CTR_LAUNCH_CHECK("ctr_pg_discount_norm");
+  return CTR_OK;
+}
+
+extern "C" int ctr_pg_loss_grad(const float* probs, const int64_t* acts, const float* vt,
+                                int64_t B, int A, float grad_scale, float* loss_out,
+                                float* dlogits, void* ws, int64_t ws_bytes, ctr_stream_t stream) {
+  (void)ws;
+  (void)ws_bytes;
+  CTR_REQUIRE(B > 0 && A > 0 && probs && acts && vt, "ctr_pg_loss_grad: bad arguments");
+  hipLaunchKernelGGL(pg_loss_grad_kernel, 1, 1024, 0, as_stream(stream), probs, acts, vt, B, A,
+                     grad_scale, loss_out, dlogits);
+  CTR_LAUNCH_CHECK("ctr_pg_loss_grad");
+  return CTR_OK;
+}

@@ -1,0 +1,489 @@
+// Embedding scatter-add of the CTR hot path, deterministic.
+//
+// The reference's autograd writes a DENSE [V,K] gradient (embedding_dense_backward
+// accumulates the slots of each row in slot order). Here a batch's S = B*F slots are
+// grouped once per step into a sparse plan — a stable radix sort of (row, slot) pairs,
+// then segment heads and a scan — and each row's contributions are summed in slot order.
+// Hot rows (Zipf ids: one row can own >1000 slots of a batch) are split into fixed
+// 16-position chunks so every lane group does equal work; chunk partials of rows that
+// span chunks are added in chunk order by a second pass. No float atomics anywhere: the
+// result is bitwise reproducible, which is what keeps data-parallel replicas identical.
+#include <hipcub/hipcub.hpp>
+
+#include "ctr_common.h"
+
+namespace ctr {
+
+constexpr int kChunk = 16;  // sorted positions per lane group (SEG_L)
+
+// --------------------------------------------------------------- plan kernels -------
+template <typename IdxT>
+__global__ __launch_bounds__(256) void plan_keys_kernel(const IdxT* __restrict__ idx, int64_t S,
+                                                        int64_t V, uint32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ vals, int32_t* err) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    keys[s] = (uint32_t)load_row(idx, s, V, err);
+    vals[s] = (int32_t)s;
+  }
+}
+
+__global__ __launch_bounds__(256) void plan_heads_kernel(const int32_t* __restrict__ rows,
+                                                         int64_t S, int32_t* __restrict__ heads) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x)
+    heads[s] = (s == 0 || rows[s] != rows[s - 1]) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void plan_scatter_kernel(const int32_t* __restrict__ rows,
+                                                           int64_t S, int32_t* __restrict__ pos_seg,
+                                                           int32_t* __restrict__ unique_rows,
+                                                           int32_t* __restrict__ seg_offsets,
+                                                           int32_t* __restrict__ num_unique) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = pos_seg[s] - 1;  // inclusive scan of heads -> ordinal
+    pos_seg[s] = u;
+    if (s == 0 || rows[s] != rows[s - 1]) {
+      unique_rows[u] = rows[s];
+      seg_offsets[u] = (int32_t)s;
+    }
+    if (s == S - 1) {
+      *num_unique = u + 1;
+      seg_offsets[u + 1] = (int32_t)S;
+    }
+  }
+}
+
+struct PlanWs {
+  uint32_t* keys_in;
+  int32_t* vals_in;
+  int32_t* heads;
+  void* temp;
+  size_t temp_bytes;
+  size_t total;
+};
+
+static int plan_ws_layout(int64_t S, int end_bit, hipStream_t st, char* base, PlanWs* w) {
+  size_t sort_bytes = 0, scan_bytes = 0;
+  const int n = (int)S;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, (const int32_t*)nullptr,
+                                         (int32_t*)nullptr, n, 0, end_bit, st) != hipSuccess) {
+    set_error("hipcub SortPairs size query failed");
+    return CTR_ERR_HIP;
+  }
+  if (hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const int32_t*)nullptr,
+                                       (int32_t*)nullptr, n, st) != hipSuccess) {
+    set_error("hipcub InclusiveSum size query failed");
+    return CTR_ERR_HIP;
+  }
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (size_t)align_up((int64_t)bytes, 256);
+    return o;
+  };
+  const size_t o_keys = take(sizeof(uint32_t) * S);
+  const size_t o_vals = take(sizeof(int32_t) * S);
+  const size_t o_heads = take(sizeof(int32_t) * S);
+  w->temp_bytes = std::max(sort_bytes, scan_bytes);
+  const size_t o_temp = take(w->temp_bytes);
+  w->total = off;
+  w->keys_in = reinterpret_cast<uint32_t*>(base + o_keys);
+  w->vals_in = reinterpret_cast<int32_t*>(base + o_vals);
+  w->heads = reinterpret_cast<int32_t*>(base + o_heads);
+  w->temp = base + o_temp;
+  return CTR_OK;
+}
+
+static int key_bits(int64_t V) {
+  int bits = 1;
+  while (bits < 32 && (int64_t(1) << bits) < V) ++bits;
+  return bits;
+}
+
+// ------------------------------------------------------- segmented row sums ----------
+// Vector width VT (float4 when K % 4 == 0, else float), KV = K / width columns, LPR lanes
+// per row (power of two >= KV), one lane group per chunk of kChunk sorted positions.
+template <typename VT>
+struct VOps;
+template <>
+struct VOps<float> {
+  __device__ static float zero() { return 0.f; }
+  __device__ static void add(float& a, float b) { a += b; }
+  // (g*s - g*e) + d, each product rounded (the reference's two autograd terms)
+  __device__ static float fm(float g, float s, float e, float d) {
+#pragma clang fp contract(off)
+    return (g * s - g * e) + d;
+  }
+};
+template <>
+struct VOps<float4> {
+  __device__ static float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ static void add(float4& a, float4 b) {
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  __device__ static float4 fm(float g, float4 s, float4 e, float4 d) {
+    return make_float4(VOps<float>::fm(g, s.x, e.x, d.x), VOps<float>::fm(g, s.y, e.y, d.y),
+                       VOps<float>::fm(g, s.z, e.z, d.z), VOps<float>::fm(g, s.w, e.w, d.w));
+  }
+};
+
+struct SegArgs {
+  int64_t S;
+  int KV;
+  const int32_t* sorted_slots;
+  const int32_t* sorted_rows;
+  const int32_t* pos_seg;
+  const int32_t* unique_rows;
+  const int32_t* seg_offsets;
+  const int32_t* num_unique;
+  // FM contribution (MODE_FM)
+  int F;
+  const float* gz;
+  const void* sum_e;
+  const void* dx;
+  const void* emb;
+  // generic contribution (MODE_VALS)
+  const void* vals;
+  const float* vals_lin;
+  // outputs
+  void* out;
+  float* out_lin;
+  int32_t* rowmap;
+  void* part;       // [n_chunks, 2, KV]  chunk partials: [0] run holding the chunk's first
+  float* part_lin;  // [n_chunks, 2]      position, [1] the chunk's last (open) run
+};
+
+enum { MODE_FM = 0, MODE_VALS = 1 };
+
+template <typename VT, int LPR, int MODE>
+__global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
+  const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR;
+  const int c = threadIdx.x % LPR;
+  const int64_t start = gid * kChunk;
+  if (start >= a.S) return;
+  const bool col = c < a.KV;
+  const int n = (int)min<int64_t>(kChunk, a.S - start);
+
+  // Stage every load of the chunk first (ILP), then walk the runs in slot order.
+  int seg[kChunk];
+  VT val[kChunk];
+  float gl[kChunk];
+#pragma unroll
+  for (int i = 0; i < kChunk; ++i) {
+    seg[i] = -1;
+    val[i] = VOps<VT>::zero();
+    gl[i] = 0.f;
+    if (i < n) {
+      const int64_t pos = start + i;
+      const int32_t slot = a.sorted_slots[pos];
+      seg[i] = a.pos_seg[pos];
+      if (MODE == MODE_FM) {
+        const int64_t b = slot / a.F;
+        const float g = a.gz[b];
+        gl[i] = g;
+        if (col) {
+          const int32_t row = a.sorted_rows[pos];
+          const VT s = static_cast<const VT*>(a.sum_e)[b * a.KV + c];
+          const VT e = static_cast<const VT*>(a.emb)[(int64_t)row * a.KV + c];
+          const VT d = a.dx ? static_cast<const VT*>(a.dx)[(int64_t)slot * a.KV + c]
+                            : VOps<VT>::zero();
+          val[i] = VOps<VT>::fm(g, s, e, d);
+        }
+      } else {
+        if (a.vals_lin) gl[i] = a.vals_lin[slot];
+        if (col) val[i] = static_cast<const VT*>(a.vals)[(int64_t)slot * a.KV + c];
+      }
+    }
+  }
+
+  auto flush = [&](int u, const VT& acc, float accl, bool first_run) {
+    const int32_t off0 = a.seg_offsets[u];
+    const int32_t off1 = a.seg_offsets[u + 1];
+    if (off0 / kChunk == (off1 - 1) / kChunk) {  // whole row inside this chunk: final
+      if (col) static_cast<VT*>(a.out)[(int64_t)u * a.KV + c] = acc;
+      if (c == 0) {
+        if (a.out_lin) a.out_lin[u] = accl;
+        if (a.rowmap) a.rowmap[a.unique_rows[u]] = u;
+      }
+    } else {
+      const int64_t k = gid * 2 + (first_run ? 0 : 1);
+      if (col) static_cast<VT*>(a.part)[k * a.KV + c] = acc;
+      if (c == 0) a.part_lin[k] = accl;
+    }
+  };
+
+  VT acc = VOps<VT>::zero();
+  float accl = 0.f;
+  int cur = seg[0];
+  bool first_run = true;
+#pragma unroll
+  for (int i = 0; i < kChunk; ++i) {
+    if (i < n) {
+      if (seg[i] != cur) {
+        flush(cur, acc, accl, first_run);
+        acc = VOps<VT>::zero();
+        accl = 0.f;
+        cur = seg[i];
+        first_run = false;
+      }
+      VOps<VT>::add(acc, val[i]);
+      accl += gl[i];
+    }
+  }
+  flush(cur, acc, accl, first_run);
+}
+
+// Rows that span chunks: head partial of the first chunk (slot [0] if the row starts the
+// chunk, else [1]), whole middle chunks ([0]), the last chunk's head partial ([0]).
+template <typename VT, int LPR>
+__global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
+  const int c = threadIdx.x % LPR;
+  const bool col = c < a.KV;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / LPR);
+  const int U = *a.num_unique;
+  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR; u < U; u += groups) {
+    const int32_t off0 = a.seg_offsets[u];
+    const int32_t off1 = a.seg_offsets[u + 1];
+    const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
+    if (fs == ls) continue;
+    const int64_t k0 = fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1);
+    VT acc = col ? static_cast<const VT*>(a.part)[k0 * a.KV + c] : VOps<VT>::zero();
+    float accl = a.part_lin[k0];
+    for (int64_t j = fs + 1; j <= ls; ++j) {
+      if (col) VOps<VT>::add(acc, static_cast<const VT*>(a.part)[(j * 2) * a.KV + c]);
+      accl += a.part_lin[j * 2];
+    }
+    if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
+    if (c == 0) {
+      if (a.out_lin) a.out_lin[u] = accl;
+      if (a.rowmap) a.rowmap[a.unique_rows[u]] = (int32_t)u;
+    }
+  }
+}
+
+template <typename VT, int LPR>
+static int launch_seg_lpr(SegArgs& a, int mode, hipStream_t st) {
+  const int64_t n_chunks = ceil_div(a.S, kChunk);
+  const int groups_per_block = 256 / LPR;
+  const unsigned g1 = (unsigned)ceil_div(n_chunks, groups_per_block);
+  if (mode == MODE_FM)
+    hipLaunchKernelGGL((seg_chunk_kernel<VT, LPR, MODE_FM>), g1, 256, 0, st, a);
+  else
+    hipLaunchKernelGGL((seg_chunk_kernel<VT, LPR, MODE_VALS>), g1, 256, 0, st, a);
+  CTR_LAUNCH_CHECK("seg_chunk_kernel");
+  const unsigned g2 = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(ceil_div(n_chunks, groups_per_block), 1024));
+  hipLaunchKernelGGL((seg_combine_kernel<VT, LPR>), g2, 256, 0, st, a);
+  CTR_LAUNCH_CHECK("seg_combine_kernel");
+  return CTR_OK;
+}
+
+static int pow2_at_least(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+static int launch_seg(SegArgs& a, int K, int mode, hipStream_t st, bool aligned16) {
+  const bool vec = (K % 4 == 0) && aligned16 && K / 4 <= 64;
+  const int KV = vec ? K / 4 : K;
+  a.KV = KV;
+  const int lpr = pow2_at_least(KV);
+  if (vec) {
+    switch (lpr) {
+      case 1: return launch_seg_lpr<float4, 1>(a, mode, st);
+      case 2: return launch_seg_lpr<float4, 2>(a, mode, st);
+      case 4: return launch_seg_lpr<float4, 4>(a, mode, st);
+      case 8: return launch_seg_lpr<float4, 8>(a, mode, st);
+      case 16: return launch_seg_lpr<float4, 16>(a, mode, st);
+      case 32: return launch_seg_lpr<float4, 32>(a, mode, st);
+      case 64: return launch_seg_lpr<float4, 64>(a, mode, st);
+    }
+  } else {
+    switch (lpr) {
+      case 1: return launch_seg_lpr<float, 1>(a, mode, st);
+      case 2: return launch_seg_lpr<float, 2>(a, mode, st);
+      case 4: return launch_seg_lpr<float, 4>(a, mode, st);
+      case 8: return launch_seg_lpr<float, 8>(a, mode, st);
+      case 16: return launch_seg_lpr<float, 16>(a, mode, st);
+      case 32: return launch_seg_lpr<float, 32>(a, mode, st);
+      case 64: return launch_seg_lpr<float, 64>(a, mode, st);
+    }
+  }
+  set_error("segmented row sum: K=%d unsupported (K<=64, or K%%4==0 and K<=256)", K);
+  return CTR_ERR_UNSUPPORTED;
+}
+
+static int64_t seg_ws_bytes(int64_t S, int K) {
+  const int64_t n_chunks = ceil_div(S, kChunk);
+  return align_up(n_chunks * 2 * (int64_t)K * 4, 256) + align_up(n_chunks * 2 * 4, 256);
+}
+
+// ------------------------------------------------------------------ to dense -------
+__global__ __launch_bounds__(256) void rows_to_dense_kernel(const int32_t* __restrict__ unique_rows,
+                                                            const int32_t* __restrict__ num_unique,
+                                                            int K, const float* __restrict__ grad,
+                                                            const float* __restrict__ grad_lin,
+                                                            float* __restrict__ dense,
+                                                            float* __restrict__ dense_lin) {
+  const int64_t U = *num_unique;
+  const int64_t total = U * K;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = t / K;
+    const int k = (int)(t - u * K);
+    const int64_t row = unique_rows[u];
+    dense[row * K + k] = grad[t];
+    if (k == 0 && dense_lin && grad_lin) dense_lin[row] = grad_lin[u];
+  }
+}
+
+static bool plan_ok(const ctr_sparse_plan* p) {
+  return p && p->S >= 0 && p->sorted_slots && p->sorted_rows && p->pos_seg && p->unique_rows &&
+         p->seg_offsets && p->num_unique;
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int64_t ctr_sparse_plan_workspace_bytes(int64_t S, int64_t V) {
+  if (S < 0 || V <= 0 || S >= (int64_t(1) << 31)) {
+    set_error("ctr_sparse_plan_workspace_bytes: bad sizes");
+    return -1;
+  }
+  PlanWs w;
+  if (plan_ws_layout(std::max<int64_t>(S, 1), key_bits(V), 0, nullptr, &w) != CTR_OK) return -1;
+  return (int64_t)w.total;
+}
+
+extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
+                                     const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,
+                                     int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_sparse_plan_build: incomplete plan");
+  CTR_REQUIRE(idx || plan->S == 0, "ctr_sparse_plan_build: null idx");
+  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && plan->S < (int64_t(1) << 31),
+              "ctr_sparse_plan_build: bad sizes");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  hipStream_t st = as_stream(stream);
+  const int64_t S = plan->S;
+  if (S == 0) {
+    CTR_HIP_CHECK(hipMemsetAsync(plan->num_unique, 0, sizeof(int32_t), st));
+    CTR_HIP_CHECK(hipMemsetAsync(plan->seg_offsets, 0, sizeof(int32_t), st));
+    return CTR_OK;
+  }
+  const int bits = key_bits(V);
+  PlanWs w;
+  int rc = plan_ws_layout(S, bits, st, static_cast<char*>(ws), &w);
+  if (rc != CTR_OK) return rc;
+  if (!ws || ws_bytes < (int64_t)w.total) {
+    set_error("ctr_sparse_plan_build: workspace %lld < %lld bytes", (long long)ws_bytes,
+              (long long)w.total);
+    return CTR_ERR_WORKSPACE;
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(S, 256), 4096);
+  if (idx_type == CTR_IDX_I64)
+    hipLaunchKernelGGL(plan_keys_kernel<int64_t>, grid, 256, 0, st,
+                       static_cast<const int64_t*>(idx), S, V, w.keys_in, w.vals_in, err_flag);
+  else
+    hipLaunchKernelGGL(plan_keys_kernel<int32_t>, grid, 256, 0, st,
+                       static_cast<const int32_t*>(idx), S, V, w.keys_in, w.vals_in, err_flag);
+  CTR_LAUNCH_CHECK("plan_keys_kernel");
+  size_t tb = w.temp_bytes;
+  CTR_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(
+      w.temp, tb, (const uint32_t*)w.keys_in, reinterpret_cast<uint32_t*>(plan->sorted_rows),
+      (const int32_t*)w.vals_in, plan->sorted_slots, (int)S, 0, bits, st));
+  hipLaunchKernelGGL(plan_heads_kernel, grid, 256, 0, st, plan->sorted_rows, S, w.heads);
+  CTR_LAUNCH_CHECK("plan_heads_kernel");
+  tb = w.temp_bytes;
+  CTR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(w.temp, tb, (const int32_t*)w.heads,
+                                                 plan->pos_seg, (int)S, st));
+  hipLaunchKernelGGL(plan_scatter_kernel, grid, 256, 0, st, plan->sorted_rows, S, plan->pos_seg,
+                     plan->unique_rows, plan->seg_offsets, plan->num_unique);
+  CTR_LAUNCH_CHECK("plan_scatter_kernel");
+  return CTR_OK;
+}
+
+extern "C" int64_t ctr_segment_workspace_bytes(int64_t S, int K) {
+  if (S < 0 || K <= 0) return -1;
+  return seg_ws_bytes(S, K);
+}
+
+static int seg_prepare(SegArgs& a, const ctr_sparse_plan* plan, int K, void* out, float* out_lin,
+                       int32_t* rowmap, void* ws, int64_t ws_bytes) {
+  memset(&a, 0, sizeof(a));
+  a.S = plan->S;
+  a.sorted_slots = plan->sorted_slots;
+  a.sorted_rows = plan->sorted_rows;
+  a.pos_seg = plan->pos_seg;
+  a.unique_rows = plan->unique_rows;
+  a.seg_offsets = plan->seg_offsets;
+  a.num_unique = plan->num_unique;
+  a.out = out;
+  a.out_lin = out_lin;
+  a.rowmap = rowmap;
+  const int64_t need = seg_ws_bytes(plan->S, K);
+  if (!ws || ws_bytes < need) {
+    set_error("segmented row sum: workspace %lld < %lld bytes", (long long)ws_bytes,
+              (long long)need);
+    return CTR_ERR_WORKSPACE;
+  }
+  const int64_t n_chunks = ceil_div(plan->S, kChunk);
+  a.part = ws;
+  a.part_lin = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                        align_up(n_chunks * 2 * (int64_t)K * 4, 256));
+  return CTR_OK;
+}
+
+extern "C" int ctr_fm_embedding_grad(const ctr_sparse_plan* plan, int F, int K, const float* emb,
+                                     const float* gz, const float* sum_e, const float* dx,
+                                     float* grad_rows, float* grad_lin, int32_t* rowmap, void* ws,
+                                     int64_t ws_bytes, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_fm_embedding_grad: incomplete plan");
+  CTR_REQUIRE(F > 0 && K > 0, "ctr_fm_embedding_grad: bad sizes");
+  CTR_REQUIRE(emb && gz && sum_e && grad_rows && grad_lin, "ctr_fm_embedding_grad: null pointer");
+  if (plan->S == 0) return CTR_OK;
+  SegArgs a;
+  int rc = seg_prepare(a, plan, K, grad_rows, grad_lin, rowmap, ws, ws_bytes);
+  if (rc != CTR_OK) return rc;
+  a.F = F;
+  a.gz = gz;
+  a.sum_e = sum_e;
+  a.dx = dx;
+  a.emb = emb;
+  const bool al = ((uintptr_t)emb | (uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)grad_rows |
+                   (uintptr_t)ws) % 16 == 0;
+  return launch_seg(a, K, MODE_FM, as_stream(stream), al);
+}
+
+extern "C" int ctr_segment_sum_rows(const ctr_sparse_plan* plan, int K, const float* vals,
+                                    const float* vals_lin, float* out, float* out_lin,
+                                    int32_t* rowmap, void* ws, int64_t ws_bytes,
+                                    ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_segment_sum_rows: incomplete plan");
+  CTR_REQUIRE(K > 0 && vals && out, "ctr_segment_sum_rows: bad arguments");
+  CTR_REQUIRE(!vals_lin == !out_lin, "ctr_segment_sum_rows: vals_lin and out_lin go together");
+  if (plan->S == 0) return CTR_OK;
+  SegArgs a;
+  int rc = seg_prepare(a, plan, K, out, out_lin, rowmap, ws, ws_bytes);
+  if (rc != CTR_OK) return rc;
+  a.vals = vals;
+  a.vals_lin = vals_lin;
+  const bool al = ((uintptr_t)vals | (uintptr_t)out | (uintptr_t)ws) % 16 == 0;
+  return launch_seg(a, K, MODE_VALS, as_stream(stream), al);
+}
+
+extern "C" int ctr_rows_to_dense(const ctr_sparse_plan* plan, int K, const float* grad_rows,
+                                 const float* grad_lin, float* dense, float* dense_lin,
+                                 ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan) && K > 0 && grad_rows && dense, "ctr_rows_to_dense: bad arguments");
+  if (plan->S == 0) return CTR_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(plan->S * (int64_t)K, 256), 4096);
+  hipLaunchKernelGGL(rows_to_dense_kernel, grid, 256, 0, as_stream(stream), plan->unique_rows,
+                     plan->num_unique, K, grad_rows, grad_lin, dense, dense_lin);
+  CTR_LAUNCH_CHECK("ctr_rows_to_dense");
+  return CTR_OK;
+}

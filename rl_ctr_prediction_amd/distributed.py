@@ -1,0 +1,66 @@
+"""Data-parallel exchange for the CTR step: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on ROCm; "gloo" for the CPU tests).
+
+Examples are independent and the loss is a mean, so the global-batch gradient is a sum
+of per-rank gradients computed with the GLOBAL mean divisor:
+  * dense parameters (FM bias, DeepFM MLP: 0.56 M floats) live in one flat buffer ->
+    ONE all-reduce per step (latency-bound at 2.2 MB; a single bucket is optimal);
+  * embedding gradients are exchanged sparsely: each rank all-gathers every rank's
+    (unique row, row-sum) pairs and re-sums them by row in (rank, row) order with the
+    deterministic segmented sum, so every replica applies bit-identical dense Adam and
+    the replicated tables never diverge — no V x K all-reduce (2.6 GB at C3).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    if world()[1] > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def allgather_sparse_rows(rows: torch.Tensor, vals: torch.Tensor, lin: torch.Tensor | None,
+                          count: int, group=None):
+    """Concatenate every rank's first `count` (rows, vals, lin) entries in rank order.
+
+    rows [>=count] int32, vals [>=count, K] fp32, lin [>=count] fp32 (optional). Counts
+    differ per rank, so the payload is padded to the largest count for the collective
+    and the padding is dropped on receipt. Returns (rows_all, vals_all, lin_all).
+    """
+    rank, ws = world()
+    if ws == 1:
+        return rows[:count], vals[:count], None if lin is None else lin[:count]
+    dev = rows.device
+    cnt = torch.tensor([count], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(ws)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    cap = max(max(counts), 1)
+    K = vals.shape[1]
+    width = K + 1 if lin is not None else K  # [vals | lin]
+    send_rows = torch.zeros(cap, dtype=torch.int32, device=dev)
+    send_rows[:count] = rows[:count].to(torch.int32)
+    send = torch.zeros(cap, width, dtype=torch.float32, device=dev)
+    send[:count, :K] = vals[:count]
+    if lin is not None:
+        send[:count, K] = lin[:count]
+    recv_rows = torch.empty(ws * cap, dtype=torch.int32, device=dev)
+    recv = torch.empty(ws * cap, width, dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(recv_rows, send_rows, group=group)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    recv_rows = recv_rows.view(ws, cap)
+    recv = recv.view(ws, cap, width)
+    rows_all = torch.cat([recv_rows[r, :counts[r]] for r in range(ws)]).contiguous()
+    allp = torch.cat([recv[r, :counts[r]] for r in range(ws)], dim=0)
+    vals_all = allp[:, :K].contiguous()
+    lin_all = allp[:, K].contiguous() if lin is not None else None
+    return rows_all, vals_all, lin_all

@@ -1,0 +1,381 @@
+"""Tensor-level wrappers over the libctr_hip.so C ABI.
+
+PyTorch only provides device memory and the current HIP stream here; every computation
+is a kernel of libctr_hip.so. Inputs must already be on a ROCm device: a CPU tensor is
+an error, never a silent fallback.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
+                   EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, SparsePlan, lib)
+
+__all__ = [
+    "embedding_gather", "fm_forward", "bce_sigmoid", "deepfm_head", "gemm", "linear",
+    "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
+    "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
+    "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
+    "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
+]
+
+
+# ----------------------------------------------------------------------- plumbing ----
+def _dev(t: torch.Tensor, name: str = "tensor") -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} is on {t.device}: the HIP hot path needs ROCm device "
+                           "tensors (there is no CPU fallback)")
+    return t
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    _dev(t, name)
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _idx(t: torch.Tensor, name: str = "idx") -> tuple[torch.Tensor, int]:
+    _dev(t, name)
+    if t.dtype == torch.int64:
+        it = CTR_IDX_I64
+    elif t.dtype == torch.int32:
+        it = CTR_IDX_I32
+    else:
+        raise TypeError(f"{name}: feature ids must be int64 or int32, got {t.dtype}")
+    return t.contiguous(), it
+
+
+class Workspace:
+    """Grow-only scratch buffer, one per (device, stream); kernels on one stream are
+    ordered, so consecutive ops can share it."""
+
+    _pool: dict = {}
+
+    @classmethod
+    def get(cls, nbytes: int, device: torch.device) -> torch.Tensor | None:
+        if nbytes <= 0:
+            return None
+        key = (device.index, _stream())
+        buf = cls._pool.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            cls._pool[key] = buf
+        return buf
+
+
+def check_index_error(err_flag: torch.Tensor) -> None:
+    """Raise like nn.Embedding does when a kernel saw an id outside [0, V). Syncs."""
+    v = int(err_flag.item())
+    if v & CTR_EFLAG_INDEX:
+        err_flag.zero_()
+        raise IndexError("index out of range in self")
+
+
+# ------------------------------------------------------------------------ forward ----
+def embedding_gather(table: torch.Tensor, idx: torch.Tensor, err_flag=None) -> torch.Tensor:
+    _f32(table, "table")
+    idx, it = _idx(idx)
+    V, K = table.shape
+    out = torch.empty(*idx.shape, K, dtype=torch.float32, device=table.device)
+    lib.ctr_embedding_gather(_p(table), V, K, _p(idx), it, idx.numel(), _p(out), _p(err_flag),
+                             _stream())
+    return out
+
+
+@dataclass
+class FMForward:
+    z: torch.Tensor
+    sum_e: torch.Tensor | None
+    emb_out: torch.Tensor | None
+    p: torch.Tensor | None
+    loss_elem: torch.Tensor | None
+    gz: torch.Tensor | None
+
+
+def fm_forward(idx: torch.Tensor, emb: torch.Tensor, lin: torch.Tensor, bias: torch.Tensor, *,
+               want_sum: bool = True, want_emb: bool = False, labels: torch.Tensor | None = None,
+               mean_div: float | None = None, want_p: bool = True, err_flag=None,
+               out: FMForward | None = None) -> FMForward:
+    """Fused gather + FM second order + linear term (+ BCE head when labels are given)."""
+    idx, it = _idx(idx)
+    B, F = idx.shape
+    _f32(emb, "feature_embedding.weight")
+    _f32(lin, "linear.weight")
+    _f32(bias, "bias")
+    V, K = emb.shape
+    dev = emb.device
+    if out is None:
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        out = FMForward(z=e(B), sum_e=e(B, K) if want_sum else None,
+                        emb_out=e(B, F * K) if want_emb else None,
+                        p=e(B) if want_p else None,
+                        loss_elem=e(B) if labels is not None else None,
+                        gz=e(B) if labels is not None else None)
+    if labels is not None:
+        _f32(labels, "labels")
+        mean_div = float(B if mean_div is None else mean_div)
+    lib.ctr_fm_forward(_p(idx), it, B, F, K, V, _p(emb), _p(lin), _p(bias), _p(out.z),
+                       _p(out.sum_e), _p(out.emb_out), _p(labels), float(mean_div or 1.0),
+                       _p(out.p), _p(out.loss_elem), _p(out.gz), _p(err_flag), _stream())
+    return out
+
+
+def bce_sigmoid(z: torch.Tensor, labels: torch.Tensor, mean_div: float | None = None):
+    _f32(z, "z")
+    _f32(labels, "labels")
+    B = z.numel()
+    p, loss, gz = (torch.empty_like(z) for _ in range(3))
+    lib.ctr_bce_sigmoid(_p(z), _p(labels), B, float(B if mean_div is None else mean_div), _p(p),
+                        _p(loss), _p(gz), _stream())
+    return p, loss, gz
+
+
+def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.0, out=None):
+    _f32(h, "h")
+    B, H = h.shape
+    dev = h.device
+    if out is None:
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        out = dict(z=e(B), p=e(B), loss_elem=e(B) if labels is not None else None,
+                   gz=e(B) if labels is not None else None,
+                   dh_pre=e(B, H) if labels is not None else None)
+    lib.ctr_deepfm_head(_p(h), B, H, _p(w_out), _p(b_out), _p(z_fm), _p(labels),
+                        float(B if mean_div is None else mean_div), float(drop_scale),
+                        _p(out["z"]), _p(out["p"]), _p(out["loss_elem"]), _p(out["gz"]),
+                        _p(out["dh_pre"]), _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- GEMM ----
+def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False, *,
+         epi: int = EPI_NONE, bias=None, aux=None, scale: float = 1.0, drop_p: float = 0.0,
+         seed: int = 0, offset: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C = op(a) @ op(b) on fp32 MFMA with a fused epilogue (see include/ctr_hip.h)."""
+    _f32(a, "A")
+    _f32(b, "B")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else b.shape
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    else:
+        _f32(out, "out")
+        if tuple(out.shape) != (M, N):
+            raise ValueError("gemm: bad out shape")
+    if aux is not None:
+        _f32(aux, "aux")
+    nbytes = lib.ctr_gemm_f32_workspace_bytes(int(trans_a), int(trans_b), M, N, K)
+    ws = Workspace.get(nbytes, a.device)
+    lib.ctr_gemm_f32(int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b), b.stride(0),
+                     _p(out), out.stride(0), int(epi), _p(bias), _p(aux),
+                     aux.stride(0) if aux is not None else 0, float(scale), float(drop_p),
+                     int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(ws),
+                     0 if ws is None else ws.numel(), _stream())
+    return out
+
+
+def linear(x, weight, bias, *, relu=False, drop_p=0.0, seed=0, offset=0, out=None):
+    """nn.Linear (+ReLU +Dropout) forward: x @ weight.T + bias, fused epilogue."""
+    if relu:
+        epi = EPI_BIAS_RELU_DROP if drop_p > 0 else EPI_BIAS_RELU
+    else:
+        epi = EPI_BIAS
+    return gemm(x, weight, False, True, epi=epi, bias=bias, drop_p=drop_p, seed=seed,
+                offset=offset, out=out)
+
+
+def tensor_sum(x: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
+    _f32(x, "x")
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+    ws = Workspace.get(lib.ctr_reduce_workspace_bytes(x.numel(), 1), x.device)
+    lib.ctr_sum_f32(_p(x), x.numel(), float(scale), _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
+def colsum(X: torch.Tensor, row_w: torch.Tensor | None = None, scale: float = 1.0,
+           out=None) -> torch.Tensor:
+    _f32(X, "X")
+    M, N = X.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=X.device)
+    ws = Workspace.get(lib.ctr_reduce_workspace_bytes(M, N), X.device)
+    lib.ctr_colsum_f32(_p(X), M, N, X.stride(0), _p(row_w), float(scale), _p(out), _p(ws),
+                       ws.numel(), _stream())
+    return out
+
+
+# ---------------------------------------------------------------- scatter-add -------
+class SparsePlanBuffers:
+    """Device buffers of a ctr_sparse_plan for up to `capacity` slots."""
+
+    def __init__(self, capacity: int, device: torch.device):
+        self.capacity = int(capacity)
+        self.device = device
+        i32 = dict(dtype=torch.int32, device=device)
+        c = max(self.capacity, 1)
+        self.sorted_slots = torch.empty(c, **i32)
+        self.sorted_rows = torch.empty(c, **i32)
+        self.pos_seg = torch.empty(c, **i32)
+        self.unique_rows = torch.empty(c, **i32)
+        self.seg_offsets = torch.empty(c + 1, **i32)
+        self.num_unique = torch.zeros(1, **i32)
+        self.S = 0
+        self._struct = SparsePlan()
+
+    def struct(self) -> SparsePlan:
+        s = self._struct
+        s.S = self.S
+        s.sorted_slots, s.sorted_rows = _p(self.sorted_slots), _p(self.sorted_rows)
+        s.pos_seg, s.unique_rows = _p(self.pos_seg), _p(self.unique_rows)
+        s.seg_offsets, s.num_unique = _p(self.seg_offsets), _p(self.num_unique)
+        return s
+
+    def build(self, idx: torch.Tensor, V: int, err_flag=None) -> "SparsePlanBuffers":
+        idx, it = _idx(idx)
+        S = idx.numel()
+        if S > self.capacity:
+            raise ValueError(f"sparse plan: {S} slots > capacity {self.capacity}")
+        self.S = S
+        nbytes = lib.ctr_sparse_plan_workspace_bytes(S, int(V))
+        if nbytes < 0:
+            raise RuntimeError(lib.load().ctr_last_error().decode())
+        ws = Workspace.get(nbytes, self.device)
+        lib.ctr_sparse_plan_build(_p(idx), it, int(V), self.struct(), _p(ws),
+                                  0 if ws is None else ws.numel(), _p(err_flag), _stream())
+        return self
+
+    def num_unique_host(self) -> int:
+        return int(self.num_unique.item())
+
+
+def _seg_ws(plan: SparsePlanBuffers, K: int):
+    return Workspace.get(lib.ctr_segment_workspace_bytes(max(plan.S, 1), K), plan.device)
+
+
+def fm_embedding_grad(plan: SparsePlanBuffers, F: int, emb, gz, sum_e, dx=None, rowmap=None,
+                      grad_rows=None, grad_lin=None):
+    V, K = emb.shape
+    cap = max(plan.capacity, 1)
+    if grad_rows is None:
+        grad_rows = torch.empty(cap, K, dtype=torch.float32, device=emb.device)
+    if grad_lin is None:
+        grad_lin = torch.empty(cap, dtype=torch.float32, device=emb.device)
+    ws = _seg_ws(plan, K)
+    lib.ctr_fm_embedding_grad(plan.struct(), int(F), int(K), _p(emb), _p(gz), _p(sum_e), _p(dx),
+                              _p(grad_rows), _p(grad_lin), _p(rowmap), _p(ws), ws.numel(),
+                              _stream())
+    return grad_rows, grad_lin
+
+
+def segment_sum_rows(plan: SparsePlanBuffers, vals, vals_lin=None, rowmap=None, out=None,
+                     out_lin=None):
+    K = vals.shape[1]
+    cap = max(plan.capacity, 1)
+    if out is None:
+        out = torch.empty(cap, K, dtype=torch.float32, device=vals.device)
+    if vals_lin is not None and out_lin is None:
+        out_lin = torch.empty(cap, dtype=torch.float32, device=vals.device)
+    ws = _seg_ws(plan, K)
+    lib.ctr_segment_sum_rows(plan.struct(), int(K), _p(vals), _p(vals_lin), _p(out), _p(out_lin),
+                             _p(rowmap), _p(ws), ws.numel(), _stream())
+    return out, out_lin
+
+
+def rows_to_dense(plan: SparsePlanBuffers, V: int, grad_rows, grad_lin=None):
+    K = grad_rows.shape[1]
+    dense = torch.zeros(V, K, dtype=torch.float32, device=grad_rows.device)
+    dense_lin = (torch.zeros(V, 1, dtype=torch.float32, device=grad_rows.device)
+                 if grad_lin is not None else None)
+    lib.ctr_rows_to_dense(plan.struct(), int(K), _p(grad_rows), _p(grad_lin), _p(dense),
+                          _p(dense_lin), _stream())
+    return dense, dense_lin
+
+
+# --------------------------------------------------------------------------- Adam ----
+def adam_scalars(step: int, lr: float, betas=(0.9, 0.999)) -> tuple[float, float]:
+    """step_size and sqrt(bias_correction2) exactly as torch/optim/adam.py computes them
+    (python doubles)."""
+    beta1, beta2 = betas
+    bias_correction1 = 1 - beta1 ** step
+    bias_correction2 = 1 - beta2 ** step
+    return lr / bias_correction1, bias_correction2 ** 0.5
+
+
+def adam_dense(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8,
+               weight_decay=0.0) -> None:
+    for t, n in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+        _f32(t, n)
+    ss, bc2s = adam_scalars(step, lr, betas)
+    lib.ctr_adam_dense(_p(p), _p(g), _p(m), _p(v), p.numel(), ss, bc2s, float(betas[0]),
+                       float(betas[1]), float(eps), float(weight_decay), _stream())
+
+
+def adam_embedding(emb, m_emb, v_emb, lin, m_lin, v_lin, rowmap, grad_rows, grad_lin, step: int,
+                   lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> None:
+    V, K = emb.shape
+    ss, bc2s = adam_scalars(step, lr, betas)
+    lib.ctr_adam_embedding(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
+                           _p(rowmap), _p(grad_rows), _p(grad_lin), ss, bc2s, float(betas[0]),
+                           float(betas[1]), float(eps), float(weight_decay), _stream())
+
+
+# ------------------------------------------------------------- Feature_Embedding ----
+def feature_embedding(idx: torch.Tensor, emb: torch.Tensor, err_flag=None) -> torch.Tensor:
+    idx, it = _idx(idx)
+    _f32(emb, "feature_embedding.weight")
+    B, F = idx.shape
+    V, K = emb.shape
+    out = torch.empty(B, F * (F - 1) // 2 + F * K, dtype=torch.float32, device=emb.device)
+    lib.ctr_feature_embedding_forward(_p(idx), it, B, F, K, V, _p(emb), _p(out), _p(err_flag),
+                                      _stream())
+    return out
+
+
+# ----------------------------------------------------------------------- REINFORCE ----
+def softmax_rows(x: torch.Tensor) -> torch.Tensor:
+    _f32(x, "x")
+    out = torch.empty_like(x)
+    lib.ctr_softmax_rows(_p(x), x.shape[0], x.shape[1], _p(out), _stream())
+    return out
+
+
+def pg_discount_norm(r: torch.Tensor, gamma: float):
+    """Returns (normalised returns fp64, the same as fp32, stats[mean, std] fp64)."""
+    r = _f32(r.reshape(-1).contiguous(), "rewards")
+    n = r.numel()
+    out = torch.empty(n, dtype=torch.float64, device=r.device)
+    out32 = torch.empty(n, dtype=torch.float32, device=r.device)
+    stats = torch.empty(2, dtype=torch.float64, device=r.device)
+    lib.ctr_pg_discount_norm(_p(r), n, float(gamma), _p(out), _p(out32), _p(stats), None, 0,
+                             _stream())
+    return out, out32, stats
+
+
+def pg_loss_grad(probs: torch.Tensor, acts: torch.Tensor, vt: torch.Tensor, grad_scale=1.0):
+    _f32(probs, "probs")
+    acts = _dev(acts, "acts").reshape(-1).to(torch.int64).contiguous()
+    vt = _f32(vt.reshape(-1).contiguous(), "vt")
+    B, A = probs.shape
+    loss = torch.empty(1, dtype=torch.float32, device=probs.device)
+    dlogits = torch.empty_like(probs)
+    lib.ctr_pg_loss_grad(_p(probs), _p(acts), _p(vt), B, A, float(grad_scale), _p(loss),
+                         _p(dlogits), None, 0, _stream())
+    return loss, dlogits
+

@@ -1,0 +1,174 @@
+"""FM and DeepFM with the reference's construction API, on the HIP kernels.
+
+Drop-in for ``src/models/p_model.py`` (FM 28-57, DeepFM 256-324): identical constructor
+signatures, submodules created in the same order (so ``torch.manual_seed(s)`` gives the
+same initial weights as the reference) and identical state_dict keys, so the RL drivers'
+``torch.load('...FMbest.pth')`` / ``load_state_dict`` and ``Feature_Embedding.load_embedding``
+work unchanged. ``forward(LongTensor[B,F]) -> FloatTensor[B,1]`` pCTR.
+
+Two execution paths, both entirely on libctr_hip.so kernels for the model math:
+  * autograd (drop-in): ``loss.backward()`` produces the reference's DENSE [V,K] embedding
+    gradient, so a stock ``torch.optim.Adam`` keeps working;
+  * fused training (the hot path): :class:`rl_ctr_prediction_amd.trainer.FusedCTRTrainer`
+    runs forward, BCE, backward, the scatter-add and dense Adam without materialising the
+    dense gradient.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+import torch.nn as nn
+
+from . import hip_ops
+
+_seed_counter = itertools.count()
+
+
+def _dropout_seed() -> int:
+    # deterministic under torch.manual_seed, distinct per call site
+    return (torch.initial_seed() * 1000003 + next(_seed_counter) * 7919) & (2**63 - 1)
+
+
+class _FMPart(torch.autograd.Function):
+    """(z_fm [B,1], flat embeddings [B,F*K]) = FM part of p_model.py:296-313 (+ the
+    gather at 320). Backward = FM gradient + MLP-input gradient, summed per row in slot
+    order (deterministic), returned as dense grads like embedding_dense_backward."""
+
+    @staticmethod
+    def forward(ctx, x, emb, lin, bias, want_emb):
+        B, F = x.shape
+        r = hip_ops.fm_forward(x, emb, lin, bias, want_sum=True, want_emb=want_emb, want_p=False)
+        ctx.save_for_backward(x, emb, r.sum_e)
+        ctx.want_emb = want_emb
+        flat = r.emb_out if want_emb else emb.new_empty(0)
+        return r.z.view(B, 1), flat
+
+    @staticmethod
+    def backward(ctx, gz, gflat):
+        x, emb, sum_e = ctx.saved_tensors
+        B, F = x.shape
+        V, K = emb.shape
+        if gz is None:
+            gz = torch.zeros(B, dtype=torch.float32, device=emb.device)
+        gz = gz.reshape(-1).contiguous()
+        dx = gflat.contiguous() if (ctx.want_emb and gflat is not None) else None
+        plan = hip_ops.SparsePlanBuffers(B * F, emb.device).build(x, V)
+        grad_rows, grad_lin = hip_ops.fm_embedding_grad(plan, F, emb, gz, sum_e, dx)
+        g_emb, g_lin = hip_ops.rows_to_dense(plan, V, grad_rows, grad_lin)
+        g_bias = hip_ops.tensor_sum(gz) if ctx.needs_input_grad[3] else None
+        return (None, g_emb if ctx.needs_input_grad[1] else None,
+                g_lin if ctx.needs_input_grad[2] else None, g_bias, None)
+
+
+class _LinearAct(torch.autograd.Function):
+    """nn.Linear (+ ReLU + Dropout) on the fp32 MFMA GEMM with fused epilogues."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, drop_p, seed):
+        y = hip_ops.linear(x.contiguous(), weight, bias, relu=relu, drop_p=drop_p, seed=seed)
+        ctx.save_for_backward(x, weight, y)
+        ctx.relu = relu
+        ctx.scale = 1.0 / (1.0 - drop_p)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        gy = gy.contiguous()
+        if ctx.relu:  # Dropout then ReLU backward: grad where the saved output is > 0
+            g = torch.where(y > 0, gy * ctx.scale, torch.zeros_like(gy))
+        else:
+            g = gy
+        dx = hip_ops.gemm(g, weight) if ctx.needs_input_grad[0] else None
+        dw = hip_ops.gemm(g, x.contiguous(), trans_a=True) if ctx.needs_input_grad[1] else None
+        db = hip_ops.colsum(g) if ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+def _fm_part(x, emb, lin, bias, want_emb):
+    return _FMPart.apply(x, emb, lin, bias, want_emb)
+
+
+def mlp_forward(mlp: nn.Sequential, h: torch.Tensor, training: bool) -> torch.Tensor:
+    """Run an nn.Sequential of [Linear, ReLU, Dropout]* + Linear on fused HIP GEMMs."""
+    mods = list(mlp)
+    i = 0
+    while i < len(mods):
+        lin = mods[i]
+        if not isinstance(lin, nn.Linear):
+            raise TypeError(f"unsupported MLP layer {type(lin).__name__}")
+        j = i + 1
+        relu = j < len(mods) and isinstance(mods[j], nn.ReLU)
+        j += int(relu)
+        drop = 0.0
+        if relu and j < len(mods) and isinstance(mods[j], nn.Dropout):
+            drop = float(mods[j].p) if training else 0.0
+            j += 1
+        h = _LinearAct.apply(h, lin.weight, lin.bias, relu, drop, _dropout_seed())
+        i = j
+    return h
+
+
+class FM(nn.Module):
+    """p_model.py:28-57. z = bias + sum_f w[x_f] + 0.5 * sum_k((sum_f e)^2 - sum_f e^2)."""
+
+    def __init__(self, feature_nums, latent_dims, output_dim=1):
+        super().__init__()
+        latent_dims = int(latent_dims)  # the driver's --latent_dims arrives as str
+        if output_dim != 1:
+            raise NotImplementedError("FM: output_dim must be 1 (the reference's only use)")
+        self.linear = nn.Embedding(feature_nums, output_dim)
+        self.bias = nn.Parameter(torch.zeros((output_dim,)))
+        self.feature_embedding = nn.Embedding(feature_nums, latent_dims)
+
+    def forward(self, x):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            z, _ = _fm_part(x, self.feature_embedding.weight, self.linear.weight, self.bias, False)
+            return torch.sigmoid(z)
+        r = hip_ops.fm_forward(x, self.feature_embedding.weight.detach(),
+                               self.linear.weight.detach(), self.bias.detach(), want_sum=False)
+        return r.p.view(-1, 1)
+
+
+class DeepFM(nn.Module):
+    """p_model.py:256-324: FM part + MLP [F*K -> 300 -> 200 -> 1] (ReLU, Dropout 0.2)."""
+
+    def __init__(self, feature_nums, field_nums, latent_dims, output_dim=1):
+        super().__init__()
+        latent_dims = int(latent_dims)
+        self.feature_nums = feature_nums
+        self.field_nums = field_nums
+        self.latent_dims = latent_dims
+        self.linear = nn.Embedding(self.feature_nums, output_dim)
+        self.bias = nn.Parameter(torch.zeros((output_dim,)))
+        self.feature_embedding = nn.Embedding(self.feature_nums, self.latent_dims)
+        deep_input_dims = self.field_nums * self.latent_dims
+        layers = []
+        for neuron_num in (300, 200):
+            layers.append(nn.Linear(deep_input_dims, neuron_num))
+            layers.append(nn.ReLU())
+            layers.append(nn.Dropout(p=0.2))
+            deep_input_dims = neuron_num
+        layers.append(nn.Linear(deep_input_dims, 1))
+        self.mlp = nn.Sequential(*layers)
+
+    def forward(self, x):
+        E, w, b = self.feature_embedding.weight, self.linear.weight, self.bias
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            z_fm, flat = _fm_part(x, E, w, b, True)
+            out = mlp_forward(self.mlp, flat, self.training)
+            return torch.sigmoid(z_fm + out)
+        with torch.no_grad():
+            r = hip_ops.fm_forward(x, E.detach(), w.detach(), b.detach(), want_sum=False,
+                                   want_emb=True, want_p=False)
+            h = r.emb_out
+            m = self.mlp
+            p0 = m[2].p if self.training else 0.0
+            p1 = m[5].p if self.training else 0.0
+            h = hip_ops.linear(h, m[0].weight, m[0].bias, relu=True, drop_p=p0,
+                               seed=_dropout_seed())
+            h = hip_ops.linear(h, m[3].weight, m[3].bias, relu=True, drop_p=p1,
+                               seed=_dropout_seed())
+            head = hip_ops.deepfm_head(h, m[6].weight, m[6].bias, r.z)
+            return head["p"].view(-1, 1)

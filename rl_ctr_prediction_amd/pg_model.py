@@ -1,0 +1,227 @@
+"""REINFORCE policy of ``src/models/PG_model.py`` on the HIP kernels.
+
+Mirrors ``Net`` (24-58) and ``PolicyGradient`` (60-179): same constructor arguments,
+same methods and return types, same CPU RNG calls in ``choose_action`` (so a seeded run
+picks the same actions), ``discount_and_norm_rewards`` in fp64 raising
+``FloatingPointError`` on a zero std like the reference's ``np.seterr(all='raise')``.
+
+Reference quirk kept by default: ``Net`` sizes its first Linear as
+``F(F-1)/2 * K + F*K`` (PG_model.py:34-39) while Feature_Embedding emits
+``F(F-1)/2 + F*K`` features, so only latent_dims == 1 runs; any other K raises the
+same shape error. ``fix_input_dims=True`` sizes it to the real state width (used for the
+C4 REINFORCE configuration; documented in DESIGN.md).
+
+``learn`` is one fused native pass: Feature_Embedding -> 5 fused GEMMs -> softmax ->
+loss + softmax-backward kernel -> 5 weight-gradient GEMMs with Dropout/ReLU mask
+epilogues -> dense Adam over one flat parameter buffer (+ one all-reduce when data
+parallel). The embedding is not updated: its output is detached (Feature_embedding.py:59),
+so torch's Adam never sees a gradient for it.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import hip_ops
+from .distributed import allreduce_sum_, world
+from .feature_embedding import Feature_Embedding
+from .p_model import _dropout_seed, mlp_forward
+
+
+class Net(nn.Module):
+    def __init__(self, field_nums, feature_nums, latent_dims, action_numbers, campaign_id,
+                 fix_input_dims: bool = False):
+        super().__init__()
+        self.field_nums = field_nums
+        self.feature_nums = feature_nums
+        self.latent_dims = int(latent_dims)
+        self.campaign_id = campaign_id
+        self.embedding_layer = Feature_Embedding(self.feature_nums, self.field_nums, self.latent_dims)
+        pairs = self.field_nums * (self.field_nums - 1) // 2
+        if fix_input_dims:
+            input_dims = pairs + self.field_nums * self.latent_dims
+        else:  # the reference's formula
+            input_dims = pairs * self.latent_dims + self.field_nums * self.latent_dims
+        self.input_dims = input_dims
+        layers = []
+        neuron_nums = 1024
+        for _ in range(4):
+            layers.append(nn.Linear(input_dims, neuron_nums))
+            layers.append(nn.ReLU())
+            layers.append(nn.Dropout(p=0.2))
+            input_dims = neuron_nums
+            neuron_nums = int(neuron_nums / 2)
+        layers.append(nn.Linear(input_dims, action_numbers))
+        self.mlp = nn.Sequential(*layers)
+
+    def _state(self, x):
+        s = self.embedding_layer(x)
+        if s.shape[1] != self.input_dims:
+            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({s.shape[0]}x"
+                               f"{s.shape[1]} and {self.input_dims}x{self.mlp[0].out_features})")
+        return s
+
+    def forward(self, input):
+        s = self._state(input)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters()):
+            return torch.softmax(mlp_forward(self.mlp, s, self.training), dim=1)
+        with torch.no_grad():
+            logits = mlp_forward(self.mlp, s, self.training)
+        return hip_ops.softmax_rows(logits.contiguous())
+
+
+class _PGLoss(torch.autograd.Function):
+    """loss_func's value from the HIP kernel; d loss / d probs for autograd callers."""
+
+    @staticmethod
+    def forward(ctx, probs, acts, vt):
+        loss, _ = hip_ops.pg_loss_grad(probs.contiguous(), acts, vt)
+        ctx.save_for_backward(probs, acts, vt)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        probs, acts, vt = ctx.saved_tensors
+        c = vt.reshape(-1).float().mean() * g
+        a = acts.reshape(-1, 1).long() - 1
+        dp = torch.zeros_like(probs)
+        dp.scatter_(1, a, -c / probs.gather(1, a))
+        return dp, None, None
+
+
+class PolicyGradient:
+    def __init__(self, feature_nums, field_nums, latent_dims, campaign_id, action_nums=2,
+                 learning_rate=1e-4, reward_decay=1, device="cuda:0", fix_input_dims=False,
+                 process_group=None):
+        self.action_nums = action_nums
+        self.feature_nums = feature_nums
+        self.field_nums = field_nums
+        self.latent_dims = latent_dims
+        self.lr = learning_rate
+        self.gamma = reward_decay
+        self.device = device
+        self.campaign_id = campaign_id
+        self.group = process_group
+        self._ep_states, self._ep_as, self._ep_rs = [], [], []
+        self.policy_net = Net(self.field_nums, self.feature_nums, self.latent_dims,
+                              self.action_nums, self.campaign_id, fix_input_dims).to(self.device)
+        # dense Adam state over one flat buffer holding every MLP parameter
+        self._layers = [m for m in self.policy_net.mlp if isinstance(m, nn.Linear)]
+        params = [t for lin in self._layers for t in (lin.weight, lin.bias)]
+        n = sum(p.numel() for p in params)
+        dev = self._layers[0].weight.device
+        self._flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self._grad = torch.zeros_like(self._flat)
+        self._m, self._v = torch.zeros_like(self._flat), torch.zeros_like(self._flat)
+        self._gviews = []
+        off = 0
+        for p in params:
+            k = p.numel()
+            self._flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self._flat[off:off + k].view_as(p)
+            self._gviews.append(self._grad[off:off + k].view_as(p))
+            off += k
+        self._step = 0
+        self.weight_decay = 1e-5  # PG_model.py:87
+        self.betas, self.eps = (0.9, 0.999), 1e-8
+        self._seed = _dropout_seed()
+        self._drop_offset = 0
+
+    # ---------------------------------------------------------------- reference API ---
+    @property
+    def ep_states(self):
+        return torch.cat(self._ep_states) if self._ep_states else torch.LongTensor().to(self.device)
+
+    @property
+    def ep_as(self):
+        return torch.cat(self._ep_as) if self._ep_as else torch.LongTensor().to(self.device)
+
+    @property
+    def ep_rs(self):
+        return torch.cat(self._ep_rs) if self._ep_rs else torch.FloatTensor().to(self.device)
+
+    @ep_rs.setter
+    def ep_rs(self, value):
+        self._ep_rs = [value]
+
+    def load_embedding(self, pretrain_params):
+        self.policy_net.embedding_layer.feature_embedding.weight.data.copy_(
+            torch.from_numpy(np.array(pretrain_params["feature_embedding.weight"].cpu())))
+
+    def loss_func(self, all_act_prob, acts, vt):
+        return _PGLoss.apply(all_act_prob, acts.to(all_act_prob.device),
+                             vt.to(all_act_prob.device).float())
+
+    def choose_action(self, states):
+        prob_weights = self.policy_net.forward(states).cpu()
+        random_seeds = torch.rand(len(states), 1)
+        max_action = torch.argsort(-prob_weights)[:, 0] + 1
+        random_action = torch.randint(low=1, high=self.action_nums + 1, size=[len(states), 1])
+        actions = torch.where(random_seeds >= torch.max(prob_weights, 1)[0].view(-1, 1),
+                              max_action.view(-1, 1), random_action)
+        return actions.to(self.device)
+
+    def choose_best_action(self, state):
+        prob_weights = self.policy_net.forward(state)
+        return torch.max(prob_weights, 1)[1].view(-1, 1) + 1
+
+    def store_transition(self, s, a, r):
+        self._ep_states.append(s)
+        self._ep_as.append(a)
+        self._ep_rs.append(r)
+
+    def _discount_norm_device(self):
+        r = self.ep_rs.to(self.device).float().reshape(-1)
+        d64, d32, stats = hip_ops.pg_discount_norm(r, float(self.gamma))
+        if float(stats[1].item()) == 0.0:
+            raise FloatingPointError("divide by zero encountered in divide")
+        return d64, d32
+
+    def discount_and_norm_rewards(self):
+        d64, _ = self._discount_norm_device()
+        return d64.cpu().numpy().reshape(-1, 1)
+
+    def learn(self):
+        _, vt = self._discount_norm_device()
+        states = self.ep_states.to(self.device)
+        acts = self.ep_as.to(self.device)
+        loss = self._fused_learn(states, acts, vt)
+        self._ep_states, self._ep_as, self._ep_rs = [], [], []
+        return loss
+
+    # ------------------------------------------------------------------ fused pass ----
+    def _fused_learn(self, states, acts, vt) -> torch.Tensor:
+        net = self.policy_net
+        training = net.training
+        x0 = net._state(states)
+        n = x0.shape[0]
+        acts_l = []
+        h = x0
+        mods = list(net.mlp)
+        drops = [float(mods[3 * i + 2].p) if training else 0.0 for i in range(4)]
+        for i, lin in enumerate(self._layers):
+            last = i == len(self._layers) - 1
+            off = self._drop_offset
+            self._drop_offset += n * lin.out_features
+            h_in = h
+            h = hip_ops.linear(h_in, lin.weight, lin.bias, relu=not last,
+                               drop_p=0.0 if last else drops[i], seed=self._seed, offset=off)
+            acts_l.append(h_in)
+        probs = hip_ops.softmax_rows(h)
+        loss, g = hip_ops.pg_loss_grad(probs, acts, vt)
+        for i in range(len(self._layers) - 1, -1, -1):
+            lin = self._layers[i]
+            inp = acts_l[i]
+            hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
+            hip_ops.colsum(g, out=self._gviews[2 * i + 1])
+            if i > 0:
+                g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
+                                 scale=1.0 / (1.0 - drops[i - 1]))
+        if world()[1] > 1:
+            allreduce_sum_(self._grad, self.group)
+            self._grad.div_(world()[1])
+        self._step += 1
+        hip_ops.adam_dense(self._flat, self._grad, self._m, self._v, self._step, self.lr,
+                           self.betas, self.eps, self.weight_decay)
+        return loss

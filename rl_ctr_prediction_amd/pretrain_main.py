@@ -1,0 +1,220 @@
+"""CTR pretraining driver — counterpart of ``src/all_main/pretrain_main.py``.
+
+Same functions (setup_seed, get_model, get_dataset, train, test, submission, main,
+eva_stopping), same flags and files (train_.txt / test_.txt / featindex.txt in, rotating
+``{model}{epoch%5}.pth`` + ``{model}best.pth`` + ``test_submission.csv`` / ``day_aucs.csv``
+out), same semantics: batches in file order (no shuffle), Adam re-created every epoch
+(here: :meth:`FusedCTRTrainer.reset_optimizer`), train loss = mean of batch losses,
+AUC over the concatenated test predictions, loss-/AUC-based early stopping with reload
+of the checkpoint four epochs back.
+
+Differences, all deliberate: the training step is the fused HIP step (FM and DeepFM;
+the other eight model families are out of scope); the batches are
+sliced from one device-resident copy of the data instead of 8 DataLoader worker
+processes; the rotating-checkpoint cleanup skips files that were never written (the
+reference crashes there when epoch < 5, all_main/pretrain_main.py:201-202).
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import os
+import random
+
+import numpy as np
+import pandas as pd
+import torch
+import torch.nn as nn
+from sklearn.metrics import roc_auc_score
+
+from . import creat_data as Data
+from . import p_model as Model
+from .trainer import FusedCTRTrainer
+
+
+def setup_seed(seed):
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
+def get_model(model_name, feature_nums, field_nums, latent_dims):
+    if model_name == "FM":
+        return Model.FM(feature_nums, latent_dims)
+    if model_name == "DeepFM":
+        return Model.DeepFM(feature_nums, field_nums, latent_dims)
+    raise NotImplementedError(
+        f"{model_name}: only FM and DeepFM (the north-star hot path) are built on HIP; "
+        "LR/FFM/W&D/FNN/IPNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
+
+
+def get_dataset(datapath, dataset_name, campaign_id):
+    data_path = datapath + dataset_name + campaign_id
+    train_fm = pd.read_csv(data_path + "train_.txt", header=None).values.astype(int)
+    test_fm = pd.read_csv(data_path + "test_.txt", header=None).values.astype(int)
+    field_nums = len(train_fm[0, 1:])
+    feature_index = pd.read_csv(data_path + "featindex.txt", header=None).values
+    feature_nums = int(feature_index[-1, 0].split("\t")[1]) + 1
+    return train_fm, train_fm, test_fm, field_nums, feature_nums
+
+
+class DeviceBatches:
+    """Batches of a libsvm_dataset in file order, sliced from one device-resident copy
+    (features int64 [N,F] like the reference's collated LongTensor, labels float)."""
+
+    def __init__(self, dataset: Data.libsvm_dataset, batch_size: int, device):
+        self.x = torch.as_tensor(np.asarray(dataset.Data), dtype=torch.int64).to(device)
+        self.y = torch.as_tensor(np.asarray(dataset.label), dtype=torch.float32).to(device)
+        self.batch_size = int(batch_size)
+
+    def __len__(self):
+        return (self.x.shape[0] + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        for s in range(0, self.x.shape[0], self.batch_size):
+            yield self.x[s:s + self.batch_size], self.y[s:s + self.batch_size]
+
+
+def train(model, optimizer, data_loader, loss, device):
+    """One epoch (all_main/pretrain_main.py:67-83); `optimizer` is the FusedCTRTrainer."""
+    model.train()
+    total_loss = 0.0
+    log_intervals = 0
+    for features, labels in data_loader:
+        train_loss = optimizer.step(features, labels)
+        total_loss += train_loss.item()
+        log_intervals += 1
+    optimizer.check_errors()
+    return total_loss / log_intervals
+
+
+def _predict(model, data_loader, loss):
+    model.eval()
+    targets, predicts = [], []
+    intervals, total = 0, 0.0
+    with torch.no_grad():
+        for features, labels in data_loader:
+            y = model(features)
+            total += loss(y, labels.view(-1, 1)).item()
+            targets.extend(labels.view(-1, 1).tolist())
+            predicts.extend(y.tolist())
+            intervals += 1
+    return targets, predicts, total / max(intervals, 1)
+
+
+def test(model, data_loader, loss, device):
+    targets, predicts, avg = _predict(model, data_loader, loss)
+    return roc_auc_score(targets, predicts), avg
+
+
+def submission(model, data_loader, device):
+    targets, predicts, _ = _predict(model, data_loader, nn.BCELoss())
+    return predicts, roc_auc_score(targets, predicts)
+
+
+def eva_stopping(valid_aucs, valid_losses, type):  # noqa: A002 (reference name)
+    if type == "auc":
+        if len(valid_aucs) >= 5:
+            a = valid_aucs
+            if a[-1] < a[-2] < a[-3] < a[-4] < a[-5]:
+                return True
+    else:
+        if len(valid_losses) >= 5:
+            v = valid_losses
+            if v[-1] > v[-2] > v[-3] > v[-4] > v[-5]:
+                return True
+    return False
+
+
+def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, learning_rate,
+         weight_decay, early_stop_type, batch_size, device, save_param_dir, verbose=True):
+    if not os.path.exists(save_param_dir + campaign_id):
+        os.mkdir(save_param_dir + campaign_id)
+    device = torch.device(device)
+    train_fm, train_data, test_data, field_nums, feature_nums = get_dataset(
+        data_path, dataset_name, campaign_id)
+    train_dataset = Data.libsvm_dataset(train_data[:, 1:], train_data[:, 0])
+    test_dataset = Data.libsvm_dataset(test_data[:, 1:], test_data[:, 0])
+    train_data_loader = DeviceBatches(train_dataset, batch_size, device)
+    test_data_loader = DeviceBatches(test_dataset, batch_size, device)
+
+    model = get_model(model_name, feature_nums, field_nums, latent_dims).to(device)
+    loss = nn.BCELoss()
+    trainer = FusedCTRTrainer(model, lr=learning_rate, weight_decay=weight_decay)
+
+    valid_aucs, valid_losses, history = [], [], []
+    early_stop_index, is_early_stop = 0, False
+    start_time = datetime.datetime.now()
+    for epoch_i in range(epoch):
+        train_start_time = datetime.datetime.now()
+        trainer.reset_optimizer()  # torch.optim.Adam(...) re-created every epoch (line 153)
+        train_average_loss = train(model, trainer, train_data_loader, loss, device)
+        torch.save(model.state_dict(),
+                   save_param_dir + campaign_id + model_name + str(np.mod(epoch_i, 5)) + ".pth")
+        auc, valid_loss = test(model, test_data_loader, loss, device)
+        valid_aucs.append(auc)
+        valid_losses.append(valid_loss)
+        history.append(dict(epoch=epoch_i, train_loss=train_average_loss, valid_auc=auc,
+                            valid_loss=valid_loss))
+        train_end_time = datetime.datetime.now()
+        if verbose:
+            print("epoch:", epoch_i, "training average loss:", train_average_loss,
+                  "validation auc:", auc, "validation loss:", valid_loss,
+                  "[{}s]".format((train_end_time - train_start_time).seconds))
+        if eva_stopping(valid_aucs, valid_losses, early_stop_type):
+            early_stop_index = np.mod(epoch_i - 4, 5)
+            is_early_stop = True
+            break
+    end_time = datetime.datetime.now()
+
+    if is_early_stop:
+        test_model = get_model(model_name, feature_nums, field_nums, latent_dims).to(device)
+        load_path = save_param_dir + campaign_id + model_name + str(early_stop_index) + ".pth"
+        test_model.load_state_dict(torch.load(load_path, map_location=device, weights_only=True))
+    else:
+        test_model = model
+    auc, test_loss = test(test_model, test_data_loader, loss, device)
+    torch.save(test_model.state_dict(), save_param_dir + campaign_id + model_name + "best.pth")
+    if verbose:
+        print("\ntest auc:", auc, datetime.datetime.now(),
+              "[{}s]".format((end_time - start_time).seconds))
+
+    submission_path = data_path + dataset_name + campaign_id + model_name + "/"
+    if not os.path.exists(submission_path):
+        os.mkdir(submission_path)
+    test_predicts, test_auc = submission(test_model, test_data_loader, device)
+    pd.DataFrame(data=test_predicts).to_csv(submission_path + "test_submission.csv", header=None)
+    pd.DataFrame(data=[[test_auc]]).to_csv(submission_path + "day_aucs.csv", header=None)
+    for i in range(5):
+        path = save_param_dir + campaign_id + model_name + str(i) + ".pth"
+        if os.path.exists(path):
+            os.remove(path)
+    return dict(history=history, test_auc=auc, test_loss=test_loss, test_preds=test_predicts,
+                model=test_model)
+
+
+def _parser():
+    parser = argparse.ArgumentParser()
+    parser.add_argument("--data_path", default="../../data/")
+    parser.add_argument("--dataset_name", default="avazu/", help="ipinyou, cretio, yoyi, avazu")
+    parser.add_argument("--campaign_id", default="avazu/", help="1458, 3358, 3386, 3427, 3476, avazu")
+    parser.add_argument("--model_name", default="FM", help="FM, DeepFM")
+    parser.add_argument("--latent_dims", type=int, default=10)
+    parser.add_argument("--epoch", type=int, default=20)
+    parser.add_argument("--learning_rate", type=float, default=1e-3)
+    parser.add_argument("--weight_decay", type=float, default=1e-5)
+    parser.add_argument("--early_stop_type", default="loss", help="auc, loss")
+    parser.add_argument("--batch_size", type=int, default=4096)
+    parser.add_argument("--device", default="cuda:0")
+    parser.add_argument("--save_param_dir", default="../models/model_params/")
+    return parser
+
+
+if __name__ == "__main__":
+    args = _parser().parse_args()
+    setup_seed(1)
+    main(args.data_path, args.dataset_name, args.campaign_id, args.latent_dims, args.model_name,
+         args.epoch, args.learning_rate, args.weight_decay, args.early_stop_type,
+         args.batch_size, args.device, args.save_param_dir)

@@ -1,0 +1,267 @@
+"""The fused CTR training step — the hot path of this repo.
+
+Replaces the per-batch body of ``all_main/pretrain_main.py:train`` (67-83):
+``y = model(x); loss = BCELoss(y, labels); model.zero_grad(); loss.backward();
+optimizer.step()`` for FM (p_model.py:28-57) and DeepFM (p_model.py:256-324) with
+torch.optim.Adam(lr, weight_decay) — reference semantics, including DENSE Adam (every
+embedding row moves every step) and the unfused BCE∘sigmoid gradient.
+
+Per step, on one HIP stream (all kernels from libctr_hip.so):
+  FM:      fm_forward(+BCE head) -> sum(gz) -> sparse plan -> per-row grad sums
+           -> Adam(E, w) dense pass -> Adam(bias)
+  DeepFM:  fm_forward(+flat gather) -> 2 x GEMM(bias+ReLU+dropout) -> head(Linear(200,1)
+           + sigmoid + BCE + dH2) -> GEMM dH1 (mask epilogue) -> GEMM dX -> 3 weight-grad
+           GEMMs (split-K, deterministic) + column sums -> sparse plan -> per-row grad
+           sums (FM + MLP-input grads) -> Adam(E, w) dense pass -> Adam(flat MLP)
+The dense [V,K] gradient is never materialised: Adam reads a row's gradient through the
+rowmap only for rows present in the batch (24 B/element/step instead of 32).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from . import hip_ops
+from .distributed import allgather_sparse_rows, allreduce_sum_, world
+from .p_model import FM, DeepFM
+
+DEEPFM_DENSE = ("bias", "mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bias",
+                "mlp.6.weight", "mlp.6.bias")
+FM_DENSE = ("bias",)
+
+
+@dataclass
+class _Bufs:
+    B: int
+    fm: hip_ops.FMForward
+    plan: hip_ops.SparsePlanBuffers
+    grad_rows: torch.Tensor
+    grad_lin: torch.Tensor
+    h1: torch.Tensor | None = None
+    h2: torch.Tensor | None = None
+    head: dict | None = None
+    dh1: torch.Tensor | None = None
+    dx: torch.Tensor | None = None
+    loss: torch.Tensor | None = None
+    gplan: hip_ops.SparsePlanBuffers | None = None
+    g_rows: torch.Tensor | None = None
+    g_lin: torch.Tensor | None = None
+
+
+class FusedCTRTrainer:
+    """Fused forward + BCE + backward + dense Adam for FM / DeepFM.
+
+    Args mirror ``torch.optim.Adam(model.parameters(), lr, betas, eps, weight_decay)``.
+    The model's dense parameters (FM bias, DeepFM MLP) are re-pointed into one flat
+    buffer (same Parameter objects, same state_dict), so the dense Adam and the
+    data-parallel all-reduce are one launch each.
+    """
+
+    def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 0.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, process_group=None, seed: int | None = None):
+        if not isinstance(model, (FM, DeepFM)):
+            raise TypeError("FusedCTRTrainer drives FM or DeepFM")
+        self.model = model
+        self.kind = "DeepFM" if isinstance(model, DeepFM) else "FM"
+        self.lr, self.weight_decay, self.betas, self.eps = float(lr), float(weight_decay), betas, eps
+        self.group = process_group
+        E = model.feature_embedding.weight
+        self.device = E.device
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedCTRTrainer needs the model on a ROCm device")
+        self.V, self.K = E.shape
+        named = dict(model.named_parameters())
+        self.dense_names = DEEPFM_DENSE if self.kind == "DeepFM" else FM_DENSE
+        total = sum(named[n].numel() for n in self.dense_names)
+        flat = torch.empty(total, dtype=torch.float32, device=self.device)
+        self.flat_grad = torch.zeros_like(flat)
+        self.views, self.grad_views = {}, {}
+        off = 0
+        for n in self.dense_names:
+            p = named[n]
+            k = p.numel()
+            flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = flat[off:off + k].view_as(p)
+            self.views[n] = p.data
+            self.grad_views[n] = self.flat_grad[off:off + k].view_as(p)
+            off += k
+        self.flat = flat
+        self.m_flat = torch.zeros_like(flat)
+        self.v_flat = torch.zeros_like(flat)
+        self.m_E = torch.zeros_like(E.data)
+        self.v_E = torch.zeros_like(E.data)
+        self.m_w = torch.zeros(self.V, dtype=torch.float32, device=self.device)
+        self.v_w = torch.zeros_like(self.m_w)
+        self.rowmap = torch.full((self.V,), -1, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.step_count = 0
+        self._bufs: _Bufs | None = None
+        self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
+        self._drop_counter = 0
+        # bench hook: {"adam": [], "gather": [], "scatter": []} -> (start, end) HIP events
+        # recorded on the launch stream around those kernels
+        self.timing: dict | None = None
+
+    def _mark(self):
+        if self.timing is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _span(self, key, start):
+        if start is not None:
+            self.timing[key].append((start, self._mark()))
+
+    # ----------------------------------------------------------------- optimiser -----
+    def reset_optimizer(self) -> None:
+        """What ``torch.optim.Adam(...)`` re-created every epoch does
+        (all_main/pretrain_main.py:153): fresh moments, step 0."""
+        for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
+            t.zero_()
+        self.step_count = 0
+
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.Adam-compatible state_dict (parameter order = model.parameters())."""
+        named = list(self.model.named_parameters())
+        m = {n: v for n, v in zip(self.dense_names, self._split(self.m_flat))}
+        v = {n: v for n, v in zip(self.dense_names, self._split(self.v_flat))}
+        m["feature_embedding.weight"], v["feature_embedding.weight"] = self.m_E, self.v_E
+        m["linear.weight"], v["linear.weight"] = self.m_w.view(-1, 1), self.v_w.view(-1, 1)
+        state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": m[n].clone(),
+                     "exp_avg_sq": v[n].clone()} for i, (n, _) in enumerate(named)}
+        return {"state": state if self.step_count else {},
+                "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                                  "weight_decay": self.weight_decay, "amsgrad": False,
+                                  "params": list(range(len(named)))}]}
+
+    def _split(self, flat):
+        out, off = [], 0
+        for n in self.dense_names:
+            k = self.views[n].numel()
+            out.append(flat[off:off + k].view_as(self.views[n]))
+            off += k
+        return out
+
+    # --------------------------------------------------------------------- buffers ---
+    def _buffers(self, B: int, F: int) -> _Bufs:
+        b = self._bufs
+        if b is not None and b.B == B and b.plan.capacity == B * F:
+            return b
+        dev, K = self.device, self.K
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        deep = self.kind == "DeepFM"
+        fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, F * K) if deep else None,
+                               p=None, loss_elem=e(B), gz=e(B))
+        S = B * F
+        b = _Bufs(B=B, fm=fm, plan=hip_ops.SparsePlanBuffers(S, dev), grad_rows=e(S, K),
+                  grad_lin=e(S), loss=e(1))
+        if deep:
+            mlp = self.model.mlp
+            H1, H2 = mlp[0].out_features, mlp[3].out_features
+            b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, F * K)
+            b.head = dict(z=e(B), p=e(B), loss_elem=fm.loss_elem, gz=fm.gz, dh_pre=e(B, H2))
+        rank, ws = world()
+        if ws > 1:
+            b.gplan = hip_ops.SparsePlanBuffers(S * ws, dev)
+            b.g_rows, b.g_lin = e(S * ws, K), e(S * ws)
+        self._bufs = b
+        return b
+
+    # ------------------------------------------------------------------------ step ----
+    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
+        """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
+        batch's mean BCE as a 1-element device tensor (no host sync)."""
+        B, F = x.shape
+        rank, ws = world()
+        mean_div = float(global_batch if global_batch is not None else B * ws)
+        b = self._buffers(B, F)
+        y = y.reshape(-1)
+        if y.dtype != torch.float32:
+            y = y.float()
+        y = y.contiguous()
+        m = self.model
+        E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
+        gv = self.grad_views
+        if self.kind == "FM":
+            t = self._mark()
+            hip_ops.fm_forward(x, E, w, bias, want_sum=True, labels=y, mean_div=mean_div,
+                               want_p=False, err_flag=self.err, out=b.fm)
+            self._span("gather", t)
+            gz = b.fm.gz
+        else:
+            gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
+        hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        t = self._mark()
+        b.plan.build(x, self.V)
+        sparse_rowmap = self.rowmap if ws == 1 else None
+        hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
+                                  grad_rows=b.grad_rows, grad_lin=b.grad_lin)
+        self._span("scatter", t)
+        hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
+        grad_rows, grad_lin = b.grad_rows, b.grad_lin
+        if ws > 1:
+            grad_rows, grad_lin = self._exchange(b)
+        self.step_count += 1
+        t = self._mark()
+        hip_ops.adam_embedding(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.rowmap,
+                               grad_rows, grad_lin, self.step_count, self.lr, self.betas,
+                               self.eps, self.weight_decay)
+        self._span("adam", t)
+        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
+                           self.lr, self.betas, self.eps, self.weight_decay)
+        return b.loss
+
+    def _deepfm_forward_backward(self, x, y, b: _Bufs, E, w, bias, mean_div):
+        mlp, gv, vw = self.model.mlp, self.grad_views, self.views
+        training = self.model.training
+        p0 = float(mlp[2].p) if training else 0.0
+        p1 = float(mlp[5].p) if training else 0.0
+        B = x.shape[0]
+        H1, H2 = b.h1.shape[1], b.h2.shape[1]
+        off = self._drop_counter
+        self._drop_counter += B * (H1 + H2)
+        t = self._mark()
+        fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
+                                err_flag=self.err, out=b.fm)
+        self._span("gather", t)
+        X = fm.emb_out
+        hip_ops.linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
+                       seed=self.seed, offset=off, out=b.h1)
+        hip_ops.linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
+                       seed=self.seed, offset=off + B * H1, out=b.h2)
+        head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
+                                   mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
+        gz, dh2 = head["gz"], head["dh_pre"]
+        # Linear(200,1): dW = gz^T H2, db = sum gz
+        hip_ops.colsum(b.h2, row_w=gz, out=gv["mlp.6.weight"].view(-1))
+        hip_ops.tensor_sum(gz, out=gv["mlp.6.bias"].view(1))
+        # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
+        hip_ops.gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
+                     scale=1.0 / (1.0 - p0), out=b.dh1)
+        hip_ops.gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
+        hip_ops.colsum(dh2, out=gv["mlp.3.bias"])
+        # Linear(F*K,300): dX = dH1 @ W0 (the MLP-input gradient), dW0 = dH1^T X
+        hip_ops.gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
+        hip_ops.gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
+        hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
+        return gz
+
+    def _exchange(self, b: _Bufs):
+        """Sum embedding-row gradients over ranks (deterministic, identical everywhere)."""
+        allreduce_sum_(self.flat_grad, self.group)
+        allreduce_sum_(b.loss, self.group)
+        b.loss.div_(world()[1])
+        U = b.plan.num_unique_host()
+        rows_all, vals_all, lin_all = allgather_sparse_rows(b.plan.unique_rows, b.grad_rows,
+                                                            b.grad_lin, U, self.group)
+        b.gplan.build(rows_all, self.V)
+        hip_ops.segment_sum_rows(b.gplan, vals_all, lin_all, rowmap=self.rowmap, out=b.g_rows,
+                                 out_lin=b.g_lin)
+        return b.g_rows, b.g_lin
+
+    def check_errors(self) -> None:
+        """Raise IndexError if any kernel saw a feature id outside [0, V). Syncs."""
+        hip_ops.check_index_error(self.err)

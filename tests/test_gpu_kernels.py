@@ -1,0 +1,309 @@
+"""GPU parity of the individual libctr_hip.so kernels against the oracle / numpy.
+
+Tolerances (written per test): integer / index work bit-exact; fp32 sums within 1e-5
+relative of an fp64 reference (the north-star bar), with an absolute floor where the
+quantity is a difference of nearly equal terms.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip():
+    from rl_ctr_prediction_amd import hip_ops
+    return hip_ops
+
+
+def _ids(rng, B, F, V, hot=True):
+    x = rng.integers(0, V, size=(B, F))
+    if hot and B > 1 and F > 2:
+        x[:, 0] = min(7, V - 1)
+        x[: B // 2, 1] = min(3, V - 1)
+    return x
+
+
+# ----------------------------------------------------------------- sparse plan ------
+@pytest.mark.parametrize("B,F,V", [(1, 1, 1), (3, 5, 2), (64, 26, 1000), (257, 13, 50),
+                                   (4096, 26, 1_000_000), (1000, 39, 1508), (33, 16, 7)])
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_sparse_plan_bit_exact(cuda, B, F, V, dtype):
+    H = _hip()
+    rng = np.random.default_rng(B * 31 + F)
+    x = _ids(rng, B, F, V)
+    plan = H.SparsePlanBuffers(B * F, cuda).build(torch.tensor(x, dtype=dtype, device=cuda), V)
+    order, rows, pos_seg, uniq, off = O.sparse_plan(x)
+    U = plan.num_unique_host()
+    assert U == uniq.size
+    np.testing.assert_array_equal(plan.sorted_slots.cpu().numpy()[: B * F], order)
+    np.testing.assert_array_equal(plan.sorted_rows.cpu().numpy()[: B * F], rows)
+    np.testing.assert_array_equal(plan.pos_seg.cpu().numpy()[: B * F], pos_seg)
+    np.testing.assert_array_equal(plan.unique_rows.cpu().numpy()[:U], uniq)
+    np.testing.assert_array_equal(plan.seg_offsets.cpu().numpy()[: U + 1], off)
+
+
+def test_sparse_plan_empty(cuda):
+    H = _hip()
+    plan = H.SparsePlanBuffers(0, cuda).build(torch.zeros(0, 26, dtype=torch.int64, device=cuda), 10)
+    assert plan.num_unique_host() == 0
+
+
+# --------------------------------------------------------------- segmented sums -----
+@pytest.mark.parametrize("K", [1, 10, 16, 64, 128])
+@pytest.mark.parametrize("S,V", [(1, 1), (15, 3), (16, 1), (17, 1), (1000, 10), (5000, 4000),
+                                 (20000, 60)])
+def test_segment_sum_rows(cuda, K, S, V):
+    H = _hip()
+    rng = np.random.default_rng(S + K)
+    keys = rng.integers(0, V, size=S)
+    keys[: S // 3] = 0  # one hot row spanning many 16-position chunks
+    vals = rng.standard_normal((S, K)).astype(np.float32)
+    lin = rng.standard_normal(S).astype(np.float32)
+    plan = H.SparsePlanBuffers(S, cuda).build(torch.tensor(keys, dtype=torch.int32, device=cuda), V)
+    rowmap = torch.full((V,), -1, dtype=torch.int32, device=cuda)
+    tv, tl = torch.tensor(vals, device=cuda), torch.tensor(lin, device=cuda)
+    out, out_lin = H.segment_sum_rows(plan, tv, tl, rowmap=rowmap)
+    U = plan.num_unique_host()
+    uniq = np.unique(keys)
+    ref = np.zeros((V, K))
+    np.add.at(ref, keys, vals.astype(np.float64))
+    refl = np.zeros(V)
+    np.add.at(refl, keys, lin.astype(np.float64))
+    got = out[:U].cpu().numpy()
+    scale = np.zeros((V, K))
+    np.add.at(scale, keys, np.abs(vals.astype(np.float64)))
+    np.testing.assert_allclose(got, ref[uniq], rtol=1e-5, atol=1e-6 * (1 + scale[uniq]).max())
+    np.testing.assert_allclose(out_lin[:U].cpu().numpy(), refl[uniq], rtol=1e-5, atol=1e-4)
+    rm = rowmap.cpu().numpy()
+    assert (rm[uniq] == np.arange(U)).all() and (np.delete(rm, uniq) == -1).all()
+    # deterministic: a second run is bitwise identical
+    out2, out_lin2 = H.segment_sum_rows(plan, tv, tl)
+    assert torch.equal(out[:U], out2[:U]) and torch.equal(out_lin[:U], out_lin2[:U])
+
+
+# ------------------------------------------------------------------- FM forward -----
+@pytest.mark.parametrize("K", [10, 16, 64, 128])
+@pytest.mark.parametrize("F", [1, 8, 26, 39, 70])
+def test_fm_forward_vs_oracle(cuda, K, F):
+    H = _hip()
+    V, B = 500, 67
+    rng = np.random.default_rng(K * 100 + F)
+    E = (rng.standard_normal((V, K)) * 0.1).astype(np.float32)
+    w = (rng.standard_normal((V, 1)) * 0.1).astype(np.float32)
+    b = np.array([0.05], np.float32)
+    x = _ids(rng, B, F, V)
+    y = (rng.random(B) < 0.3).astype(np.float32)
+    params = {"feature_embedding.weight": torch.tensor(E), "linear.weight": torch.tensor(w),
+              "bias": torch.tensor(b)}
+    z_ref = O.fm_logit(params, torch.tensor(x)).reshape(-1).double()
+    d = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    r = H.fm_forward(d(x), d(E), d(w), d(b), want_sum=True, want_emb=True, labels=d(y))
+    zt = r.z.cpu().double()
+    # |z| ~ 0.1..1: FM sum-square cancellation bounds the absolute error, not relative
+    np.testing.assert_allclose(zt.numpy(), z_ref.numpy(), rtol=1e-5, atol=2e-6)
+    e = E[x]
+    np.testing.assert_allclose(r.sum_e.cpu().numpy(), e.sum(1), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(r.emb_out.cpu().numpy(), e.reshape(B, -1))
+    p = torch.sigmoid(z_ref.float())
+    np.testing.assert_allclose(r.p.cpu().numpy(), p.numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_fm_forward_saturated_gradient_is_exactly_zero(cuda, golden):
+    H = _hip()
+    g = golden("g_bce.npz")
+    z, y = torch.tensor(g["z"], device=cuda), torch.tensor(g["y"], device=cuda)
+    p, loss, gz = H.bce_sigmoid(z, y)
+    np.testing.assert_allclose(p.cpu().numpy(), g["p"], rtol=1e-6, atol=0)
+    ref_gz = g["gz"]
+    zero = ref_gz == 0
+    assert (gz.cpu().numpy()[zero] == 0).all(), "saturated sigmoid must give a 0 gradient"
+    np.testing.assert_allclose(gz.cpu().numpy(), ref_gz, rtol=2e-5, atol=0)
+    assert loss.mean().item() == pytest.approx(float(g["loss"]), rel=1e-5)
+
+
+def test_out_of_range_ids_flag_not_fault(cuda):
+    H = _hip()
+    V, K = 100, 16
+    E = torch.randn(V, K, device=cuda)
+    w = torch.randn(V, 1, device=cuda)
+    b = torch.zeros(1, device=cuda)
+    x = torch.randint(0, V, (8, 26), device=cuda)
+    x[3, 4] = V + 5
+    x[5, 0] = -1
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    H.fm_forward(x, E, w, b, err_flag=err)
+    with pytest.raises(IndexError):
+        H.check_index_error(err)
+    H.check_index_error(err)  # flag was cleared
+
+
+# ------------------------------------------------------------------------- GEMM -----
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 5, 3), (64, 64, 32), (130, 70, 33),
+                                   (300, 1664, 8192), (8192, 300, 1664), (8192, 1664, 300),
+                                   (512, 200, 300), (4, 1024, 741)])
+def test_gemm_vs_fp64(cuda, ta, tb, M, N, K):
+    H = _hip()
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(K, N, generator=g)
+    a = (A.t() if ta else A).contiguous().to(cuda)
+    b = (Bm.t() if tb else Bm).contiguous().to(cuda)
+    C = H.gemm(a, b, ta, tb).cpu().double()
+    ref = A.double() @ Bm.double()
+    bound = (A.double().abs() @ Bm.double().abs())
+    # fp32 accumulation (exact-fp32 MFMA = a k-ordered fmaf chain): error grows ~sqrt(K)
+    tol = 1e-6 * max(1.0, (K / 1024) ** 0.5)
+    assert ((C - ref).abs() <= tol * bound + 1e-30).all()
+
+
+def test_gemm_epilogues(cuda):
+    H = _hip()
+    g = torch.Generator().manual_seed(0)
+    M, N, K = 512, 300, 128
+    A, W, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    d = lambda t: t.contiguous().to(cuda)  # noqa: E731
+    ref = (A.double() @ W.double().t() + bias.double())
+    y = H.linear(d(A), d(W), d(bias)).cpu().double()
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=1e-5, atol=1e-4)
+    y = H.linear(d(A), d(W), d(bias), relu=True).cpu().double()
+    np.testing.assert_allclose(y.numpy(), ref.clamp(min=0).numpy(), rtol=1e-5, atol=1e-4)
+    yd = H.linear(d(A), d(W), d(bias), relu=True, drop_p=0.2, seed=123).cpu().double()
+    pos = ref > 1e-3
+    kept = (yd[pos] != 0)
+    frac = kept.double().mean().item()
+    assert 0.78 < frac < 0.82, frac  # Bernoulli(0.8) keep rate
+    np.testing.assert_allclose(yd[pos][kept].numpy(), (ref[pos][kept] * 1.25).numpy(), rtol=1e-5,
+                               atol=1e-4)
+    yd2 = H.linear(d(A), d(W), d(bias), relu=True, drop_p=0.2, seed=123).cpu().double()
+    assert torch.equal(yd, yd2)  # stateless mask: same (seed, offset) -> same mask
+    aux = d(yd.float())
+    gm = H.gemm(d(A), d(W), False, True, epi=H.EPI_GRAD_MASK, aux=aux, scale=1.25).cpu().double()
+    refm = torch.where(yd > 0, (A.double() @ W.double().t()) * 1.25, torch.zeros_like(yd))
+    np.testing.assert_allclose(gm.numpy(), refm.numpy(), rtol=1e-5, atol=1e-4)
+
+
+def test_reductions(cuda):
+    H = _hip()
+    g = torch.Generator().manual_seed(1)
+    for M, N in [(1, 1), (8192, 300), (4096, 1), (7, 129), (100000, 3)]:
+        X = torch.randn(M, N, generator=g)
+        w = torch.randn(M, generator=g)
+        c = H.colsum(X.to(cuda), w.to(cuda), scale=0.5).cpu().double()
+        ref = 0.5 * (w.double()[:, None] * X.double()).sum(0)
+        np.testing.assert_allclose(c.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5 * M ** 0.5)
+        s = H.tensor_sum(X.reshape(-1).contiguous().to(cuda), scale=2.0).item()
+        assert s == pytest.approx(2.0 * X.double().sum().item(), rel=1e-5, abs=1e-4 * (M * N) ** 0.5)
+
+
+# ------------------------------------------------------------------------- Adam -----
+def _torch_adam_ref(p0, grads, lr, wd, steps):
+    p = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p], lr=lr, weight_decay=wd)
+    for g in grads[:steps]:
+        p.grad = g.clone()
+        opt.step()
+    st = opt.state[p]
+    return p.detach(), st["exp_avg"], st["exp_avg_sq"]
+
+
+def test_adam_dense_vs_torch_cpu(cuda):
+    H = _hip()
+    g = torch.Generator().manual_seed(2)
+    n = 100003
+    p0 = torch.randn(n, generator=g) * 0.1
+    grads = [torch.randn(n, generator=g) * 1e-3 for _ in range(3)]
+    p, m, v = p0.clone().to(cuda), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    for t in range(3):
+        H.adam_dense(p, grads[t].to(cuda), m, v, t + 1, 1e-3, weight_decay=1e-5)
+    pr, mr, vr = _torch_adam_ref(p0, grads, 1e-3, 1e-5, 3)
+    np.testing.assert_array_equal(m.cpu().numpy(), mr.numpy())  # FMA forms: bit-exact
+    np.testing.assert_array_equal(v.cpu().numpy(), vr.numpy())
+    np.testing.assert_allclose(p.cpu().numpy(), pr.numpy(), rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("K", [10, 16, 64])
+def test_adam_embedding_dense_semantics(cuda, K):
+    """Touched rows get their gradient, untouched rows still move (g = wd*p), as with a
+    dense nn.Embedding gradient + torch.optim.Adam."""
+    H = _hip()
+    g = torch.Generator().manual_seed(K)
+    V = 3001
+    E0 = torch.randn(V, K, generator=g) * 0.1
+    w0 = torch.randn(V, 1, generator=g) * 0.1
+    touched = torch.unique(torch.randint(0, V, (700,), generator=g)).to(torch.int32)
+    U = touched.numel()
+    gr = torch.randn(U, K, generator=g) * 1e-2
+    gl = torch.randn(U, generator=g) * 1e-2
+    dense = torch.zeros(V, K)
+    dense[touched.long()] = gr
+    dense_l = torch.zeros(V, 1)
+    dense_l[touched.long(), 0] = gl
+    E, w = E0.clone().to(cuda), w0.clone().to(cuda).reshape(-1)
+    mE, vE = torch.zeros_like(E), torch.zeros_like(E)
+    mw, vw = torch.zeros_like(w), torch.zeros_like(w)
+    rowmap = torch.full((V,), -1, dtype=torch.int32, device=cuda)
+    rowmap[touched.long().to(cuda)] = torch.arange(U, dtype=torch.int32, device=cuda)
+    H.adam_embedding(E, mE, vE, w, mw, vw, rowmap, gr.to(cuda), gl.to(cuda), 1, 1e-3,
+                     weight_decay=1e-5)
+    assert (rowmap.cpu() == -1).all(), "rowmap must be reset by the Adam pass"
+    Er, _, _ = _torch_adam_ref(E0, [dense], 1e-3, 1e-5, 1)
+    wr, _, _ = _torch_adam_ref(w0, [dense_l], 1e-3, 1e-5, 1)
+    np.testing.assert_allclose(E.cpu().numpy(), Er.numpy(), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(w.cpu().numpy(), wr.numpy().reshape(-1), rtol=1e-6, atol=1e-9)
+    assert not torch.equal(E.cpu()[0], E0[0]) or 0 in touched  # untouched rows moved
+
+
+# --------------------------------------------------------------- Feature_Embedding ---
+def test_feature_embedding_vs_golden(cuda, golden):
+    H = _hip()
+    g = golden("g_fe.npz")
+    out = H.feature_embedding(torch.tensor(g["x"], device=cuda), torch.tensor(g["E"], device=cuda))
+    # pair dots of N(0,1) rows: absolute error scales with sqrt(K)*|e|^2
+    np.testing.assert_allclose(out.cpu().numpy(), g["out"], rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("F,K", [(2, 1), (26, 64), (22, 128), (5, 3)])
+def test_feature_embedding_vs_oracle(cuda, F, K):
+    H = _hip()
+    g = torch.Generator().manual_seed(F * K)
+    V, B = 300, 45
+    E = torch.randn(V, K, generator=g)
+    x = torch.randint(0, V, (B, F), generator=g)
+    out = H.feature_embedding(x.to(cuda), E.to(cuda)).cpu()
+    ref = O.feature_embedding(E.double(), x).float()
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5 * K)
+
+
+# ------------------------------------------------------------------------ REINFORCE ---
+def test_pg_discount_norm_vs_golden(cuda, golden):
+    H = _hip()
+    g = golden("g_pg.npz")
+    r = torch.tensor(g["dn_r"], device=cuda)
+    for gamma in (1.0, 0.9):
+        d64, d32, stats = H.pg_discount_norm(r, gamma)
+        np.testing.assert_allclose(d64.cpu().numpy(), g[f"dn_gamma{gamma}"].reshape(-1),
+                                   rtol=1e-12, atol=1e-12)
+
+
+def test_pg_loss_grad_vs_golden(cuda, golden):
+    H = _hip()
+    g = golden("g_pg.npz")
+    probs = torch.softmax(torch.tensor(g["lf_logits"]), dim=1).to(cuda)
+    loss, dlogits = H.pg_loss_grad(probs, torch.tensor(g["lf_acts"], device=cuda),
+                                   torch.tensor(g["lf_vt"], device=cuda))
+    assert loss.item() == pytest.approx(float(g["lf_loss"]), rel=1e-5)
+    np.testing.assert_allclose(dlogits.cpu().numpy(), g["lf_dlogits"], rtol=1e-5, atol=1e-7)
+
+
+def test_softmax_rows(cuda):
+    H = _hip()
+    x = torch.randn(1000, 5) * 3
+    np.testing.assert_allclose(H.softmax_rows(x.to(cuda)).cpu().numpy(),
+                               torch.softmax(x, 1).numpy(), rtol=1e-5, atol=1e-7)

@@ -1,0 +1,144 @@
+"""The CPU oracle against the reference's golden vectors (tests/golden, captured by
+importing jqsl2012/RL_CTR_Prediction itself). CPU only: this pins the oracle that the
+GPU parity tests then trust."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as O
+
+
+def _params_from(g, prefix, keys_map):
+    return {k: torch.tensor(g[f"{prefix}{src}"]).clone().requires_grad_(True)
+            for k, src in keys_map.items()}
+
+
+@pytest.mark.parametrize("tag", ["small", "sat"])
+def test_fm_matches_reference(golden, tag):
+    g = golden("g_fm.npz")
+    params = {"bias": torch.tensor(g[f"{tag}_b0"]), "linear.weight": torch.tensor(g[f"{tag}_w0"]),
+              "feature_embedding.weight": torch.tensor(g[f"{tag}_E0"])}
+    params = {k: v.clone().requires_grad_(True) for k, v in params.items()}
+    opt = O.make_optimizer(params, 1e-3, 1e-5)
+    for s in range(2):
+        x = torch.tensor(g[f"{tag}_x{s}"])
+        y = torch.tensor(g[f"{tag}_y{s}"])
+        loss, p, gr = O.grads("FM", params, x, y)
+        np.testing.assert_array_equal(p.numpy(), g[f"{tag}_p{s}"])
+        assert loss == pytest.approx(float(g[f"{tag}_loss{s}"]), rel=1e-7, abs=0)
+        np.testing.assert_array_equal(gr["feature_embedding.weight"].numpy(), g[f"{tag}_gE{s}"])
+        np.testing.assert_array_equal(gr["linear.weight"].numpy(), g[f"{tag}_gw{s}"])
+        np.testing.assert_array_equal(gr["bias"].numpy(), g[f"{tag}_gb{s}"])
+        opt.step()
+        np.testing.assert_array_equal(params["feature_embedding.weight"].detach().numpy(),
+                                      g[f"{tag}_E{s + 1}"])
+        np.testing.assert_array_equal(params["linear.weight"].detach().numpy(), g[f"{tag}_w{s + 1}"])
+
+
+def test_deepfm_matches_reference(golden):
+    g = golden("g_deepfm.npz")
+    params = {k: torch.tensor(g[f"init/{k}"]).clone().requires_grad_(True) for k in O.DEEPFM_KEYS}
+    opt = O.make_optimizer(params, 1e-3, 1e-5)
+    for s in range(2):
+        x, y = torch.tensor(g[f"x{s}"]), torch.tensor(g[f"y{s}"])
+        loss, p, gr = O.grads("DeepFM", params, x, y, drop_p=0.0)
+        np.testing.assert_allclose(p.numpy(), g[f"p{s}"], rtol=1e-6, atol=0)
+        assert loss == pytest.approx(float(g[f"loss{s}"]), rel=1e-6)
+        for k in O.DEEPFM_KEYS:
+            np.testing.assert_allclose(gr[k].numpy(), g[f"grad{s}/{k}"], rtol=1e-5, atol=1e-9,
+                                       err_msg=k)
+        opt.step()
+        for k in O.DEEPFM_KEYS:
+            np.testing.assert_allclose(params[k].detach().numpy(), g[f"step{s + 1}/{k}"],
+                                       rtol=1e-6, atol=1e-8, err_msg=k)
+
+
+def test_bce_formula_matches_reference(golden):
+    """The unfused BCE∘sigmoid gradient the kernels implement, in ATen's op order."""
+    g = golden("g_bce.npz")
+    z, y, p_ref = (torch.tensor(g[k]) for k in ("z", "y", "p"))
+    p = p_ref  # torch's own sigmoid output feeds the formulas below
+    n = p.numel()
+    gp = ((p - y) / torch.clamp((1 - p) * p, min=1e-12)) / n
+    gz = gp * (1 - p) * p
+    np.testing.assert_array_equal(gz.numpy(), g["gz"])
+    loss = ((y - 1) * torch.clamp(torch.log1p(-p), min=-100) - y * torch.clamp(torch.log(p), min=-100))
+    assert loss.mean().item() == pytest.approx(float(g["loss"]), rel=1e-6)
+    # saturated logits give an exactly-zero gradient
+    sat = (p == 1.0) | (p == 0.0)
+    assert sat.any() and (torch.tensor(g["gz"])[sat] == 0).all()
+    # the oracle path reproduces it through autograd
+    zz = z.clone().requires_grad_(True)
+    O.bce(torch.sigmoid(zz), y).backward()
+    np.testing.assert_array_equal(zz.grad.numpy(), g["gz"])
+
+
+def test_feature_embedding_matches_reference(golden):
+    g = golden("g_fe.npz")
+    out = O.feature_embedding(torch.tensor(g["E"]), torch.tensor(g["x"]))
+    np.testing.assert_allclose(out.numpy(), g["out"], rtol=1e-6, atol=1e-6)
+
+
+def test_pg_discount_and_norm_matches_reference(golden):
+    g = golden("g_pg.npz")
+    for gamma in (1.0, 0.9):
+        d = O.pg_discount_and_norm(g["dn_r"], gamma)
+        np.testing.assert_array_equal(d, g[f"dn_gamma{gamma}"])
+
+
+def test_pg_discount_and_norm_zero_std_raises():
+    with pytest.raises(FloatingPointError):
+        O.pg_discount_and_norm(np.zeros(5, np.float32), 1.0)
+
+
+def test_pg_loss_and_grad_match_reference(golden):
+    g = golden("g_pg.npz")
+    logits = torch.tensor(g["lf_logits"]).requires_grad_(True)
+    loss = O.pg_loss(torch.softmax(logits, dim=1), torch.tensor(g["lf_acts"]),
+                     torch.tensor(g["lf_vt"]))
+    loss.backward()
+    assert loss.item() == pytest.approx(float(g["lf_loss"]), rel=1e-6)
+    np.testing.assert_allclose(logits.grad.numpy(), g["lf_dlogits"], rtol=1e-5, atol=1e-7)
+
+
+def test_pg_choose_action_matches_reference(golden):
+    g = golden("g_pg.npz")
+    torch.manual_seed(12)
+    acts = O.pg_choose_action(torch.tensor(g["ca_probs"]), 3)
+    np.testing.assert_array_equal(acts.numpy(), g["ca_actions"])
+
+
+def test_sparse_plan_is_a_stable_grouping():
+    rng = np.random.default_rng(0)
+    x = rng.integers(0, 50, size=(37, 11))
+    order, rows, pos_seg, uniq, off = O.sparse_plan(x)
+    flat = x.reshape(-1)
+    assert (np.diff(rows) >= 0).all() and (flat[order] == rows).all()
+    for u, r in enumerate(uniq):
+        seg = order[off[u]:off[u + 1]]
+        assert (flat[seg] == r).all() and (np.diff(seg) > 0).all()  # slot order kept
+        assert (pos_seg[off[u]:off[u + 1]] == u).all()
+    assert off[-1] == flat.size
+
+
+@pytest.mark.parametrize("kind", ["FM", "DeepFM"])
+def test_toy_driver_matches_reference(golden, kind):
+    """C1: the reference's pretrain_main.main on the toy, 5 epochs (dropout p=0)."""
+    ref = golden("g_toy.json")
+    train = np.loadtxt(_toy("train_.txt"), delimiter=",", dtype=np.int64)
+    test = np.loadtxt(_toy("test_.txt"), delimiter=",", dtype=np.int64)
+    hist, params = O.pretrain_run(kind, train, test, ref["V"], ref["K"], ref["epoch"], ref["lr"],
+                                  ref["wd"], ref["batch_size"], seed=1, drop_p=0.0)
+    for h, r in zip(hist, ref[kind]["epochs"]):
+        assert h["train_loss"] == pytest.approx(r["train_loss"], rel=1e-6)
+        assert h["valid_loss"] == pytest.approx(r["valid_loss"], rel=1e-6)
+        assert h["valid_auc"] == pytest.approx(r["valid_auc"], abs=1e-9)
+    for k, s in ref[kind]["state_sums"].items():
+        assert float(params[k].detach().double().sum()) == pytest.approx(s, rel=1e-6, abs=1e-6)
+
+
+def _toy(name):
+    from conftest import GOLDEN
+    return GOLDEN / "toy" / name
