@@ -38,3 +38,23 @@ def cuda():
     from rl_ctr_prediction_amd._lib import lib
     lib.load()  # the HIP library must load: no fallback
     return torch.device("cuda:0")
+
+
+def assert_adam_close(actual, desired, lr, *, rtol=1e-5, atol=2e-7, frac=1e-4, step_frac=1e-2,
+                      err_msg=""):
+    """Parameters after Adam steps: the two-tier parity bar.
+
+    Adam's per-element step lr*m/(sqrt(v)+eps) is invariant to the gradient's scale, so an
+    element whose gradient is a cancellation (terms >> their sum) carries that gradient's
+    relative rounding difference straight into its step. Hence: at least (1 - frac) of
+    the elements within rtol/atol (1e-5 relative, the north-star bar), and EVERY element
+    within step_frac of one Adam step (lr)."""
+    a = np.asarray(actual, dtype=np.float64)
+    d = np.asarray(desired, dtype=np.float64)
+    diff = np.abs(a - d)
+    tight = diff <= atol + rtol * np.abs(d)
+    assert tight.mean() >= 1.0 - frac, (
+        f"{err_msg}: {int((~tight).sum())}/{tight.size} elements outside rtol={rtol} atol={atol}; "
+        f"max diff {diff.max():.3g}")
+    loose = diff <= rtol * np.abs(d) + step_frac * lr
+    assert loose.all(), f"{err_msg}: max diff {diff.max():.3g} > {step_frac} * lr"

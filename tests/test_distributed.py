@@ -1,0 +1,100 @@
+"""Data-parallel exchange on CPU with gloo, world size 2 (the N>1 path's host logic).
+
+Each rank builds the per-row gradient sums of its own batch (the oracle's numpy
+grouping stands in for the GPU scatter kernel), exchanges them with
+allgather_sparse_rows, re-sums by row in (rank, row) order and must obtain the
+gradient of the GLOBAL batch — identical on both ranks. The dense flat buffer goes
+through one all-reduce.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _row_sums(keys, vals, lin):
+    uniq, inv = np.unique(keys, return_inverse=True)
+    out = np.zeros((uniq.size, vals.shape[1]), np.float64)
+    outl = np.zeros(uniq.size, np.float64)
+    np.add.at(out, inv, vals)
+    np.add.at(outl, inv, lin)
+    return uniq, out, outl
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rl_ctr_prediction_amd.distributed import allgather_sparse_rows, allreduce_sum_, world as w
+        assert w() == (rank, world)
+        rng = np.random.default_rng(100 + rank)
+        K = 8
+        n = 300 + 57 * rank                      # ragged: ranks hold different row counts
+        keys = rng.integers(0, 120, size=n)
+        vals = rng.standard_normal((n, K))
+        lin = rng.standard_normal(n)
+        uniq, rs, rl = _row_sums(keys, vals, lin)
+        cap = uniq.size + 5                      # buffers larger than the valid count
+        rows_t = torch.zeros(cap, dtype=torch.int32)
+        rows_t[: uniq.size] = torch.tensor(uniq, dtype=torch.int32)
+        vals_t = torch.zeros(cap, K)
+        vals_t[: uniq.size] = torch.tensor(rs, dtype=torch.float32)
+        lin_t = torch.zeros(cap)
+        lin_t[: uniq.size] = torch.tensor(rl, dtype=torch.float32)
+        r_all, v_all, l_all = allgather_sparse_rows(rows_t, vals_t, lin_t, uniq.size)
+        g_uniq, g_sum, g_lin = _row_sums(r_all.numpy(), v_all.numpy().astype(np.float64),
+                                         l_all.numpy().astype(np.float64))
+        flat = torch.full((1000,), float(rank + 1))
+        allreduce_sum_(flat)
+        q.put((rank, g_uniq, g_sum, g_lin, r_all.numpy(), float(flat[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sparse_exchange_world2_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # expected: the global batch's per-row sums
+    keys, vals, lin = [], [], []
+    for rank in range(world):
+        rng = np.random.default_rng(100 + rank)
+        n = 300 + 57 * rank
+        keys.append(rng.integers(0, 120, size=n))
+        vals.append(rng.standard_normal((n, 8)))
+        lin.append(rng.standard_normal(n))
+    gu, gs, gl = _row_sums(np.concatenate(keys), np.concatenate(vals), np.concatenate(lin))
+    for rank in range(world):
+        u, s, l_, rows_all, flat0 = res[rank]
+        np.testing.assert_array_equal(u, gu)
+        np.testing.assert_allclose(s, gs, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(l_, gl, rtol=1e-5, atol=1e-5)
+        assert flat0 == 3.0  # 1 + 2
+    # both ranks received the same concatenation (rank order), so their re-sums agree bitwise
+    np.testing.assert_array_equal(res[0][3], res[1][3])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
