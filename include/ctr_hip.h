@@ -179,7 +179,8 @@ int ctr_rows_to_dense(const ctr_sparse_plan* plan, int K, const float* grad_rows
  * element (dense semantics). Host-computed step scalars (as torch computes them):
  *   step_size = lr / (1 - beta1^t),  bc2_sqrt = sqrt(1 - beta2^t).
  * Per element: g += wd*p; m += (1-beta1)*(g-m); v = v*beta2 + (1-beta2)*g*g;
- *              p += -step_size * (m / (sqrt(v)/bc2_sqrt + eps)).
+ *              p += -step_size * (m / (sqrt(v)/bc2_sqrt + eps))
+ * (m, v bit-identical to torch's CPU Adam; the p step uses ~1-ulp hardware sqrt/rcp).
  * ctr_adam_dense:     g is a dense gradient (MLP, bias).
  * ctr_adam_embedding: the embedding table E[V,K] and the linear table w[V] in one pass;
  *   the gradient of row r is grad_rows[rowmap[r]] when rowmap[r] >= 0, else 0; rowmap
@@ -193,6 +194,30 @@ int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float
                        const float* grad_rows, const float* grad_lin, double step_size,
                        double bc2_sqrt, double beta1, double beta2, double eps,
                        double weight_decay, ctr_stream_t stream);
+
+/* Deferred-exact dense Adam (temporal blocking) — same results as ctr_adam_embedding,
+ * bitwise. A row absent from a batch is updated with g = wd*p, a function of its own state;
+ * last[r] (int32 [V], 0 at optimizer creation) records the step row r is current to, and
+ * missed steps are replayed in registers with the same per-element arithmetic and the same
+ * per-step scalars step_table[2t] = -lr/(1-beta1^t), step_table[2t+1] = 1/sqrt(1-beta2^t)
+ * (fp32, host-computed in double as torch does; entries 0..step valid):
+ *   ctr_adam_deferred_rows, grad_rows == NULL: bring the plan's unique rows to `step`
+ *     (call before a forward pass reads them; catch-up to the last completed step);
+ *   ctr_adam_deferred_rows, grad_rows != NULL: bring them to step-1 and apply step `step`
+ *     with their gradient (grad_rows[u], grad_lin[u] for unique row u);
+ *   ctr_adam_deferred_flush: bring every row to `step` (before anything else reads the
+ *     tables: epoch end, checkpoint, evaluation).
+ * Replaces: torch.optim.Adam.step at all_main/pretrain_main.py:78 over nn.Embedding weights. */
+int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                           float* v_lin, int64_t V, int K, int32_t* last,
+                           const ctr_sparse_plan* plan, const float* grad_rows,
+                           const float* grad_lin, int64_t step, const float* step_table,
+                           double beta1, double beta2, double eps, double weight_decay,
+                           ctr_stream_t stream);
+int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                            float* v_lin, int64_t V, int K, int32_t* last, int64_t step,
+                            const float* step_table, double beta1, double beta2, double eps,
+                            double weight_decay, ctr_stream_t stream);
 
 /* ------------------------------------------------ A7: Feature_Embedding -------------
  * out[b] = [ <E[x_bi],E[x_bj]> for i<j in row-major pair order ] ++ flat(E[x_b]),

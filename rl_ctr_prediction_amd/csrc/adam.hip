@@ -6,15 +6,26 @@
 // when rowmap[row] >= 0, so the dense pass costs 24 B/elem + 4 B/row, not 32 B/elem.
 //
 // Arithmetic follows torch's single-tensor CPU Adam (torch/optim/adam.py), checked
-// against torch 2.10: m and v bit-exact with the FMA forms below; p to <=1 ulp of the
-// update (torch's vectorised CPU sqrt is not correctly rounded; ours is).
+// against torch 2.10: m and v bit-exact with the FMA forms below; the parameter step to a
+// few ulps of the step (see adam_elem).
+//
+// Deferred-exact mode (temporal blocking). A row absent from a batch gets g = wd*p — a
+// function of its own state only — so its per-step update needs no information from the
+// step it skipped. Instead of streaming all V rows through HBM every step, each row keeps
+// last[r] = the step it is current to; a row is brought forward by replaying the missed
+// steps in registers with the SAME adam_elem and the SAME per-step scalars, (1) before a
+// batch reads it (catch-up, unique rows of the batch), (2) when its gradient is applied
+// (apply), (3) for every row at a flush (epoch end, checkpoint, eval). Every element still
+// receives every step's arithmetic, in order; only the HBM round trips of untouched rows
+// between two uses disappear. Results are bitwise identical to the dense pass
+// (tests/test_gpu_deferred.py).
 #include "ctr_common.h"
 
 namespace ctr {
 
 struct AdamHP {
   float neg_step_size;  // -lr / (1 - beta1^t)
-  float bc2_sqrt;       // sqrt(1 - beta2^t)
+  float inv_bc2_sqrt;   // 1 / sqrt(1 - beta2^t)
   float w1;             // 1 - beta1   (lerp weight)
   float beta2;
   float w2;             // 1 - beta2   (addcmul value)
@@ -22,14 +33,21 @@ struct AdamHP {
   float wd;
 };
 
+// One Adam element update. m and v use torch's own FMA forms (bit-identical to its CPU
+// single-tensor Adam, pinned by tests); the parameter step uses the hardware square root
+// and reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp) instead of IEEE-exact sequences: torch's
+// own CPU sqrt is not correctly rounded either, the step differs by a few ulps of the
+// step (~1e-10 absolute at lr 1e-3), and the replayed (deferred) path stays ~3x cheaper.
+// Every Adam kernel below calls this one function, so the dense and the deferred-exact
+// paths produce bitwise identical tables.
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
                                           const AdamHP& h) {
 #pragma clang fp contract(off)
   g = __builtin_fmaf(h.wd, p, g);                 // grad.add(param, alpha=wd)
   m = __builtin_fmaf(h.w1, g - m, m);             // exp_avg.lerp_(grad, 1-beta1)
   v = __builtin_fmaf(h.w2 * g, g, v * h.beta2);   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;  // (v.sqrt() / bc2_sqrt).add_(eps)
-  p = p + (h.neg_step_size * m) / denom;          // param.addcdiv_(m, denom, value=-ss)
+  const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), h.inv_bc2_sqrt, h.eps);
+  p = __builtin_fmaf(h.neg_step_size * m, __builtin_amdgcn_rcpf(denom), p);  // addcdiv_
 }
 
 __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4& v,
@@ -151,13 +169,142 @@ __global__ __launch_bounds__(256) void adam_embedding_scalar(
   }
 }
 
+// ------------------------------------------------------------ deferred-exact --------
+// step_tab[2t] = -lr/(1-beta1^t), step_tab[2t+1] = 1/sqrt(1-beta2^t)  (host doubles -> f32)
+__device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s) {
+  const float2 v = reinterpret_cast<const float2*>(tab)[s];
+  h.neg_step_size = v.x;
+  h.inv_bc2_sqrt = v.y;
+}
+
+// Rows of a sparse plan (unique rows of a batch). One lane group of K4 lanes per row
+// (float4 columns), 64/K4 rows per wave. APPLY=false: replay to `step` (catch-up before
+// the forward reads the rows). APPLY=true: replay to step-1, then step `step` with the
+// row's gradient. Lane 0 of the group also owns the row's linear weight.
+template <int K4, bool APPLY>
+__global__ __launch_bounds__(256) void deferred_rows_vec(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
+    int32_t* __restrict__ last, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ num_unique, const float4* __restrict__ grows,
+    const float* __restrict__ glin, int step, const float* __restrict__ tab, AdamHP h) {
+  const int c = threadIdx.x % K4;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  const int U = *num_unique;
+  const int target = APPLY ? step - 1 : step;
+  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; u < U; u += groups) {
+    const int64_t r = rows[u];
+    const int from = last[r];
+    if (!APPLY && from >= target) continue;
+    const int64_t e = r * K4 + c;
+    float4 pp = E[e], mm = mE[e], vv = vE[e];
+    float pw = 0.f, mws = 0.f, vws = 0.f;
+    const bool own_lin = w && c == 0;
+    if (own_lin) {
+      pw = w[r]; mws = mw[r]; vws = vw[r];
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = from + 1; s <= target; ++s) {
+      load_step(h, tab, s);
+      adam_vec(pp, z4, mm, vv, h);
+      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
+    }
+    if (APPLY) {
+      load_step(h, tab, step);
+      adam_vec(pp, grows[u * K4 + c], mm, vv, h);
+      if (own_lin) adam_elem(pw, glin[u], mws, vws, h);
+    }
+    E[e] = pp; mE[e] = mm; vE[e] = vv;
+    if (own_lin) {
+      w[r] = pw; mw[r] = mws; vw[r] = vws;
+    }
+    if (c == 0) last[r] = APPLY ? step : target;
+  }
+}
+
+// Every row to `step` (epoch end / checkpoint / eval). Rows already current cost 4 B.
+template <int K4>
+__global__ __launch_bounds__(256) void deferred_flush_vec(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
+  const int c = threadIdx.x % K4;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; r < V; r += groups) {
+    const int from = last[r];
+    if (from >= step) continue;
+    const int64_t e = r * K4 + c;
+    float4 pp = E[e], mm = mE[e], vv = vE[e];
+    float pw = 0.f, mws = 0.f, vws = 0.f;
+    const bool own_lin = w && c == 0;
+    if (own_lin) {
+      pw = w[r]; mws = mw[r]; vws = vw[r];
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = from + 1; s <= step; ++s) {
+      load_step(h, tab, s);
+      adam_vec(pp, z4, mm, vv, h);
+      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
+    }
+    E[e] = pp; mE[e] = mm; vE[e] = vv;
+    if (own_lin) {
+      w[r] = pw; mw[r] = mws; vw[r] = vws;
+    }
+    if (c == 0) last[r] = step;
+  }
+}
+
+// Any K: a thread per row (rows list, or all rows when rows == NULL).
+template <bool APPLY>
+__global__ __launch_bounds__(256) void deferred_scalar(
+    float* __restrict__ E, float* __restrict__ mE, float* __restrict__ vE, float* __restrict__ w,
+    float* __restrict__ mw, float* __restrict__ vw, int64_t n_rows, int K,
+    int32_t* __restrict__ last, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ num_unique, const float* __restrict__ grows,
+    const float* __restrict__ glin, int step, const float* __restrict__ tab, AdamHP h) {
+  const int64_t n = rows ? (int64_t)*num_unique : n_rows;
+  const int target = APPLY ? step - 1 : step;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = rows ? (int64_t)rows[u] : u;
+    const int from = last[r];
+    if (!APPLY && from >= target) continue;
+    for (int k = 0; k < K; ++k) {
+      const int64_t e = r * K + k;
+      float pp = E[e], mm = mE[e], vv = vE[e];
+      for (int s = from + 1; s <= target; ++s) {
+        load_step(h, tab, s);
+        adam_elem(pp, 0.f, mm, vv, h);
+      }
+      if (APPLY) {
+        load_step(h, tab, step);
+        adam_elem(pp, grows[u * K + k], mm, vv, h);
+      }
+      E[e] = pp; mE[e] = mm; vE[e] = vv;
+    }
+    if (w) {
+      float pp = w[r], mm = mw[r], vv = vw[r];
+      for (int s = from + 1; s <= target; ++s) {
+        load_step(h, tab, s);
+        adam_elem(pp, 0.f, mm, vv, h);
+      }
+      if (APPLY) {
+        load_step(h, tab, step);
+        adam_elem(pp, glin[u], mm, vv, h);
+      }
+      w[r] = pp; mw[r] = mm; vw[r] = vv;
+    }
+    last[r] = APPLY ? step : target;
+  }
+}
+
 // Hyper-parameters arrive as doubles, exactly as torch's python code holds them; each is
 // rounded to float once, where ATen casts the python scalar for the fp32 kernel.
 static AdamHP make_hp(double step_size, double bc2_sqrt, double beta1, double beta2, double eps,
                       double wd) {
   AdamHP h;
   h.neg_step_size = (float)(-step_size);
-  h.bc2_sqrt = (float)bc2_sqrt;
+  h.inv_bc2_sqrt = (float)(1.0 / bc2_sqrt);
   h.w1 = (float)(1.0 - beta1);
   h.beta2 = (float)beta2;
   h.w2 = (float)(1.0 - beta2);
@@ -238,5 +385,113 @@ extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float*
   hipLaunchKernelGGL(adam_embedding_scalar, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin, v_lin,
                      V, K, rowmap, grad_rows, grad_lin, h);
   CTR_LAUNCH_CHECK("adam_embedding_scalar");
+  return CTR_OK;
+}
+
+static bool deferred_vec_ok(int K, const void* a, const void* b, const void* c, const void* g) {
+  return K % 4 == 0 && K / 4 <= 64 && (kWave % (K / 4)) == 0 &&
+         ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)g) % 16 == 0;
+}
+
+extern "C" int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, float* lin,
+                                      float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
+                                      const ctr_sparse_plan* plan, const float* grad_rows,
+                                      const float* grad_lin, int64_t step, const float* step_table,
+                                      double beta1, double beta2, double eps, double weight_decay,
+                                      ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && step_table, "ctr_adam_deferred_rows: null pointer");
+  CTR_REQUIRE(plan && plan->unique_rows && plan->num_unique, "ctr_adam_deferred_rows: bad plan");
+  CTR_REQUIRE(V > 0 && K > 0 && step >= 1 && step < (int64_t(1) << 31),
+              "ctr_adam_deferred_rows: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_rows: linear table pointers must be all set or all NULL");
+  CTR_REQUIRE(!grad_rows || !lin || grad_lin, "ctr_adam_deferred_rows: grad_lin missing");
+  if (plan->S == 0) return CTR_OK;
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipStream_t st = as_stream(stream);
+  const bool apply = grad_rows != nullptr;
+  const int64_t n = plan->S;  // upper bound on unique rows
+  if (deferred_vec_ok(K, emb, m_emb, v_emb, grad_rows)) {
+    const int K4 = K / 4;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n * K4, 256), 8192));
+#define CTR_DEF_ROWS(K4_)                                                                        \
+  if (apply)                                                                                     \
+    hipLaunchKernelGGL((deferred_rows_vec<K4_, true>), grid, 256, 0, st,                         \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
+                       plan->unique_rows, plan->num_unique,                                      \
+                       reinterpret_cast<const float4*>(grad_rows), grad_lin, (int)step,          \
+                       step_table, h);                                                           \
+  else                                                                                           \
+    hipLaunchKernelGGL((deferred_rows_vec<K4_, false>), grid, 256, 0, st,                        \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
+                       plan->unique_rows, plan->num_unique, nullptr, nullptr, (int)step,         \
+                       step_table, h)
+    switch (K4) {
+      case 1: CTR_DEF_ROWS(1); break;
+      case 2: CTR_DEF_ROWS(2); break;
+      case 4: CTR_DEF_ROWS(4); break;
+      case 8: CTR_DEF_ROWS(8); break;
+      case 16: CTR_DEF_ROWS(16); break;
+      case 32: CTR_DEF_ROWS(32); break;
+      case 64: CTR_DEF_ROWS(64); break;
+    }
+#undef CTR_DEF_ROWS
+    CTR_LAUNCH_CHECK("deferred_rows_vec");
+    return CTR_OK;
+  }
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), 8192));
+  if (apply)
+    hipLaunchKernelGGL(deferred_scalar<true>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
+                       v_lin, n, K, last, plan->unique_rows, plan->num_unique, grad_rows, grad_lin,
+                       (int)step, step_table, h);
+  else
+    hipLaunchKernelGGL(deferred_scalar<false>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
+                       v_lin, n, K, last, plan->unique_rows, plan->num_unique, nullptr, nullptr,
+                       (int)step, step_table, h);
+  CTR_LAUNCH_CHECK("deferred_scalar");
+  return CTR_OK;
+}
+
+extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, float* lin,
+                                       float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
+                                       int64_t step, const float* step_table, double beta1,
+                                       double beta2, double eps, double weight_decay,
+                                       ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && step_table, "ctr_adam_deferred_flush: null pointer");
+  CTR_REQUIRE(V > 0 && K > 0 && step >= 0 && step < (int64_t(1) << 31),
+              "ctr_adam_deferred_flush: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_flush: linear table pointers must be all set or all NULL");
+  if (step == 0) return CTR_OK;
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipStream_t st = as_stream(stream);
+  if (deferred_vec_ok(K, emb, m_emb, v_emb, nullptr)) {
+    const int K4 = K / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V * K4, 256), 16384);
+#define CTR_DEF_FLUSH(K4_)                                                                      \
+  hipLaunchKernelGGL((deferred_flush_vec<K4_>), grid, 256, 0, st,                               \
+                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
+                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step,   \
+                     step_table, h)
+    switch (K4) {
+      case 1: CTR_DEF_FLUSH(1); break;
+      case 2: CTR_DEF_FLUSH(2); break;
+      case 4: CTR_DEF_FLUSH(4); break;
+      case 8: CTR_DEF_FLUSH(8); break;
+      case 16: CTR_DEF_FLUSH(16); break;
+      case 32: CTR_DEF_FLUSH(32); break;
+      case 64: CTR_DEF_FLUSH(64); break;
+    }
+#undef CTR_DEF_FLUSH
+    CTR_LAUNCH_CHECK("deferred_flush_vec");
+    return CTR_OK;
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
+  hipLaunchKernelGGL(deferred_scalar<false>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
+                     v_lin, V, K, last, nullptr, nullptr, nullptr, nullptr, (int)step, step_table,
+                     h);
+  CTR_LAUNCH_CHECK("deferred_flush_scalar");
   return CTR_OK;
 }

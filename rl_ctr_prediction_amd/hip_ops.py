@@ -17,6 +17,7 @@ __all__ = [
     "embedding_gather", "fm_forward", "bce_sigmoid", "deepfm_head", "gemm", "linear",
     "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
+    "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -334,6 +335,52 @@ def adam_embedding(emb, m_emb, v_emb, lin, m_lin, v_lin, rowmap, grad_rows, grad
     lib.ctr_adam_embedding(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
                            _p(rowmap), _p(grad_rows), _p(grad_lin), ss, bc2s, float(betas[0]),
                            float(betas[1]), float(eps), float(weight_decay), _stream())
+
+
+class AdamStepTable:
+    """Device table of the per-step Adam scalars for the deferred-exact path:
+    tab[2t] = -lr/(1-beta1^t), tab[2t+1] = 1/sqrt(1-beta2^t), computed in python doubles
+    exactly like adam_scalars() (so dense and deferred paths see identical fp32 values)."""
+
+    def __init__(self, lr: float, betas, device, capacity: int = 1024):
+        self.lr, self.betas, self.device = float(lr), tuple(betas), device
+        self.capacity = 0
+        self.tab = torch.zeros(2, dtype=torch.float32, device=device)
+        self.ensure(capacity)
+
+    def ensure(self, step: int) -> torch.Tensor:
+        if step > self.capacity:
+            cap = max(step, 2 * self.capacity, 1024)
+            host = torch.zeros(2 * (cap + 1), dtype=torch.float64)
+            for t in range(1, cap + 1):
+                ss, bc2s = adam_scalars(t, self.lr, self.betas)
+                host[2 * t] = -ss
+                host[2 * t + 1] = 1.0 / bc2s
+            self.tab = host.to(torch.float32).to(self.device)
+            self.capacity = cap
+        return self.tab
+
+
+def adam_deferred_rows(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "SparsePlanBuffers",
+                       step: int, table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8,
+                       weight_decay=0.0, grad_rows=None, grad_lin=None) -> None:
+    """grad_rows None: bring the plan's rows to `step`; else to step-1 and apply `step`."""
+    V, K = emb.shape
+    tab = table.ensure(step)
+    lib.ctr_adam_deferred_rows(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
+                               _p(last), plan.struct(), _p(grad_rows), _p(grad_lin), int(step),
+                               _p(tab), float(betas[0]), float(betas[1]), float(eps),
+                               float(weight_decay), _stream())
+
+
+def adam_deferred_flush(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step: int,
+                        table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8,
+                        weight_decay=0.0) -> None:
+    V, K = emb.shape
+    tab = table.ensure(step)
+    lib.ctr_adam_deferred_flush(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
+                                _p(last), int(step), _p(tab), float(betas[0]), float(betas[1]),
+                                float(eps), float(weight_decay), _stream())
 
 
 # ------------------------------------------------------------- Feature_Embedding ----

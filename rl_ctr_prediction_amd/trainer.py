@@ -13,8 +13,16 @@ Per step, on one HIP stream (all kernels from libctr_hip.so):
            + sigmoid + BCE + dH2) -> GEMM dH1 (mask epilogue) -> GEMM dX -> 3 weight-grad
            GEMMs (split-K, deterministic) + column sums -> sparse plan -> per-row grad
            sums (FM + MLP-input grads) -> Adam(E, w) dense pass -> Adam(flat MLP)
-The dense [V,K] gradient is never materialised: Adam reads a row's gradient through the
-rowmap only for rows present in the batch (24 B/element/step instead of 32).
+The dense [V,K] gradient is never materialised.
+
+Optimizer modes (identical results, bitwise — tests/test_gpu_deferred.py):
+  "deferred" (default): deferred-exact dense Adam (temporal blocking, csrc/adam.hip): the
+      batch's rows are brought up to date before the forward reads them, updated with their
+      gradient after the backward, and every other row replays its missed g = wd*p steps in
+      registers at flush() — called automatically before model.forward / state_dict and by
+      reset_optimizer(), and by the driver at every epoch end.
+  "dense": one streaming pass over all V rows every step (rowmap-gated gradients,
+      24 B/element/step).
 """
 from __future__ import annotations
 
@@ -60,7 +68,8 @@ class FusedCTRTrainer:
     """
 
     def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 0.0,
-                 betas=(0.9, 0.999), eps: float = 1e-8, process_group=None, seed: int | None = None):
+                 betas=(0.9, 0.999), eps: float = 1e-8, process_group=None, seed: int | None = None,
+                 optimizer_mode: str = "deferred"):
         if not isinstance(model, (FM, DeepFM)):
             raise TypeError("FusedCTRTrainer drives FM or DeepFM")
         self.model = model
@@ -94,13 +103,22 @@ class FusedCTRTrainer:
         self.v_E = torch.zeros_like(E.data)
         self.m_w = torch.zeros(self.V, dtype=torch.float32, device=self.device)
         self.v_w = torch.zeros_like(self.m_w)
+        if optimizer_mode not in ("deferred", "dense"):
+            raise ValueError(f"optimizer_mode must be 'deferred' or 'dense', not {optimizer_mode!r}")
+        self.deferred = optimizer_mode == "deferred"
         self.rowmap = torch.full((self.V,), -1, dtype=torch.int32, device=self.device)
+        self.last = torch.zeros(self.V, dtype=torch.int32, device=self.device)
+        self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
+        self._dirty = False
+        if self.deferred:  # nothing may read a table with rows still owed steps
+            model.register_forward_pre_hook(lambda mod, inp: self.flush())
+            model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars: self.flush())
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.step_count = 0
         self._bufs: _Bufs | None = None
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
         self._drop_counter = 0
-        # bench hook: {"adam": [], "gather": [], "scatter": []} -> (start, end) HIP events
+        # bench hook: {"adam": [], "gather": [], "scatter": [], "flush": []} -> (start, end)
         # recorded on the launch stream around those kernels
         self.timing: dict | None = None
 
@@ -111,20 +129,54 @@ class FusedCTRTrainer:
         ev.record()
         return ev
 
-    def _span(self, key, start):
+    def _span(self, key, start, work=None):
         if start is not None:
-            self.timing[key].append((start, self._mark()))
+            self.timing.setdefault(key, []).append((start, self._mark(), work))
+
+    def _gemm(self, *args, **kw):
+        """hip_ops.gemm with a timing span carrying the product's flop count."""
+        t = self._mark()
+        out = hip_ops.gemm(*args, **kw)
+        if t is not None:
+            a, bb = args[0], args[1]
+            ta, tb = kw.get("trans_a", False), kw.get("trans_b", False)
+            M, K = (a.shape[1], a.shape[0]) if ta else a.shape
+            N = bb.shape[0] if tb else bb.shape[1]
+            self._span("gemm", t, 2.0 * M * N * K)
+        return out
+
+    def _linear(self, x, w, b, **kw):
+        t = self._mark()
+        out = hip_ops.linear(x, w, b, **kw)
+        if t is not None:
+            self._span("gemm", t, 2.0 * x.shape[0] * w.shape[0] * x.shape[1])
+        return out
 
     # ----------------------------------------------------------------- optimiser -----
+    def flush(self) -> None:
+        """Bring every embedding row up to the last completed step (deferred mode)."""
+        if self.deferred and self._dirty and self.step_count > 0:
+            t = self._mark()
+            m = self.model
+            hip_ops.adam_deferred_flush(m.feature_embedding.weight.data, self.m_E, self.v_E,
+                                        m.linear.weight.data, self.m_w, self.v_w, self.last,
+                                        self.step_count, self.step_table, self.betas, self.eps,
+                                        self.weight_decay)
+            self._span("flush", t)
+        self._dirty = False
+
     def reset_optimizer(self) -> None:
         """What ``torch.optim.Adam(...)`` re-created every epoch does
         (all_main/pretrain_main.py:153): fresh moments, step 0."""
+        self.flush()
         for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
             t.zero_()
+        self.last.zero_()
         self.step_count = 0
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.Adam-compatible state_dict (parameter order = model.parameters())."""
+        self.flush()
         named = list(self.model.named_parameters())
         m = {n: v for n, v in zip(self.dense_names, self._split(self.m_flat))}
         v = {n: v for n, v in zip(self.dense_names, self._split(self.v_flat))}
@@ -185,6 +237,15 @@ class FusedCTRTrainer:
         m = self.model
         E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
         gv = self.grad_views
+        t_plan = self._mark()
+        b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
+        self._span("scatter", t_plan)
+        if self.deferred and self.step_count > 0:
+            t = self._mark()
+            hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
+                                       b.plan, self.step_count, self.step_table, self.betas,
+                                       self.eps, self.weight_decay)
+            self._span("adam", t)
         if self.kind == "FM":
             t = self._mark()
             hip_ops.fm_forward(x, E, w, bias, want_sum=True, labels=y, mean_div=mean_div,
@@ -195,20 +256,27 @@ class FusedCTRTrainer:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
         hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         t = self._mark()
-        b.plan.build(x, self.V)
-        sparse_rowmap = self.rowmap if ws == 1 else None
+        sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
                                   grad_rows=b.grad_rows, grad_lin=b.grad_lin)
         self._span("scatter", t)
         hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
-        grad_rows, grad_lin = b.grad_rows, b.grad_lin
+        grad_rows, grad_lin, plan = b.grad_rows, b.grad_lin, b.plan
         if ws > 1:
             grad_rows, grad_lin = self._exchange(b)
+            plan = b.gplan
         self.step_count += 1
         t = self._mark()
-        hip_ops.adam_embedding(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.rowmap,
-                               grad_rows, grad_lin, self.step_count, self.lr, self.betas,
-                               self.eps, self.weight_decay)
+        if self.deferred:
+            hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
+                                       plan, self.step_count, self.step_table, self.betas,
+                                       self.eps, self.weight_decay, grad_rows=grad_rows,
+                                       grad_lin=grad_lin)
+            self._dirty = True
+        else:
+            hip_ops.adam_embedding(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.rowmap,
+                                   grad_rows, grad_lin, self.step_count, self.lr, self.betas,
+                                   self.eps, self.weight_decay)
         self._span("adam", t)
         hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
                            self.lr, self.betas, self.eps, self.weight_decay)
@@ -228,10 +296,10 @@ class FusedCTRTrainer:
                                 err_flag=self.err, out=b.fm)
         self._span("gather", t)
         X = fm.emb_out
-        hip_ops.linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
-                       seed=self.seed, offset=off, out=b.h1)
-        hip_ops.linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
-                       seed=self.seed, offset=off + B * H1, out=b.h2)
+        self._linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
+                     seed=self.seed, offset=off, out=b.h1)
+        self._linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
+                     seed=self.seed, offset=off + B * H1, out=b.h2)
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]
@@ -239,13 +307,13 @@ class FusedCTRTrainer:
         hip_ops.colsum(b.h2, row_w=gz, out=gv["mlp.6.weight"].view(-1))
         hip_ops.tensor_sum(gz, out=gv["mlp.6.bias"].view(1))
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
-        hip_ops.gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
-                     scale=1.0 / (1.0 - p0), out=b.dh1)
-        hip_ops.gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
+        self._gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
+                   scale=1.0 / (1.0 - p0), out=b.dh1)
+        self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
         hip_ops.colsum(dh2, out=gv["mlp.3.bias"])
         # Linear(F*K,300): dX = dH1 @ W0 (the MLP-input gradient), dW0 = dH1^T X
-        hip_ops.gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
-        hip_ops.gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
+        self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
+        self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
         hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
         return gz
 
@@ -258,7 +326,8 @@ class FusedCTRTrainer:
         rows_all, vals_all, lin_all = allgather_sparse_rows(b.plan.unique_rows, b.grad_rows,
                                                             b.grad_lin, U, self.group)
         b.gplan.build(rows_all, self.V)
-        hip_ops.segment_sum_rows(b.gplan, vals_all, lin_all, rowmap=self.rowmap, out=b.g_rows,
+        hip_ops.segment_sum_rows(b.gplan, vals_all, lin_all,
+                                 rowmap=None if self.deferred else self.rowmap, out=b.g_rows,
                                  out_lin=b.g_lin)
         return b.g_rows, b.g_lin
 

@@ -58,6 +58,7 @@ def test_fused_fm_two_steps_vs_reference(cuda, golden, tag):
         loss = tr.step(x, y).item()
         assert loss == pytest.approx(float(g[f"{tag}_loss{s}"]), rel=1e-5)
         gE, gw, dense = _fused_grads(tr)
+        tr.flush()  # deferred-exact Adam: bring every row to this step before reading tables
         assert_grad_close(gE, g[f"{tag}_gE{s}"], err_msg="grad E")
         assert_grad_close(gw, g[f"{tag}_gw{s}"], err_msg="grad w")
         assert_grad_close(dense["bias"], g[f"{tag}_gb{s}"], err_msg="grad bias")
@@ -345,6 +346,7 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     lref = O.train_step(kind, params_cpu, opt, torch.tensor(x), torch.tensor(y), drop_p=0.0)
     assert loss == pytest.approx(lref, rel=1e-5)
     gE, gw, dense = _fused_grads(tr)
+    tr.flush()
     assert_grad_close(gE, params_cpu["feature_embedding.weight"].grad.numpy(), err_msg="grad E")
     assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(), err_msg="grad w")
     for k, v in dense.items():
