@@ -117,6 +117,34 @@ def grads(kind: str, params: dict, x, y, drop_p=0.0) -> tuple[float, torch.Tenso
     return loss.item(), p.detach(), {k: v.grad.clone() for k, v in params.items()}
 
 
+def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) -> dict:
+    """Per-element L1 norm of the summands of each embedding-gradient element:
+    A[r,k] = sum over the slots (b,f) with x_bf = r of |d loss / d e_bf,k|, with the FM and
+    the MLP contributions counted separately (the reference sums them as two dense
+    gradients). A row gradient is a sum over up to ~1e3 slot terms; its rounding error is
+    bounded relative to A, not to |g| (cancellation). Dropout off."""
+    B, F = x.shape
+    E = params["feature_embedding.weight"].detach()
+    w = params["linear.weight"].detach()
+    V, K = E.shape
+    e_fm = Fn.embedding(x, E).detach().requires_grad_(True)
+    e_mlp = Fn.embedding(x, E).detach().requires_grad_(True)
+    lw = Fn.embedding(x, w).detach().requires_grad_(True)
+    inter = ((e_fm.sum(dim=1) ** 2) - (e_fm ** 2).sum(dim=1)).sum(dim=1, keepdim=True)
+    z = params["bias"].detach() + lw.sum(dim=1) + inter * 0.5
+    if kind == "DeepFM":
+        det = {k: v.detach() for k, v in params.items()}
+        z = z + mlp(det, e_mlp.reshape(B, -1), 0.0, False)
+    bce(torch.sigmoid(z), y.reshape(-1, 1).float()).backward()
+    flat = x.reshape(-1)
+    terms = e_fm.grad.abs()
+    if e_mlp.grad is not None:
+        terms = terms + e_mlp.grad.abs()
+    A_E = torch.zeros(V, K).index_add_(0, flat, terms.reshape(-1, K))
+    A_w = torch.zeros(V, 1).index_add_(0, flat, lw.grad.abs().reshape(-1, 1))
+    return {"feature_embedding.weight": A_E, "linear.weight": A_w}
+
+
 # ------------------------------------------------------------ scatter grouping -------
 def sparse_plan(x: np.ndarray):
     """Stable grouping of slots by id: (sorted_slots, sorted_rows, pos_seg, unique_rows,

@@ -15,6 +15,8 @@
 // backward the Dropout+ReLU gradient mask read from the saved activation.
 // Long-K products (weight gradients, K = batch) are split over blockIdx.z into fp32
 // slabs and summed in slab order by a second kernel: deterministic, no atomics.
+#include <stdlib.h>
+
 #include "ctr_common.h"
 
 namespace ctr {
@@ -64,21 +66,31 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
+// Global->register staging, built so the loads of k-tile t+1 really overlap the MFMAs of
+// k-tile t: no select or branch touches a loaded value until the LDS store that follows
+// the MFMA loop (a select right after a load makes hipcc wait vmcnt there). Addresses are
+// clamped instead: a row beyond M (or a column beyond N) is read from row 0 — it only
+// feeds C entries that are never stored — and the K tail, which feeds every output, is
+// zeroed at LDS-store time. Per-thread row pointers are computed once; a k-tile step is
+// one pointer increment. VEC: 16-B aligned rows, contiguous extents multiple of 4.
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(GemmArgs a) {
   constexpr int BK = 32;
-  constexpr int PADA = TA ? 4 : 1;
+  constexpr int PADA = TA ? 4 : 1;  // k-major images; odd stride for transposed writes
   constexpr int PADB = TB ? 1 : 4;
   constexpr int SA = BM + PADA, SB = BN + PADB;
   constexpr int WAVES_N = BN / WN;
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;  // 4 waves (1/SIMD) or 8 (2/SIMD)
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int NA = BM * BK / 4 / 256;  // float4 loads per thread per k-tile
-  constexpr int NB = BN * BK / 4 / 256;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  static_assert(NA >= 1 && NB >= 1, "tile too small for 256 threads");
+  constexpr int NA = BM * BK / 4 / NT;  // float4 loads per thread per k-tile
+  constexpr int NB = BN * BK / 4 / NT;
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
+  static_assert(NA >= 1 && NB >= 1, "tile too small for the block");
 
-  __shared__ __attribute__((aligned(16))) float As[BK * SA];
-  __shared__ __attribute__((aligned(16))) float Bs[BK * SB];
+  // two LDS stages: the next k-tile is written while the current one feeds the MFMAs,
+  // one barrier per k-tile
+  __shared__ __attribute__((aligned(16))) float As[2][BK * SA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * SB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -90,108 +102,135 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
   const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
   const int64_t ke = min(a.K, kb + a.k_per_split);
 
-  float4 ra[NA], rb[NB];
+  // per-thread fixed tile coordinates and row pointers (at k = kb)
+  const float* pa[NA];
+  const float* pb[NB];
+  int ka[NA], kbv[NB];  // k offset inside the tile this thread's float4 starts at
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int q = tid + NT * i;
+    if (!TA) {  // A[m][k], k contiguous
+      const int m = q / (BK / 4), k4 = q % (BK / 4);
+      const int64_t gm = m0 + m;
+      ka[i] = k4 * 4;
+      pa[i] = a.A + (gm < a.M ? gm : 0) * a.lda + kb + ka[i];
+    } else {  // A stored [k][m], m contiguous
+      const int k = q / (BM / 4), m4 = q % (BM / 4);
+      const int64_t gm = m0 + m4 * 4;
+      ka[i] = k;
+      pa[i] = a.A + (kb + k) * a.lda + (gm < a.M ? gm : 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int q = tid + NT * i;
+    if (!TB) {  // B[k][n], n contiguous
+      const int k = q / (BN / 4), n4 = q % (BN / 4);
+      const int64_t gn = n0 + n4 * 4;
+      kbv[i] = k;
+      pb[i] = a.B + (kb + k) * a.ldb + (gn < a.N ? gn : 0);
+    } else {  // B stored [n][k] (nn.Linear weight), k contiguous
+      const int n = q / (BK / 4), k4 = q % (BK / 4);
+      const int64_t gn = n0 + n;
+      kbv[i] = k4 * 4;
+      pb[i] = a.B + (gn < a.N ? gn : 0) * a.ldb + kb + kbv[i];
+    }
+  }
+  const int64_t stepA = TA ? BK * a.lda : BK;  // pointer advance per k-tile
+  const int64_t stepB = TB ? BK : BK * a.ldb;
 
-  auto load_tile = [&](int64_t k0) {
+  float4 ra[NA], rb[NB];
+  auto load_tile = [&](int t) {  // k-tile t of this split, rows clamped, K tail not masked
+    const int64_t k0 = kb + (int64_t)t * BK;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int q = tid + 256 * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!TA) {  // A[m][k], k contiguous
-        const int m = q / (BK / 4), k4 = q % (BK / 4);
-        const int64_t gm = m0 + m, gk = k0 + k4 * 4;
-        if (gm < a.M) {
-          const float* src = a.A + gm * a.lda + gk;
-          if (a.vec_a && gk + 3 < ke) {
-            v = *reinterpret_cast<const float4*>(src);
-          } else {
-            if (gk + 0 < ke) v.x = src[0];
-            if (gk + 1 < ke) v.y = src[1];
-            if (gk + 2 < ke) v.z = src[2];
-            if (gk + 3 < ke) v.w = src[3];
-          }
+      const float* p = pa[i] + t * stepA;
+      if (VEC) {
+        // a float4 wholly past the K end reads the split's first tile instead (masked later)
+        const bool okk = k0 + ka[i] < ke;
+        ra[i] = *reinterpret_cast<const float4*>(okk ? p : pa[i]);
+      } else {
+        const int kl0 = (int)(k0 + ka[i] - kb);
+        float4 v;
+        if (!TA) {
+          v.x = (k0 + ka[i] + 0 < ke) ? p[0] : 0.f;
+          v.y = (k0 + ka[i] + 1 < ke) ? p[1] : 0.f;
+          v.z = (k0 + ka[i] + 2 < ke) ? p[2] : 0.f;
+          v.w = (k0 + ka[i] + 3 < ke) ? p[3] : 0.f;
+        } else {
+          const int q = tid + NT * i;
+          const int64_t gm = m0 + (q % (BM / 4)) * 4;
+          const bool okk = k0 + ka[i] < ke;
+          v.x = (okk && gm + 0 < a.M) ? p[0] : 0.f;
+          v.y = (okk && gm + 1 < a.M) ? p[1] : 0.f;
+          v.z = (okk && gm + 2 < a.M) ? p[2] : 0.f;
+          v.w = (okk && gm + 3 < a.M) ? p[3] : 0.f;
         }
-      } else {  // A stored [k][m], m contiguous
-        const int k = q / (BM / 4), m4 = q % (BM / 4);
-        const int64_t gk = k0 + k, gm = m0 + m4 * 4;
-        if (gk < ke) {
-          const float* src = a.A + gk * a.lda + gm;
-          if (a.vec_a && gm + 3 < a.M) {
-            v = *reinterpret_cast<const float4*>(src);
-          } else {
-            if (gm + 0 < a.M) v.x = src[0];
-            if (gm + 1 < a.M) v.y = src[1];
-            if (gm + 2 < a.M) v.z = src[2];
-            if (gm + 3 < a.M) v.w = src[3];
-          }
-        }
+        (void)kl0;
+        ra[i] = v;
       }
-      ra[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int q = tid + 256 * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!TB) {  // B[k][n], n contiguous
-        const int k = q / (BN / 4), n4 = q % (BN / 4);
-        const int64_t gk = k0 + k, gn = n0 + n4 * 4;
-        if (gk < ke) {
-          const float* src = a.B + gk * a.ldb + gn;
-          if (a.vec_b && gn + 3 < a.N) {
-            v = *reinterpret_cast<const float4*>(src);
-          } else {
-            if (gn + 0 < a.N) v.x = src[0];
-            if (gn + 1 < a.N) v.y = src[1];
-            if (gn + 2 < a.N) v.z = src[2];
-            if (gn + 3 < a.N) v.w = src[3];
-          }
+      const float* p = pb[i] + t * stepB;
+      if (VEC) {
+        const bool okk = k0 + kbv[i] < ke;
+        rb[i] = *reinterpret_cast<const float4*>(okk ? p : pb[i]);
+      } else {
+        float4 v;
+        if (TB) {
+          v.x = (k0 + kbv[i] + 0 < ke) ? p[0] : 0.f;
+          v.y = (k0 + kbv[i] + 1 < ke) ? p[1] : 0.f;
+          v.z = (k0 + kbv[i] + 2 < ke) ? p[2] : 0.f;
+          v.w = (k0 + kbv[i] + 3 < ke) ? p[3] : 0.f;
+        } else {
+          const int q = tid + NT * i;
+          const int64_t gn = n0 + (q % (BN / 4)) * 4;
+          const bool okk = k0 + kbv[i] < ke;
+          v.x = (okk && gn + 0 < a.N) ? p[0] : 0.f;
+          v.y = (okk && gn + 1 < a.N) ? p[1] : 0.f;
+          v.z = (okk && gn + 2 < a.N) ? p[2] : 0.f;
+          v.w = (okk && gn + 3 < a.N) ? p[3] : 0.f;
         }
-      } else {  // B stored [n][k] (nn.Linear weight), k contiguous
-        const int n = q / (BK / 4), k4 = q % (BK / 4);
-        const int64_t gn = n0 + n, gk = k0 + k4 * 4;
-        if (gn < a.N) {
-          const float* src = a.B + gn * a.ldb + gk;
-          if (a.vec_b && gk + 3 < ke) {
-            v = *reinterpret_cast<const float4*>(src);
-          } else {
-            if (gk + 0 < ke) v.x = src[0];
-            if (gk + 1 < ke) v.y = src[1];
-            if (gk + 2 < ke) v.z = src[2];
-            if (gk + 3 < ke) v.w = src[3];
-          }
-        }
+        rb[i] = v;
       }
-      rb[i] = v;
     }
   };
 
-  auto store_tile = [&]() {
+  auto store_tile = [&](int buf, int t) {
+    const int64_t k0 = kb + (int64_t)t * BK;
+    float* as = As[buf];
+    float* bs = Bs[buf];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int q = tid + 256 * i;
+      const int q = tid + NT * i;
+      float4 v = ra[i];
+      if (VEC && !(k0 + ka[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // K tail
       if (!TA) {
         const int m = q / (BK / 4), k4 = q % (BK / 4);
-        As[(k4 * 4 + 0) * SA + m] = ra[i].x;
-        As[(k4 * 4 + 1) * SA + m] = ra[i].y;
-        As[(k4 * 4 + 2) * SA + m] = ra[i].z;
-        As[(k4 * 4 + 3) * SA + m] = ra[i].w;
+        as[(k4 * 4 + 0) * SA + m] = v.x;
+        as[(k4 * 4 + 1) * SA + m] = v.y;
+        as[(k4 * 4 + 2) * SA + m] = v.z;
+        as[(k4 * 4 + 3) * SA + m] = v.w;
       } else {
         const int k = q / (BM / 4), m4 = q % (BM / 4);
-        *reinterpret_cast<float4*>(&As[k * SA + m4 * 4]) = ra[i];
+        *reinterpret_cast<float4*>(&as[k * SA + m4 * 4]) = v;
       }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int q = tid + 256 * i;
+      const int q = tid + NT * i;
+      float4 v = rb[i];
+      if (VEC && !(k0 + kbv[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!TB) {
         const int k = q / (BN / 4), n4 = q % (BN / 4);
-        *reinterpret_cast<float4*>(&Bs[k * SB + n4 * 4]) = rb[i];
+        *reinterpret_cast<float4*>(&bs[k * SB + n4 * 4]) = v;
       } else {
         const int n = q / (BK / 4), k4 = q % (BK / 4);
-        Bs[(k4 * 4 + 0) * SB + n] = rb[i].x;
-        Bs[(k4 * 4 + 1) * SB + n] = rb[i].y;
-        Bs[(k4 * 4 + 2) * SB + n] = rb[i].z;
-        Bs[(k4 * 4 + 3) * SB + n] = rb[i].w;
+        bs[(k4 * 4 + 0) * SB + n] = v.x;
+        bs[(k4 * 4 + 1) * SB + n] = v.y;
+        bs[(k4 * 4 + 2) * SB + n] = v.z;
+        bs[(k4 * 4 + 3) * SB + n] = v.w;
       }
     }
   };
@@ -207,30 +246,39 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs a) {
   const int kl = lane >> 5;  // k within the MFMA's K=2
   const int il = lane & 31;
   if (kb < ke) {
-    load_tile(kb);
-    store_tile();
+    const int nt = (int)((ke - kb + BK - 1) / BK);
+    load_tile(0);
+    store_tile(0, 0);
     __syncthreads();
-    for (int64_t k0 = kb; k0 < ke; k0 += BK) {
-      const bool more = k0 + BK < ke;
-      if (more) load_tile(k0 + BK);
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      const bool more = t + 1 < nt;
+      if (more) load_tile(t + 1);  // in flight under the MFMAs below
+      const float* as = As[buf] + kl * SA + wm0 + il;
+      const float* bs = Bs[buf] + kl * SB + wn0 + il;
+      // every fragment of the k-tile is read first; the MFMA chain then only waits for
+      // the reads it consumes (progressive lgkmcnt), not a full LDS round trip per step
+      float af[BK / 2][TM], bf[BK / 2][TN];
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
-        float af[TM], bf[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = As[(kk * 2 + kl) * SA + wm0 + i * 32 + il];
+        for (int i = 0; i < TM; ++i) af[kk][i] = as[kk * 2 * SA + i * 32];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf[j] = Bs[(kk * 2 + kl) * SB + wn0 + j * 32 + il];
+        for (int j = 0; j < TN; ++j) bf[kk][j] = bs[kk * 2 * SB + j * 32];
+      }
+      // keep the reads ahead of the chain: hipcc's scheduler otherwise re-interleaves them
+      // with an lgkmcnt(0) before every MFMA group
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk][i], bf[kk][j], acc[i][j],
+                                                             0, 0, 0);
+      if (more) store_tile(buf ^ 1, t + 1);  // the other stage: last read one barrier ago
       __syncthreads();
-      if (more) {
-        store_tile();
-        __syncthreads();
-      }
     }
   }
 
@@ -266,46 +314,74 @@ struct TileCfg {
   int bm, bn;
   int splits;
   int64_t kps;
+  int waves;  // 4 (one per SIMD) or 8 (two per SIMD)
 };
 
+// Pick (tile, split-K, waves) by a makespan model calibrated on MI355X (tools/gemm_bench.py,
+// profiles/r01_gemm_tuning.txt): every tiling sustains about the same per-CU rate
+// (~0.36 TFLOP/s), so the choice is about load balance — blocks are dealt to 256 CUs in
+// rounds, a round costs one block's flops at that rate plus ~1.5 us of prologue/epilogue,
+// and split-K adds its fp32 slab round trip (2 * splits * M * N * 4 B at ~5 TB/s) and a
+// reduce launch. CTR_GEMM_CFG="bm,bn,splits[,waves]" forces a choice (tuning only).
 static TileCfg choose_tiles(int64_t M, int64_t N, int64_t K) {
-  constexpr int64_t kTarget = 256;  // one workgroup per CU at least
-  const int64_t t128 = ceil_div(M, 128) * ceil_div(N, 128);
-  const int64_t t12864 = ceil_div(M, 128) * ceil_div(N, 64);
-  const int64_t t64128 = ceil_div(M, 64) * ceil_div(N, 128);
-  const int64_t t64 = ceil_div(M, 64) * ceil_div(N, 64);
-  TileCfg c{64, 64, 1, K};
-  int64_t tiles = t64;
-  if (t128 >= kTarget) {
-    c.bm = 128; c.bn = 128; tiles = t128;
-  } else if (t12864 >= kTarget && M >= N) {
-    c.bm = 128; c.bn = 64; tiles = t12864;
-  } else if (t64128 >= kTarget) {
-    c.bm = 64; c.bn = 128; tiles = t64128;
-  }
-  // Few output tiles and a long K (weight gradients: K = batch): split K so the grid
-  // covers the chip; each split keeps >= 512 of K.
-  if (tiles < kTarget && K >= 1024) {
-    int64_t s = std::min<int64_t>(ceil_div(2 * kTarget, tiles), K / 512);
-    s = std::max<int64_t>(1, std::min<int64_t>(s, 64));
-    if (s > 1) {
-      c.kps = align_up(ceil_div(K, s), 32);
-      c.splits = (int)ceil_div(K, c.kps);
+  static const struct { int bm, bn, waves; } cands[] = {
+      {128, 128, 4}, {128, 64, 4}, {64, 128, 4}, {64, 64, 4}, {128, 64, 8}, {64, 128, 8}};
+  const double cu_tflops = 0.36;
+  TileCfg best{64, 64, 1, std::max<int64_t>(K, 1), 4};
+  double best_t = 1e30;
+  if (const char* env = getenv("CTR_GEMM_CFG")) {
+    int bm = 0, bn = 0, sp = 0, wv = 4;
+    const int nf = sscanf(env, "%d,%d,%d,%d", &bm, &bn, &sp, &wv);
+    if (nf >= 3 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && sp >= 1 &&
+        (wv == 4 || (wv == 8 && bm * bn >= 128 * 64))) {
+      TileCfg c{bm, bn, 1, std::max<int64_t>(K, 1), wv};
+      if (sp > 1 && K >= 64) {
+        c.kps = align_up(ceil_div(K, sp), 32);
+        c.splits = (int)ceil_div(K, c.kps);
+      }
+      return c;
     }
   }
-  return c;
+  for (const auto& cd : cands) {
+    const int64_t tiles = ceil_div(M, cd.bm) * ceil_div(N, cd.bn);
+    for (int s = 1; s <= 32; ++s) {
+      if (s > 1 && K / s < 256) break;  // keep >= 8 k-tiles per split
+      const int64_t kps = s == 1 ? K : align_up(ceil_div(K, s), 32);
+      const int splits = s == 1 ? 1 : (int)ceil_div(K, kps);
+      if (splits != s) continue;
+      const int64_t blocks = tiles * splits;
+      const double rounds = (double)ceil_div(blocks, 256);
+      const double t_block = 2.0 * cd.bm * cd.bn * (double)kps / (cu_tflops * 1e6) + 1.5;
+      double t = rounds * t_block;
+      if (splits > 1) t += 2.0 * splits * (double)M * N * 4 / 5e6 + 3.0;  // us
+      if (t < best_t * 0.98) {
+        best_t = t;
+        best = TileCfg{cd.bm, cd.bn, splits, splits > 1 ? kps : std::max<int64_t>(K, 1), cd.waves};
+      }
+    }
+  }
+  return best;
+}
+
+template <int BM, int BN, int WM, int WN, bool VEC>
+static void launch_vec(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  if (!ta && !tb)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, VEC>), grid, NT, 0, st, a);
+  else if (!ta && tb)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true, VEC>), grid, NT, 0, st, a);
+  else if (ta && !tb)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false, VEC>), grid, NT, 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true, VEC>), grid, NT, 0, st, a);
 }
 
 template <int BM, int BN, int WM, int WN>
 static void launch_cfg(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
-  if (!ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false>), grid, 256, 0, st, a);
-  else if (!ta && tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true>), grid, 256, 0, st, a);
-  else if (ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false>), grid, 256, 0, st, a);
+  if (a.vec_a && a.vec_b)
+    launch_vec<BM, BN, WM, WN, true>(a, ta, tb, grid, st);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true>), grid, 256, 0, st, a);
+    launch_vec<BM, BN, WM, WN, false>(a, ta, tb, grid, st);
 }
 
 }  // namespace ctr
@@ -350,8 +426,13 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
   a.drop_thr = (uint32_t)std::min(thr, 4294967295.0);
   a.drop_scale = (float)(1.0 / (1.0 - (double)drop_p));
   a.seed = seed; a.offset = offset;
-  a.vec_a = (reinterpret_cast<uintptr_t>(A) % 16 == 0) && (lda % 4 == 0);
-  a.vec_b = (reinterpret_cast<uintptr_t>(B) % 16 == 0) && (ldb % 4 == 0);
+  // float4 path: 16-B aligned rows whose contiguous extent is a multiple of 4 (then a
+  // float4 is entirely inside or entirely outside the matrix; split-K bounds are
+  // multiples of 32)
+  a.vec_a = (reinterpret_cast<uintptr_t>(A) % 16 == 0) && (lda % 4 == 0) &&
+            ((trans_a ? M : K) % 4 == 0);
+  a.vec_b = (reinterpret_cast<uintptr_t>(B) % 16 == 0) && (ldb % 4 == 0) &&
+            ((trans_b ? K : N) % 4 == 0);
 
   const TileCfg c = choose_tiles(M, N, K);
   a.k_per_split = c.splits > 1 ? c.kps : std::max<int64_t>(K, 1);
@@ -369,7 +450,12 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
   }
   const dim3 grid((unsigned)ceil_div(N, c.bn), (unsigned)ceil_div(M, c.bm), (unsigned)c.splits);
   const bool ta = trans_a != 0, tb = trans_b != 0;
-  if (c.bm == 128 && c.bn == 128) launch_cfg<128, 128, 64, 64>(a, ta, tb, grid, st);
+  if (c.waves == 8) {  // two waves per SIMD: one's LDS-store/barrier phase hides under the
+                      // other's MFMA chain
+    if (c.bm == 128 && c.bn == 128) launch_cfg<128, 128, 64, 32>(a, ta, tb, grid, st);
+    else if (c.bm == 128) launch_cfg<128, 64, 32, 32>(a, ta, tb, grid, st);
+    else launch_cfg<64, 128, 32, 32>(a, ta, tb, grid, st);
+  } else if (c.bm == 128 && c.bn == 128) launch_cfg<128, 128, 64, 64>(a, ta, tb, grid, st);
   else if (c.bm == 128) launch_cfg<128, 64, 64, 32>(a, ta, tb, grid, st);
   else if (c.bn == 128) launch_cfg<64, 128, 32, 64>(a, ta, tb, grid, st);
   else launch_cfg<64, 64, 32, 32>(a, ta, tb, grid, st);

@@ -61,11 +61,18 @@ def assert_adam_close(actual, desired, lr, *, rtol=1e-5, atol=2e-7, frac=1e-3, s
     assert loose.all(), f"{err_msg}: max diff {diff.max():.3g} > {step_frac} * lr"
 
 
-def assert_grad_close(actual, desired, *, rtol=1e-5, atol_frac=1e-6, err_msg=""):
-    """Gradients: 1e-5 relative with an absolute floor of 1e-6 x the tensor's largest
-    magnitude (a row gradient is a sum over up to ~1e3 slot terms; cancellation makes its
-    absolute, not relative, error the meaningful one)."""
+def assert_grad_close(actual, desired, *, rtol=1e-5, atol_frac=1e-6, cond=None, err_msg=""):
+    """Gradients: 1e-5 relative, with an absolute floor of 1e-6 x the tensor's largest
+    magnitude, or — when `cond` (the per-element L1 norm of the summands,
+    oracle.grad_condition) is given — 1e-5 x cond: a row gradient is a sum over up to ~1e3
+    slot terms and, under cancellation, only its error relative to the terms is meaningful."""
     a = np.asarray(actual, dtype=np.float64)
     d = np.asarray(desired, dtype=np.float64)
-    np.testing.assert_allclose(a, d, rtol=rtol, atol=atol_frac * max(np.abs(d).max(), 1e-30),
-                               err_msg=err_msg)
+    if cond is None:
+        np.testing.assert_allclose(a, d, rtol=rtol, atol=atol_frac * max(np.abs(d).max(), 1e-30),
+                                   err_msg=err_msg)
+        return
+    c = np.asarray(cond, dtype=np.float64)
+    bad = np.abs(a - d) > rtol * np.abs(d) + rtol * c + 1e-30
+    assert not bad.any(), (f"{err_msg}: {int(bad.sum())}/{bad.size} outside 1e-5*|g| + 1e-5*sum|terms|; "
+                           f"max excess {np.max(np.abs(a - d) - rtol * np.abs(d) - rtol * c):.3g}")

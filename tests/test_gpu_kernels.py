@@ -224,10 +224,14 @@ def test_adam_dense_vs_torch_cpu(cuda):
     p, m, v = p0.clone().to(cuda), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
     for t in range(3):
         H.adam_dense(p, grads[t].to(cuda), m, v, t + 1, 1e-3, weight_decay=1e-5)
-    pr, mr, vr = _torch_adam_ref(p0, grads, 1e-3, 1e-5, 3)
-    np.testing.assert_array_equal(m.cpu().numpy(), mr.numpy())  # FMA forms: bit-exact
-    np.testing.assert_array_equal(v.cpu().numpy(), vr.numpy())
-    np.testing.assert_allclose(p.cpu().numpy(), pr.numpy(), rtol=1e-6, atol=1e-9)
+        pr, mr, vr = _torch_adam_ref(p0, grads, 1e-3, 1e-5, t + 1)
+        if t == 0:  # same inputs: torch's FMA forms reproduced bit-exactly
+            np.testing.assert_array_equal(m.cpu().numpy(), mr.numpy())
+            np.testing.assert_array_equal(v.cpu().numpy(), vr.numpy())
+        else:  # later steps see p (through wd*p) that differs by a few ulps of the step
+            np.testing.assert_allclose(m.cpu().numpy(), mr.numpy(), rtol=1e-6, atol=1e-12)
+            np.testing.assert_allclose(v.cpu().numpy(), vr.numpy(), rtol=1e-6, atol=1e-18)
+        np.testing.assert_allclose(p.cpu().numpy(), pr.numpy(), rtol=1e-6, atol=1e-9)
 
 
 @pytest.mark.parametrize("K", [10, 16, 64])

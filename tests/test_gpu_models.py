@@ -339,16 +339,19 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
         m.linear.weight.mul_(0.05)
     params_cpu = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
     x, y = next(CriteoSynth(V, F, seed=9).batches(1, B))
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cond = O.grad_condition(kind, params_cpu, torch.tensor(x), torch.tensor(y))
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
     loss = tr.step(torch.tensor(x, device=cuda), torch.tensor(y, device=cuda)).item()
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
     opt = O.make_optimizer(params_cpu, 1e-3, 1e-5)
     lref = O.train_step(kind, params_cpu, opt, torch.tensor(x), torch.tensor(y), drop_p=0.0)
     assert loss == pytest.approx(lref, rel=1e-5)
     gE, gw, dense = _fused_grads(tr)
     tr.flush()
-    assert_grad_close(gE, params_cpu["feature_embedding.weight"].grad.numpy(), err_msg="grad E")
-    assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(), err_msg="grad w")
+    assert_grad_close(gE, params_cpu["feature_embedding.weight"].grad.numpy(),
+                      cond=cond["feature_embedding.weight"].numpy(), err_msg="grad E")
+    assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(),
+                      cond=cond["linear.weight"].numpy(), err_msg="grad w")
     for k, v in dense.items():
         assert_grad_close(v, params_cpu[k].grad.numpy(), err_msg=f"grad {k}")
     E = m.feature_embedding.weight.detach()

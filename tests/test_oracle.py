@@ -142,3 +142,17 @@ def test_toy_driver_matches_reference(golden, kind):
 def _toy(name):
     from conftest import GOLDEN
     return GOLDEN / "toy" / name
+
+
+def test_grad_condition_bounds_the_gradient(golden):
+    """sum|terms| >= |sum terms| elementwise, with equality for single-slot rows."""
+    g = golden("g_fm.npz")
+    params = {"bias": torch.tensor(g["small_b0"]), "linear.weight": torch.tensor(g["small_w0"]),
+              "feature_embedding.weight": torch.tensor(g["small_E0"])}
+    x, y = torch.tensor(g["small_x0"]), torch.tensor(g["small_y0"])
+    A = O.grad_condition("FM", {k: v.clone() for k, v in params.items()}, x, y)
+    gE = torch.tensor(g["small_gE0"]).double()
+    assert (A["feature_embedding.weight"].double() >= gE.abs() * (1 - 1e-6) - 1e-12).all()
+    single = np.bincount(x.reshape(-1).numpy(), minlength=gE.shape[0]) == 1
+    np.testing.assert_allclose(A["feature_embedding.weight"].numpy()[single],
+                               gE.abs().numpy()[single], rtol=1e-6, atol=1e-12)

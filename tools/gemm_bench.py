@@ -1,0 +1,86 @@
+"""Time the DeepFM MLP GEMM shapes (C3: B=8192, 1664-300-200) per tile configuration.
+
+    python tools/gemm_bench.py [--reps 20] [--configs auto,128x128x1,...]
+
+Uses CTR_GEMM_CFG to force a (BM, BN, splits) choice; 'auto' = the built-in chooser.
+Prints one JSON line per (shape, config) with microseconds and TFLOP/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from rl_ctr_prediction_amd import hip_ops as H  # noqa: E402
+
+B = 8192
+SHAPES = {  # name: (M, N, K, trans_a, trans_b)
+    "fwd0 X.W0^T": (B, 300, 1664, False, True),
+    "fwd1 H1.W1^T": (B, 200, 300, False, True),
+    "dH1 dH2.W1": (B, 300, 200, False, False),
+    "dX dH1.W0": (B, 1664, 300, False, False),
+    "dW1 dH2^T.H1": (200, 300, B, True, False),
+    "dW0 dH1^T.X": (300, 1664, B, True, False),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--configs", default="auto,128x128x1,128x128x1x8,128x64x1x8,64x128x1x8,"
+                                         "64x64x1,128x128x4,128x128x4x8,64x64x4,128x64x2x8,"
+                                         "64x128x2x8,128x64x4x8,64x64x8,128x128x16x8,"
+                                         "128x64x8x8,64x128x8x8,64x64x16,128x64x16x8")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    total_best = 0.0
+    for name, (M, N, K, ta, tb) in SHAPES.items():
+        a = torch.randn(*((K, M) if ta else (M, K)), device=dev, generator=g)
+        b = torch.randn(*((N, K) if tb else (K, N)), device=dev, generator=g)
+        out = torch.empty(M, N, device=dev)
+        best = None
+        for cfg in args.configs.split(","):
+            if cfg == "auto":
+                os.environ.pop("CTR_GEMM_CFG", None)
+            else:
+                parts = cfg.split("x")
+                bm, bn, sp = parts[:3]
+                wv = parts[3] if len(parts) > 3 else "4"
+                if int(sp) > 1 and K < 512:
+                    continue
+                os.environ["CTR_GEMM_CFG"] = f"{bm},{bn},{sp},{wv}"
+            for _ in range(3):
+                H.gemm(a, b, ta, tb, out=out)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                H.gemm(a, b, ta, tb, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / args.reps * 1e3
+            tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+            print(json.dumps({"shape": name, "cfg": cfg, "us": round(us, 2), "TFLOPs": round(tf, 1)}),
+                  flush=True)
+            if cfg != "auto" and (best is None or us < best[1]):
+                best = (cfg, us)
+        total_best += best[1]
+        print(json.dumps({"shape": name, "best": best[0], "us": round(best[1], 2)}), flush=True)
+    os.environ.pop("CTR_GEMM_CFG", None)
+    print(json.dumps({"sum_best_us": round(total_best, 1)}))
+    # correctness spot check of the auto path
+    a = torch.randn(513, 300, device=dev)
+    w = torch.randn(200, 300, device=dev)
+    ref = (a.double() @ w.double().t()).float()
+    got = H.gemm(a, w, False, True)
+    print(json.dumps({"check_max_abs_err": float((got - ref).abs().max())}))
+
+
+if __name__ == "__main__":
+    main()
