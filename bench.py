@@ -164,7 +164,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    trainer.timing = {"adam": [], "gather": [], "scatter": [], "flush": [], "gemm": []}
+    trainer.timing = {"adam": [], "gather": [], "plan": [], "scatter": [], "flush": [],
+                      "gemm": []}
     t_start = time.perf_counter()
     for i in range(args.steps):
         trainer.step(xs[i % len(xs)], ys[i % len(ys)])
@@ -204,7 +205,8 @@ def main():
         "gemm_f32_kernel (MLP, fwd+bwd)": {"ms_per_step": per_step["gemm"],
                                            "TFLOP/s": gemm_tfs},
         "gather (fm_forward_vec)": {"ms_per_step": per_step["gather"]},
-        "scatter (plan + fm_embedding_grad)": {"ms_per_step": per_step["scatter"]},
+        "sparse plan (radix sort + scan)": {"ms_per_step": per_step["plan"]},
+        "scatter (fm_embedding_grad segmented sums)": {"ms_per_step": per_step["scatter"]},
     }
     if args.optimizer == "dense" or not deep or per_step["adam"] >= per_step["gemm"]:
         # HBM-bound dense pass (dense mode) or per-step row updates (deferred)
@@ -248,7 +250,8 @@ def main():
         "gather_scatter": {
             "gather_kernel": "fm_forward_vec", "gather_ms": gather_ms,
             "gather_GBps": gather_bytes(S, K, B, deep) / (gather_ms * 1e-3) / 1e9,
-            "scatter_kernels": "sparse plan (radix sort + scan) + fm_embedding_grad",
+            "scatter_kernels": "seg_chunk_kernel + seg_combine_kernel (per-row sums; the "
+                               "sparse plan is timed separately under kernels)",
             "scatter_ms": scatter_ms,
             "scatter_GBps": scatter_bytes(S, K, U, deep) / (scatter_ms * 1e-3) / 1e9,
             "unique_rows_per_batch": U, "slots_per_batch": S},

@@ -223,34 +223,57 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
 }
 
 // Every row to `step` (epoch end / checkpoint / eval). Rows already current cost 4 B.
-template <int K4>
+// The per-step scalars of steps 1..step are staged once per block in LDS (one ds_read_b64
+// per replayed step instead of a dependent global load); the linear table has its own
+// thread-per-row pass (deferred_flush_lin, run first: it reads last[] without writing it).
+constexpr int kMaxLdsSteps = 8192;  // 64 KiB of float2
+
+template <int K4, bool LDS_TAB>
 __global__ __launch_bounds__(256) void deferred_flush_vec(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE, int64_t V,
     int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
+  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
+  if (LDS_TAB) {
+    for (int i = threadIdx.x; i <= step; i += blockDim.x)
+      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
+    __syncthreads();
+  }
   const int c = threadIdx.x % K4;
   const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; r < V; r += groups) {
     const int from = last[r];
     if (from >= step) continue;
     const int64_t e = r * K4 + c;
     float4 pp = E[e], mm = mE[e], vv = vE[e];
-    float pw = 0.f, mws = 0.f, vws = 0.f;
-    const bool own_lin = w && c == 0;
-    if (own_lin) {
-      pw = w[r]; mws = mw[r]; vws = vw[r];
-    }
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int s = from + 1; s <= step; ++s) {
-      load_step(h, tab, s);
+      if (LDS_TAB) {
+        const float2 t = s_tab[s];
+        h.neg_step_size = t.x;
+        h.inv_bc2_sqrt = t.y;
+      } else {
+        load_step(h, tab, s);
+      }
       adam_vec(pp, z4, mm, vv, h);
-      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
     }
     E[e] = pp; mE[e] = mm; vE[e] = vv;
-    if (own_lin) {
-      w[r] = pw; mw[r] = mws; vw[r] = vws;
-    }
     if (c == 0) last[r] = step;
+  }
+}
+
+__global__ __launch_bounds__(256) void deferred_flush_lin(
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    const int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < V;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int from = last[r];
+    if (from >= step) continue;
+    float pp = w[r], mm = mw[r], vv = vw[r];
+    for (int s = from + 1; s <= step; ++s) {
+      load_step(h, tab, s);
+      adam_elem(pp, 0.f, mm, vv, h);
+    }
+    w[r] = pp; mw[r] = mm; vw[r] = vv;
   }
 }
 
@@ -468,13 +491,25 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
   const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
   hipStream_t st = as_stream(stream);
   if (deferred_vec_ok(K, emb, m_emb, v_emb, nullptr)) {
+    if (lin) {  // first: it reads last[] and the E pass below rewrites it
+      const unsigned gl = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
+      hipLaunchKernelGGL(deferred_flush_lin, gl, 256, 0, st, lin, m_lin, v_lin, V, last,
+                         (int)step, step_table, h);
+      CTR_LAUNCH_CHECK("deferred_flush_lin");
+    }
     const int K4 = K / 4;
-    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V * K4, 256), 16384);
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V * K4, 256), 8192);
+    const bool lds = step < kMaxLdsSteps;
+    const size_t lds_bytes = lds ? (size_t)(step + 1) * sizeof(float2) : 0;
 #define CTR_DEF_FLUSH(K4_)                                                                      \
-  hipLaunchKernelGGL((deferred_flush_vec<K4_>), grid, 256, 0, st,                               \
-                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
-                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step,   \
-                     step_table, h)
+  if (lds)                                                                                      \
+    hipLaunchKernelGGL((deferred_flush_vec<K4_, true>), grid, 256, lds_bytes, st,               \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
+                       reinterpret_cast<float4*>(v_emb), V, last, (int)step, step_table, h);    \
+  else                                                                                          \
+    hipLaunchKernelGGL((deferred_flush_vec<K4_, false>), grid, 256, 0, st,                      \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
+                       reinterpret_cast<float4*>(v_emb), V, last, (int)step, step_table, h)
     switch (K4) {
       case 1: CTR_DEF_FLUSH(1); break;
       case 2: CTR_DEF_FLUSH(2); break;

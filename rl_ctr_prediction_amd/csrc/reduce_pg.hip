@@ -27,9 +27,28 @@ __global__ __launch_bounds__(256) void sum_stage1(const float* __restrict__ x, i
   const int64_t lo = blockIdx.x * per_block;
   const int64_t hi = min(n, lo + per_block);
   float acc = 0.f;
+#pragma unroll 8
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += x[i];
   const float r = block_sum_256(acc, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+// One launch for n <= kSmallSum (batch-sized vectors): 1024 threads, fixed order.
+constexpr int64_t kSmallSum = 1 << 16;
+__global__ __launch_bounds__(1024) void sum_small(const float* __restrict__ x, int64_t n,
+                                                  float scale, float* __restrict__ out) {
+  __shared__ float sh[16];
+  float acc = 0.f;
+#pragma unroll 8
+  for (int64_t i = threadIdx.x; i < n; i += 1024) acc += x[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    for (int w2 = 0; w2 < 16; ++w2) r += sh[w2];
+    out[0] = r * scale;
+  }
 }
 
 __global__ __launch_bounds__(256) void sum_stage2(const float* __restrict__ part, int nparts,
@@ -53,8 +72,17 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X
   const int64_t lo = (int64_t)blockIdx.y * rows_per_split;
   const int64_t hi = min(M, lo + rows_per_split);
   float acc = 0.f;
-  if (n < N)
-    for (int64_t m = lo + ry; m < hi; m += 4) acc += (w ? w[m] * X[m * ldx + n] : X[m * ldx + n]);
+  // unrolled so the loads of 8 rows are in flight together (a rolled loop waits one
+  // memory round trip per row); the additions stay in row order (deterministic)
+  if (n < N) {
+    if (w) {
+#pragma unroll 8
+      for (int64_t m = lo + ry; m < hi; m += 4) acc += w[m] * X[m * ldx + n];
+    } else {
+#pragma unroll 8
+      for (int64_t m = lo + ry; m < hi; m += 4) acc += X[m * ldx + n];
+    }
+  }
   sh[ry][cx] = acc;
   __syncthreads();
   if (ry == 0 && n < N) part[blockIdx.y * N + n] = (sh[0][cx] + sh[1][cx]) + (sh[2][cx] + sh[3][cx]);
@@ -66,6 +94,7 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ p
   for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
        n += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
+#pragma unroll 8
     for (int r = 0; r < rs; ++r) s += part[(int64_t)r * N + n];
     out[n] = s * scale;
   }
@@ -228,6 +257,11 @@ extern "C" int ctr_sum_f32(const float* x, int64_t n, float scale, float* out, v
   CTR_REQUIRE(out && n >= 0 && (x || n == 0), "ctr_sum_f32: bad arguments");
   CTR_REQUIRE(ws && ws_bytes >= (int64_t)kSumBlocks * 4, "ctr_sum_f32: workspace too small");
   hipStream_t st = as_stream(stream);
+  if (n <= kSmallSum) {
+    hipLaunchKernelGGL(sum_small, 1, 1024, 0, st, x, n, scale, out);
+    CTR_LAUNCH_CHECK("sum_small");
+    return CTR_OK;
+  }
   const int64_t per = std::max<int64_t>(1, ceil_div(n, kSumBlocks));
   float* part = static_cast<float*>(ws);
   hipLaunchKernelGGL(sum_stage1, kSumBlocks, 256, 0, st, x, n, per, part);

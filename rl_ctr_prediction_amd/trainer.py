@@ -239,7 +239,7 @@ class FusedCTRTrainer:
         gv = self.grad_views
         t_plan = self._mark()
         b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
-        self._span("scatter", t_plan)
+        self._span("plan", t_plan)
         if self.deferred and self.step_count > 0:
             t = self._mark()
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
