@@ -72,6 +72,12 @@ def scatter_bytes(S, K, U, deep):
     return S * (12 + 4 + 4 * K + (4 * K if deep else 0)) + U * (8 * K + 8)
 
 
+def plan_bytes(S, U):
+    """Sparse plan, algorithmic: read the ids (8 B/slot), write sorted slots, sorted rows
+    and slot->segment (12 B/slot), unique rows and segment offsets (8 B/unique)."""
+    return S * 20 + U * 8
+
+
 def cpu_baseline(cfg, batches, max_seconds=25.0):
     """The oracle (torch-CPU restatement, pinned to the reference) on this host."""
     from oracle import ctr_oracle as O
@@ -122,6 +128,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batches", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--breakdown-steps", type=int, default=10,
+                    help="un-timed steps with every kernel group instrumented (kernel table)")
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
@@ -158,14 +166,32 @@ def main():
 
     for i in range(args.warmup):
         trainer.step(xs[i % len(xs)], ys[i % len(ys)])
-    trainer.flush()  # timed region starts from a fully current table
+
+    def total_ms(spans):
+        return float(sum(a.elapsed_time(b) for a, b, _ in spans))
+
+    def avg_ms(spans):
+        return total_ms(spans) / len(spans) if spans else float("nan")
+
+    # breakdown pass (NOT timed): every kernel group bracketed by HIP events, to find the
+    # dominant kernel and report the per-kernel table
+    keys = ("adam", "gather", "plan", "scatter", "flush", "gemm")
+    n_bd = max(1, min(args.steps, args.breakdown_steps))
+    trainer.flush()
+    trainer.timing = {k: [] for k in keys}
+    for i in range(n_bd):
+        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+    trainer.flush()
     torch.cuda.synchronize()
+    bd, trainer.timing = trainer.timing, None
+    per_step = {k: total_ms(v) / n_bd for k, v in bd.items()}
+    dominant = max(("adam", "gather", "plan", "scatter", "gemm"), key=lambda k: per_step[k])
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-
-    trainer.timing = {"adam": [], "gather": [], "plan": [], "scatter": [], "flush": [],
-                      "gemm": []}
+    # timed region: only the dominant kernel (roofline) and the final flush are instrumented
+    trainer.timing = {dominant: [], "flush": []}
     t_start = time.perf_counter()
     for i in range(args.steps):
         trainer.step(xs[i % len(xs)], ys[i % len(ys)])
@@ -184,55 +210,60 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    def total_ms(spans):
-        return float(sum(a.elapsed_time(b) for a, b, _ in spans))
-
-    def avg_ms(spans):
-        return total_ms(spans) / len(spans) if spans else float("nan")
-
     U = trainer._bufs.plan.num_unique_host()
     S = B * F
     deep = cfg["kind"] == "DeepFM"
-    gather_ms, scatter_ms = avg_ms(timing["gather"]), avg_ms(timing["scatter"])
-    per_step = {k: total_ms(v) / args.steps for k, v in timing.items()}
-    gemm_flops = sum(w for _, _, w in timing["gemm"])
-    gemm_tfs = gemm_flops / (total_ms(timing["gemm"]) * 1e-3) / 1e12 if timing["gemm"] else None
+    gemm_flops_bd = sum(w for _, _, w in bd["gemm"])
     kernels = {
+        "_note": f"breakdown pass of {n_bd} un-timed steps (+flush), every group bracketed "
+                 f"by HIP events; ms per step",
         "adam_rows" if args.optimizer == "deferred" else "adam_embedding_vec":
             {"ms_per_step": per_step["adam"]},
-        "flush (deferred_flush_vec, once per timed region)": {"ms_per_step": per_step["flush"],
-                                                             "ms_total": total_ms(timing["flush"])},
-        "gemm_f32_kernel (MLP, fwd+bwd)": {"ms_per_step": per_step["gemm"],
-                                           "TFLOP/s": gemm_tfs},
+        "flush (deferred_flush_vec, once per region)": {"ms_per_step": per_step["flush"]},
+        "gemm_f32_kernel (MLP, fwd+bwd)": {
+            "ms_per_step": per_step["gemm"],
+            "TFLOP/s": gemm_flops_bd / (total_ms(bd["gemm"]) * 1e-3) / 1e12 if bd["gemm"] else None},
         "gather (fm_forward_vec)": {"ms_per_step": per_step["gather"]},
         "sparse plan (radix sort + scan)": {"ms_per_step": per_step["plan"]},
         "scatter (fm_embedding_grad segmented sums)": {"ms_per_step": per_step["scatter"]},
     }
-    if args.optimizer == "dense" or not deep or per_step["adam"] >= per_step["gemm"]:
-        # HBM-bound dense pass (dense mode) or per-step row updates (deferred)
-        adam_ms = avg_ms(timing["adam"])
-        if args.optimizer == "dense":
-            a_bytes = adam_bytes(V, K, U)
-            kname = "adam_embedding_vec (dense Adam over E[V,K] + w[V])"
-        else:  # catch-up + apply of the batch's U rows: read+write p,m,v + grad rows
-            a_bytes = 2 * U * 24 * (K + 1) + U * (4 * K + 8)
-            kname = "deferred_rows_vec (catch-up + apply of the batch's rows)"
-        achieved = a_bytes / (adam_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config, "adam_embedding_vec") \
-            if args.optimizer == "dense" else (None, None)
-        roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                    "traffic_source": traffic_src, "algorithmic_bytes_per_launch": a_bytes,
-                    "avg_launch_ms": adam_ms}
+    spans = timing[dominant]
+    launch_ms = avg_ms(spans)
+    if dominant == "gemm":
+        flops = sum(w for _, _, w in spans) / len(spans)
+        achieved = flops / (launch_ms * 1e-3) / 1e12
+        roofline = {"kernel": "gemm_f32_kernel (fp32 MFMA 32x32x2; the 6 MLP GEMMs of a step, "
+                              "averaged per launch)",
+                    "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
+                    "algorithmic_flops_per_launch": flops}
+        traffic, src = load_traffic(args.config, "gemm_f32_kernel")
     else:
-        gemm_ms = avg_ms(timing["gemm"])
-        flops = gemm_flops / len(timing["gemm"])
-        roofline = {"kernel": "gemm_f32_kernel (fp32 MFMA 32x32x2, the 7 MLP GEMMs of a step)",
-                    "bound": "mfma", "achieved": gemm_tfs, "peak": MFMA_F32_PEAK_TFS,
-                    "unit": "TFLOP/s", "frac": gemm_tfs / MFMA_F32_PEAK_TFS,
-                    "traffic": load_traffic(args.config, "gemm_f32_kernel")[0],
-                    "traffic_source": load_traffic(args.config, "gemm_f32_kernel")[1],
-                    "algorithmic_flops_per_launch": flops, "avg_launch_ms": gemm_ms}
+        if dominant == "adam":
+            if args.optimizer == "dense":
+                nbytes = adam_bytes(V, K, U)
+                kname = "adam_embedding_vec (dense Adam over E[V,K] + w[V])"
+            else:  # catch-up or apply of the batch's U rows: read+write p,m,v (+grad rows)
+                nbytes = U * 24 * (K + 1) + U * (4 * K + 8) // 2
+                kname = "deferred_rows_vec (catch-up / apply of the batch's rows, per launch)"
+        elif dominant == "gather":
+            nbytes, kname = gather_bytes(S, K, B, deep), "fm_forward_vec (embedding gather + FM)"
+        elif dominant == "scatter":
+            nbytes = scatter_bytes(S, K, U, deep)
+            kname = "seg_chunk_kernel + seg_combine_kernel (per-row gradient sums)"
+        else:
+            nbytes = plan_bytes(S, U)
+            kname = "sparse plan (keys + radix sort + scan + scatter)"
+        achieved = nbytes / (launch_ms * 1e-3) / 1e9
+        roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_launch": nbytes}
+        traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec"}.get(dominant, dominant))
+    roofline.update({"traffic": traffic, "traffic_source": src, "avg_launch_ms": launch_ms,
+                     "launches_timed": len(spans)})
+    kernels["flush (deferred_flush_vec, once per region)"]["timed_region_ms_total"] = \
+        total_ms(timing["flush"])
+    gather_ms, scatter_ms = avg_ms(bd["gather"]), avg_ms(bd["scatter"])
     value = world * B * args.steps / elapsed
     result = {
         "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,

@@ -118,30 +118,35 @@ def grads(kind: str, params: dict, x, y, drop_p=0.0) -> tuple[float, torch.Tenso
 
 
 def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) -> dict:
-    """Per-element L1 norm of the summands of each embedding-gradient element:
-    A[r,k] = sum over the slots (b,f) with x_bf = r of |d loss / d e_bf,k|, with the FM and
-    the MLP contributions counted separately (the reference sums them as two dense
-    gradients). A row gradient is a sum over up to ~1e3 slot terms; its rounding error is
-    bounded relative to A, not to |g| (cancellation). Dropout off."""
+    """Per-element L1 norm of the products summed into each embedding-gradient element.
+
+    The reference's gradient of slot (b,f) is g_b*s_bk - g_b*e_bfk (FM, two rounded
+    products; g = dL/dz, s = sum_f e) plus the MLP-input gradient; a row sums these over up
+    to ~1e3 slots. Both cancellations (inside a slot term and across slots) make the
+    rounding error of g[r,k] proportional to A[r,k] = sum over the row's slots of
+    |g_b*s_bk| + |g_b*e_bfk| + |mlp_bfk|, not to |g[r,k]|. Dropout off."""
     B, F = x.shape
     E = params["feature_embedding.weight"].detach()
     w = params["linear.weight"].detach()
     V, K = E.shape
-    e_fm = Fn.embedding(x, E).detach().requires_grad_(True)
-    e_mlp = Fn.embedding(x, E).detach().requires_grad_(True)
-    lw = Fn.embedding(x, w).detach().requires_grad_(True)
-    inter = ((e_fm.sum(dim=1) ** 2) - (e_fm ** 2).sum(dim=1)).sum(dim=1, keepdim=True)
-    z = params["bias"].detach() + lw.sum(dim=1) + inter * 0.5
+    e = Fn.embedding(x, E)
+    e_mlp = e.clone().requires_grad_(True)
+    lw = Fn.embedding(x, w).detach()
+    s = e.sum(dim=1)
+    inter = ((s ** 2) - (e ** 2).sum(dim=1)).sum(dim=1, keepdim=True)
+    z = (params["bias"].detach() + lw.sum(dim=1) + inter * 0.5).requires_grad_(True)
+    zt = z
     if kind == "DeepFM":
         det = {k: v.detach() for k, v in params.items()}
-        z = z + mlp(det, e_mlp.reshape(B, -1), 0.0, False)
-    bce(torch.sigmoid(z), y.reshape(-1, 1).float()).backward()
-    flat = x.reshape(-1)
-    terms = e_fm.grad.abs()
+        zt = z + mlp(det, e_mlp.reshape(B, -1), 0.0, False)
+    bce(torch.sigmoid(zt), y.reshape(-1, 1).float()).backward()
+    g = z.grad.reshape(B, 1, 1)                                   # dL/dz per example
+    terms = (g * s.unsqueeze(1)).abs() + (g * e).abs()            # [B,F,K]
     if e_mlp.grad is not None:
         terms = terms + e_mlp.grad.abs()
+    flat = x.reshape(-1)
     A_E = torch.zeros(V, K).index_add_(0, flat, terms.reshape(-1, K))
-    A_w = torch.zeros(V, 1).index_add_(0, flat, lw.grad.abs().reshape(-1, 1))
+    A_w = torch.zeros(V, 1).index_add_(0, flat, g.reshape(B, 1).abs().expand(B, F).reshape(-1, 1))
     return {"feature_embedding.weight": A_E, "linear.weight": A_w}
 
 

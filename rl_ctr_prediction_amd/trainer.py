@@ -118,12 +118,13 @@ class FusedCTRTrainer:
         self._bufs: _Bufs | None = None
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
         self._drop_counter = 0
-        # bench hook: {"adam": [], "gather": [], "scatter": [], "flush": []} -> (start, end)
-        # recorded on the launch stream around those kernels
+        # bench hook: {"adam": [], "gather": [], ...} -> [(start, end, work)] HIP events
+        # recorded on the launch stream around those kernels; only the keys present in the
+        # dict are instrumented (each event is a queue packet: keep the timed region lean)
         self.timing: dict | None = None
 
-    def _mark(self):
-        if self.timing is None:
+    def _mark(self, key):
+        if self.timing is None or key not in self.timing:
             return None
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
@@ -131,11 +132,13 @@ class FusedCTRTrainer:
 
     def _span(self, key, start, work=None):
         if start is not None:
-            self.timing.setdefault(key, []).append((start, self._mark(), work))
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.timing[key].append((start, ev, work))
 
     def _gemm(self, *args, **kw):
         """hip_ops.gemm with a timing span carrying the product's flop count."""
-        t = self._mark()
+        t = self._mark("gemm")
         out = hip_ops.gemm(*args, **kw)
         if t is not None:
             a, bb = args[0], args[1]
@@ -146,7 +149,7 @@ class FusedCTRTrainer:
         return out
 
     def _linear(self, x, w, b, **kw):
-        t = self._mark()
+        t = self._mark("gemm")
         out = hip_ops.linear(x, w, b, **kw)
         if t is not None:
             self._span("gemm", t, 2.0 * x.shape[0] * w.shape[0] * x.shape[1])
@@ -156,7 +159,7 @@ class FusedCTRTrainer:
     def flush(self) -> None:
         """Bring every embedding row up to the last completed step (deferred mode)."""
         if self.deferred and self._dirty and self.step_count > 0:
-            t = self._mark()
+            t = self._mark("flush")
             m = self.model
             hip_ops.adam_deferred_flush(m.feature_embedding.weight.data, self.m_E, self.v_E,
                                         m.linear.weight.data, self.m_w, self.v_w, self.last,
@@ -237,17 +240,17 @@ class FusedCTRTrainer:
         m = self.model
         E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
         gv = self.grad_views
-        t_plan = self._mark()
+        t_plan = self._mark("plan")
         b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
         self._span("plan", t_plan)
         if self.deferred and self.step_count > 0:
-            t = self._mark()
+            t = self._mark("adam")
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                        b.plan, self.step_count, self.step_table, self.betas,
                                        self.eps, self.weight_decay)
             self._span("adam", t)
         if self.kind == "FM":
-            t = self._mark()
+            t = self._mark("gather")
             hip_ops.fm_forward(x, E, w, bias, want_sum=True, labels=y, mean_div=mean_div,
                                want_p=False, err_flag=self.err, out=b.fm)
             self._span("gather", t)
@@ -255,7 +258,7 @@ class FusedCTRTrainer:
         else:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
         hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
-        t = self._mark()
+        t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
                                   grad_rows=b.grad_rows, grad_lin=b.grad_lin)
@@ -266,7 +269,7 @@ class FusedCTRTrainer:
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
         self.step_count += 1
-        t = self._mark()
+        t = self._mark("adam")
         if self.deferred:
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                        plan, self.step_count, self.step_table, self.betas,
@@ -291,7 +294,7 @@ class FusedCTRTrainer:
         H1, H2 = b.h1.shape[1], b.h2.shape[1]
         off = self._drop_counter
         self._drop_counter += B * (H1 + H2)
-        t = self._mark()
+        t = self._mark("gather")
         fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
                                 err_flag=self.err, out=b.fm)
         self._span("gather", t)

@@ -145,14 +145,26 @@ def _toy(name):
 
 
 def test_grad_condition_bounds_the_gradient(golden):
-    """sum|terms| >= |sum terms| elementwise, with equality for single-slot rows."""
+    """A = sum of |g*s| + |g*e| over a row's slots bounds |grad| elementwise, and for a
+    single-slot row equals |g|*(|s|+|e|) of that slot."""
     g = golden("g_fm.npz")
     params = {"bias": torch.tensor(g["small_b0"]), "linear.weight": torch.tensor(g["small_w0"]),
               "feature_embedding.weight": torch.tensor(g["small_E0"])}
     x, y = torch.tensor(g["small_x0"]), torch.tensor(g["small_y0"])
     A = O.grad_condition("FM", {k: v.clone() for k, v in params.items()}, x, y)
+    AE = A["feature_embedding.weight"].double()
     gE = torch.tensor(g["small_gE0"]).double()
-    assert (A["feature_embedding.weight"].double() >= gE.abs() * (1 - 1e-6) - 1e-12).all()
-    single = np.bincount(x.reshape(-1).numpy(), minlength=gE.shape[0]) == 1
-    np.testing.assert_allclose(A["feature_embedding.weight"].numpy()[single],
-                               gE.abs().numpy()[single], rtol=1e-6, atol=1e-12)
+    assert (AE >= gE.abs() * (1 - 1e-6) - 1e-12).all()
+    # single-slot rows: recompute the two products directly
+    E = params["feature_embedding.weight"].double()
+    e = E[x]                                            # [B,F,K]
+    s = e.sum(1, keepdim=True)
+    zp = (params["bias"].double() + params["linear.weight"].double()[x].sum((1, 2))
+          + 0.5 * ((s.squeeze(1) ** 2) - (e ** 2).sum(1)).sum(1))
+    p = torch.sigmoid(zp)
+    gz = (p - y.double().reshape(-1)) / x.shape[0]
+    expect = gz.abs().view(-1, 1, 1) * (s.abs() + e.abs())
+    flat = x.reshape(-1).numpy()
+    single = np.bincount(flat, minlength=gE.shape[0]) == 1
+    want = torch.zeros_like(AE).index_add_(0, x.reshape(-1), expect.reshape(-1, E.shape[1]))
+    np.testing.assert_allclose(AE.numpy()[single], want.numpy()[single], rtol=1e-4, atol=1e-12)

@@ -36,7 +36,15 @@ def main():
                                          "64x64x1,128x128x4,128x128x4x8,64x64x4,128x64x2x8,"
                                          "64x128x2x8,128x64x4x8,64x64x8,128x128x16x8,"
                                          "128x64x8x8,64x128x8x8,64x64x16,128x64x16x8")
+    ap.add_argument("--square", type=int, default=0,
+                    help="time only an NxNxN NN product (kernel's intrinsic rate)")
     args = ap.parse_args()
+    if args.square:
+        n = args.square
+        SHAPES.clear()
+        SHAPES[f"square {n}"] = (n, n, n, False, False)
+        SHAPES[f"square {n} NT"] = (n, n, n, False, True)
+        SHAPES[f"square {n} TN"] = (n, n, n, True, False)
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     total_best = 0.0
