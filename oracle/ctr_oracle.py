@@ -118,19 +118,22 @@ def grads(kind: str, params: dict, x, y, drop_p=0.0) -> tuple[float, torch.Tenso
 
 
 def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) -> dict:
-    """Per-element L1 norm of the products summed into each embedding-gradient element.
+    """First-order L1 condition of each embedding-gradient element: the sum of |summand|
+    over every rounded operation that feeds it, so |fp32 error| <= ~u * A regardless of
+    cancellation (used as the parity scale of a gradient, tests/conftest.py).
 
-    The reference's gradient of slot (b,f) is g_b*s_bk - g_b*e_bfk (FM, two rounded
-    products; g = dL/dz, s = sum_f e) plus the MLP-input gradient; a row sums these over up
-    to ~1e3 slots. Both cancellations (inside a slot term and across slots) make the
-    rounding error of g[r,k] proportional to A[r,k] = sum over the row's slots of
-    |g_b*s_bk| + |g_b*e_bfk| + |mlp_bfk|, not to |g[r,k]|. Dropout off."""
+    The reference's gradient of slot (b,f) is g_b*s_bk - g_b*e_bfk (FM; g = dL/dz,
+    s = sum_f e: a K-column sum whose own rounding depends on summation order, so its
+    condition is sum_f |e_bfk|, not |s_bk|) plus the MLP-input gradient dX = dH1 @ W0 with
+    dH1 = mask * (dH2 @ W1) (condition |dH2| @ |W1| @ |W0| through the ReLU mask); a row
+    sums these over up to ~1e4 slots, so
+    A[r,k] = sum over the row's slots of |g_b|*sum_f|e_bfk| + |g_b*e_bfk| + mlp_cond_bfk.
+    Dropout off."""
     B, F = x.shape
     E = params["feature_embedding.weight"].detach()
     w = params["linear.weight"].detach()
     V, K = E.shape
     e = Fn.embedding(x, E)
-    e_mlp = e.clone().requires_grad_(True)
     lw = Fn.embedding(x, w).detach()
     s = e.sum(dim=1)
     inter = ((s ** 2) - (e ** 2).sum(dim=1)).sum(dim=1, keepdim=True)
@@ -138,12 +141,16 @@ def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) ->
     zt = z
     if kind == "DeepFM":
         det = {k: v.detach() for k, v in params.items()}
-        zt = z + mlp(det, e_mlp.reshape(B, -1), 0.0, False)
+        h1 = Fn.relu(Fn.linear(e.reshape(B, -1), det["mlp.0.weight"], det["mlp.0.bias"]))
+        h2 = Fn.relu(Fn.linear(h1, det["mlp.3.weight"], det["mlp.3.bias"]))
+        zt = z + Fn.linear(h2, det["mlp.6.weight"], det["mlp.6.bias"])
     bce(torch.sigmoid(zt), y.reshape(-1, 1).float()).backward()
     g = z.grad.reshape(B, 1, 1)                                   # dL/dz per example
-    terms = (g * s.unsqueeze(1)).abs() + (g * e).abs()            # [B,F,K]
-    if e_mlp.grad is not None:
-        terms = terms + e_mlp.grad.abs()
+    terms = g.abs() * e.abs().sum(dim=1, keepdim=True) + (g * e).abs()   # [B,F,K]
+    if kind == "DeepFM":
+        dh2 = (g.reshape(B, 1) * det["mlp.6.weight"]).abs() * (h2 > 0)      # [B,200]
+        c1 = (dh2 @ det["mlp.3.weight"].abs()) * (h1 > 0)                  # [B,300]
+        terms = terms + (c1 @ det["mlp.0.weight"].abs()).reshape(B, F, K)
     flat = x.reshape(-1)
     A_E = torch.zeros(V, K).index_add_(0, flat, terms.reshape(-1, K))
     A_w = torch.zeros(V, 1).index_add_(0, flat, g.reshape(B, 1).abs().expand(B, F).reshape(-1, 1))

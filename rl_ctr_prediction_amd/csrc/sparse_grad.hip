@@ -2,106 +2,18 @@
 //
 // The reference's autograd writes a DENSE [V,K] gradient (embedding_dense_backward
 // accumulates the slots of each row in slot order). Here a batch's S = B*F slots are
-// grouped once per step into a sparse plan — a stable radix sort of (row, slot) pairs,
-// then segment heads and a scan — and each row's contributions are summed in slot order.
+// grouped once per step into a sparse plan (csrc/sparse_plan.hip: a stable radix sort of
+// (row, slot) pairs, then segment heads) and each row's contributions are summed in slot
+// order.
 // Hot rows (Zipf ids: one row can own >1000 slots of a batch) are split into fixed
 // 16-position chunks so every lane group does equal work; chunk partials of rows that
 // span chunks are added in chunk order by a second pass. No float atomics anywhere: the
 // result is bitwise reproducible, which is what keeps data-parallel replicas identical.
-#include <hipcub/hipcub.hpp>
-
 #include "ctr_common.h"
 
 namespace ctr {
 
 constexpr int kChunk = 16;  // sorted positions per lane group (SEG_L)
-
-// --------------------------------------------------------------- plan kernels -------
-template <typename IdxT>
-__global__ __launch_bounds__(256) void plan_keys_kernel(const IdxT* __restrict__ idx, int64_t S,
-                                                        int64_t V, uint32_t* __restrict__ keys,
-                                                        int32_t* __restrict__ vals, int32_t* err) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    keys[s] = (uint32_t)load_row(idx, s, V, err);
-    vals[s] = (int32_t)s;
-  }
-}
-
-__global__ __launch_bounds__(256) void plan_heads_kernel(const int32_t* __restrict__ rows,
-                                                         int64_t S, int32_t* __restrict__ heads) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
-       s += (int64_t)gridDim.x * blockDim.x)
-    heads[s] = (s == 0 || rows[s] != rows[s - 1]) ? 1 : 0;
-}
-
-__global__ __launch_bounds__(256) void plan_scatter_kernel(const int32_t* __restrict__ rows,
-                                                           int64_t S, int32_t* __restrict__ pos_seg,
-                                                           int32_t* __restrict__ unique_rows,
-                                                           int32_t* __restrict__ seg_offsets,
-                                                           int32_t* __restrict__ num_unique) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t u = pos_seg[s] - 1;  // inclusive scan of heads -> ordinal
-    pos_seg[s] = u;
-    if (s == 0 || rows[s] != rows[s - 1]) {
-      unique_rows[u] = rows[s];
-      seg_offsets[u] = (int32_t)s;
-    }
-    if (s == S - 1) {
-      *num_unique = u + 1;
-      seg_offsets[u + 1] = (int32_t)S;
-    }
-  }
-}
-
-struct PlanWs {
-  uint32_t* keys_in;
-  int32_t* vals_in;
-  int32_t* heads;
-  void* temp;
-  size_t temp_bytes;
-  size_t total;
-};
-
-static int plan_ws_layout(int64_t S, int end_bit, hipStream_t st, char* base, PlanWs* w) {
-  size_t sort_bytes = 0, scan_bytes = 0;
-  const int n = (int)S;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint32_t*)nullptr,
-                                         (uint32_t*)nullptr, (const int32_t*)nullptr,
-                                         (int32_t*)nullptr, n, 0, end_bit, st) != hipSuccess) {
-    set_error("hipcub SortPairs size query failed");
-    return CTR_ERR_HIP;
-  }
-  if (hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (const int32_t*)nullptr,
-                                       (int32_t*)nullptr, n, st) != hipSuccess) {
-    set_error("hipcub InclusiveSum size query failed");
-    return CTR_ERR_HIP;
-  }
-  size_t off = 0;
-  auto take = [&](size_t bytes) {
-    size_t o = off;
-    off += (size_t)align_up((int64_t)bytes, 256);
-    return o;
-  };
-  const size_t o_keys = take(sizeof(uint32_t) * S);
-  const size_t o_vals = take(sizeof(int32_t) * S);
-  const size_t o_heads = take(sizeof(int32_t) * S);
-  w->temp_bytes = std::max(sort_bytes, scan_bytes);
-  const size_t o_temp = take(w->temp_bytes);
-  w->total = off;
-  w->keys_in = reinterpret_cast<uint32_t*>(base + o_keys);
-  w->vals_in = reinterpret_cast<int32_t*>(base + o_vals);
-  w->heads = reinterpret_cast<int32_t*>(base + o_heads);
-  w->temp = base + o_temp;
-  return CTR_OK;
-}
-
-static int key_bits(int64_t V) {
-  int bits = 1;
-  while (bits < 32 && (int64_t(1) << bits) < V) ++bits;
-  return bits;
-}
 
 // ------------------------------------------------------- segmented row sums ----------
 // Vector width VT (float4 when K % 4 == 0, else float), KV = K / width columns, LPR lanes
@@ -349,63 +261,6 @@ static bool plan_ok(const ctr_sparse_plan* p) {
 }  // namespace ctr
 
 using namespace ctr;
-
-extern "C" int64_t ctr_sparse_plan_workspace_bytes(int64_t S, int64_t V) {
-  if (S < 0 || V <= 0 || S >= (int64_t(1) << 31)) {
-    set_error("ctr_sparse_plan_workspace_bytes: bad sizes");
-    return -1;
-  }
-  PlanWs w;
-  if (plan_ws_layout(std::max<int64_t>(S, 1), key_bits(V), 0, nullptr, &w) != CTR_OK) return -1;
-  return (int64_t)w.total;
-}
-
-extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
-                                     const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,
-                                     int32_t* err_flag, ctr_stream_t stream) {
-  CTR_REQUIRE(plan_ok(plan), "ctr_sparse_plan_build: incomplete plan");
-  CTR_REQUIRE(idx || plan->S == 0, "ctr_sparse_plan_build: null idx");
-  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && plan->S < (int64_t(1) << 31),
-              "ctr_sparse_plan_build: bad sizes");
-  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
-  hipStream_t st = as_stream(stream);
-  const int64_t S = plan->S;
-  if (S == 0) {
-    CTR_HIP_CHECK(hipMemsetAsync(plan->num_unique, 0, sizeof(int32_t), st));
-    CTR_HIP_CHECK(hipMemsetAsync(plan->seg_offsets, 0, sizeof(int32_t), st));
-    return CTR_OK;
-  }
-  const int bits = key_bits(V);
-  PlanWs w;
-  int rc = plan_ws_layout(S, bits, st, static_cast<char*>(ws), &w);
-  if (rc != CTR_OK) return rc;
-  if (!ws || ws_bytes < (int64_t)w.total) {
-    set_error("ctr_sparse_plan_build: workspace %lld < %lld bytes", (long long)ws_bytes,
-              (long long)w.total);
-    return CTR_ERR_WORKSPACE;
-  }
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(S, 256), 4096);
-  if (idx_type == CTR_IDX_I64)
-    hipLaunchKernelGGL(plan_keys_kernel<int64_t>, grid, 256, 0, st,
-                       static_cast<const int64_t*>(idx), S, V, w.keys_in, w.vals_in, err_flag);
-  else
-    hipLaunchKernelGGL(plan_keys_kernel<int32_t>, grid, 256, 0, st,
-                       static_cast<const int32_t*>(idx), S, V, w.keys_in, w.vals_in, err_flag);
-  CTR_LAUNCH_CHECK("plan_keys_kernel");
-  size_t tb = w.temp_bytes;
-  CTR_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(
-      w.temp, tb, (const uint32_t*)w.keys_in, reinterpret_cast<uint32_t*>(plan->sorted_rows),
-      (const int32_t*)w.vals_in, plan->sorted_slots, (int)S, 0, bits, st));
-  hipLaunchKernelGGL(plan_heads_kernel, grid, 256, 0, st, plan->sorted_rows, S, w.heads);
-  CTR_LAUNCH_CHECK("plan_heads_kernel");
-  tb = w.temp_bytes;
-  CTR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(w.temp, tb, (const int32_t*)w.heads,
-                                                 plan->pos_seg, (int)S, st));
-  hipLaunchKernelGGL(plan_scatter_kernel, grid, 256, 0, st, plan->sorted_rows, S, plan->pos_seg,
-                     plan->unique_rows, plan->seg_offsets, plan->num_unique);
-  CTR_LAUNCH_CHECK("plan_scatter_kernel");
-  return CTR_OK;
-}
 
 extern "C" int64_t ctr_segment_workspace_bytes(int64_t S, int K) {
   if (S < 0 || K <= 0) return -1;

@@ -1,0 +1,382 @@
+// Sparse plan of a batch: the stable grouping of the S = B*F slots by
+// embedding row that embedding_dense_backward performs implicitly. Output (ctr_sparse_plan):
+// slots sorted by (row, slot), the sorted rows, each position's segment ordinal, the unique
+// rows in ascending order and their segment offsets — bit-identical to numpy's stable
+// argsort + unique (tests/test_gpu_kernels.py).
+//
+// LSD radix sort, 8-bit digits, ceil(log2 V / 8) passes, two launches per pass and no
+// inter-workgroup hand-off inside a launch (a cross-XCD look-back chain costs ~1 us per hop
+// on gfx950; a kernel boundary ~1.5 us):
+//   radix_hist:    per tile (256 threads x IPT keys) the 256-bin digit histogram, LDS
+//                  integer atomics (order-free, so deterministic counts) -> hist[tile][256]
+//   radix_scatter: each block scans the tile histograms itself (coalesced 1-KB rows, one
+//                  digit per thread) for its global digit bases, ranks its keys stably with
+//                  wave ballots (8 ballots give the lanes holding the same digit; popcount
+//                  below the lane = rank), and scatters (key, slot).
+// Keys of a tile are striped (item i of thread t = tile + i*256 + t), so (item, wave,
+// lane) order is input order and the ranking is stable. Pass 0 reads the feature ids
+// directly (int64 or int32; the slot index is the value), the last pass writes the plan.
+// Then two launches turn the sorted rows into segments (head counts per tile, then a
+// block scan that writes pos_seg / unique_rows / seg_offsets / num_unique).
+#include "ctr_common.h"
+
+namespace ctr {
+
+constexpr int kRadixBits = 8;
+constexpr int kRadix = 1 << kRadixBits;
+constexpr int kSortThreads = 256;
+constexpr int kSortWaves = kSortThreads / kWave;
+
+struct RadixPass {
+  const void* idx;     // pass 0: feature ids
+  int idx_type;
+  int64_t V;
+  const uint32_t* keys_in;
+  const int32_t* vals_in;
+  uint32_t* keys_out;
+  int32_t* vals_out;
+  int32_t* hist;       // [n_tiles][256]
+  int64_t S;
+  int n_tiles;
+  int shift;
+  int32_t* err;
+};
+
+template <bool FIRST>
+__device__ __forceinline__ uint32_t radix_key(const RadixPass& a, int64_t i, int32_t* err) {
+  if (FIRST) {
+    return a.idx_type == CTR_IDX_I64
+               ? (uint32_t)load_row(static_cast<const int64_t*>(a.idx), i, a.V, err)
+               : (uint32_t)load_row(static_cast<const int32_t*>(a.idx), i, a.V, err);
+  }
+  return a.keys_in[i];
+}
+
+template <int IPT, bool FIRST>
+__global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(RadixPass a) {
+  __shared__ int32_t h[kRadix];
+  const int t = threadIdx.x;
+  h[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * (kSortThreads * IPT);
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t e = base + i * kSortThreads + t;
+    if (e < a.S) atomicAdd(&h[(radix_key<FIRST>(a, e, a.err) >> a.shift) & (kRadix - 1)], 1);
+  }
+  __syncthreads();
+  a.hist[(int64_t)blockIdx.x * kRadix + t] = h[t];
+}
+
+// Exclusive scan of one value per thread over the 256-thread block (4 waves).
+__device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t* wave_tot) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int32_t x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wave_tot[w] = x;
+  __syncthreads();
+  int32_t off = 0;
+#pragma unroll
+  for (int j = 0; j < kSortWaves; ++j) off += j < w ? wave_tot[j] : 0;
+  __syncthreads();
+  return off + x - v;
+}
+
+template <int IPT, bool FIRST, bool LAST>
+__global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a) {
+  __shared__ int32_t s_base[kRadix];               // global base of each digit for this tile
+  __shared__ int32_t s_run[kRadix];                // digits ranked so far in this tile
+  __shared__ int32_t s_wcnt[kSortWaves][kRadix];   // per-wave digit counts of one item row
+  __shared__ int32_t s_wtot[kSortWaves];
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1), w = t / kWave;
+  const int tile = blockIdx.x;
+
+  // keys of this tile, striped (loads first: they overlap the histogram scan below)
+  const int64_t base = (int64_t)tile * (kSortThreads * IPT);
+  uint32_t key[IPT];
+  int32_t val[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t e = base + i * kSortThreads + t;
+    key[i] = 0;
+    val[i] = 0;
+    if (e < a.S) {
+      key[i] = radix_key<FIRST>(a, e, nullptr);
+      val[i] = FIRST ? (int32_t)e : a.vals_in[e];
+    }
+  }
+
+  // thread t owns digit t: total over all tiles and the part of the tiles before this one
+  int32_t tot = 0, before = 0;
+  {
+    const int32_t* hcol = a.hist + t;
+    int j = 0;
+    for (; j + 4 <= a.n_tiles; j += 4) {
+      const int32_t h0 = hcol[(int64_t)(j + 0) * kRadix], h1 = hcol[(int64_t)(j + 1) * kRadix];
+      const int32_t h2 = hcol[(int64_t)(j + 2) * kRadix], h3 = hcol[(int64_t)(j + 3) * kRadix];
+      tot += (h0 + h1) + (h2 + h3);
+      before += (j + 0 < tile ? h0 : 0) + (j + 1 < tile ? h1 : 0) + (j + 2 < tile ? h2 : 0) +
+                (j + 3 < tile ? h3 : 0);
+    }
+    for (; j < a.n_tiles; ++j) {
+      const int32_t h0 = hcol[(int64_t)j * kRadix];
+      tot += h0;
+      before += j < tile ? h0 : 0;
+    }
+  }
+  const int32_t digit_start = block_exclusive_scan(tot, s_wtot);
+  s_base[t] = digit_start + before;
+  s_run[t] = 0;
+#pragma unroll
+  for (int j = 0; j < kSortWaves; ++j) s_wcnt[j][t] = 0;
+  __syncthreads();
+
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
+  int32_t pos[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t e = base + i * kSortThreads + t;
+    const bool ok = e < a.S;
+    const uint32_t d = (key[i] >> a.shift) & (kRadix - 1);
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < kRadixBits; ++b) {
+      const uint64_t m = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    const int rank = __popcll(peers & lt);
+    if (ok && rank == 0) s_wcnt[w][d] = __popcll(peers);
+    __syncthreads();
+    int32_t off = s_run[d] + rank;
+#pragma unroll
+    for (int j = 0; j < kSortWaves; ++j) off += j < w ? s_wcnt[j][d] : 0;
+    pos[i] = ok ? s_base[d] + off : -1;
+    __syncthreads();
+    int32_t add = 0;
+#pragma unroll
+    for (int j = 0; j < kSortWaves; ++j) {
+      add += s_wcnt[j][t];
+      s_wcnt[j][t] = 0;
+    }
+    s_run[t] += add;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    if (pos[i] >= 0) {
+      a.keys_out[pos[i]] = key[i];
+      a.vals_out[pos[i]] = val[i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------- segments --------
+constexpr int kSegIPT = 8;
+constexpr int kSegTile = kSortThreads * kSegIPT;
+
+__global__ __launch_bounds__(kSortThreads) void seg_count_kernel(const int32_t* __restrict__ rows,
+                                                                 int64_t S,
+                                                                 int32_t* __restrict__ tile_heads) {
+  __shared__ int32_t s_w[kSortWaves];
+  const int64_t base = (int64_t)blockIdx.x * kSegTile;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < kSegIPT; ++i) {
+    const int64_t s = base + i * kSortThreads + threadIdx.x;
+    if (s < S) c += (s == 0 || rows[s] != rows[s - 1]) ? 1 : 0;
+  }
+  c = wave_sum_i32(c);
+  if ((threadIdx.x & (kWave - 1)) == 0) s_w[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t tot = 0;
+    for (int j = 0; j < kSortWaves; ++j) tot += s_w[j];
+    tile_heads[blockIdx.x] = tot;
+  }
+}
+
+__global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
+    const int32_t* __restrict__ rows, int64_t S, const int32_t* __restrict__ tile_heads,
+    int n_tiles, int32_t* __restrict__ pos_seg, int32_t* __restrict__ unique_rows,
+    int32_t* __restrict__ seg_offsets, int32_t* __restrict__ num_unique) {
+  __shared__ int32_t s_w[kSortWaves];
+  const int t = threadIdx.x;
+  // heads in the tiles before this one
+  int32_t before = 0;
+  for (int j = t; j < (int)blockIdx.x; j += kSortThreads) before += tile_heads[j];
+  before = wave_sum_i32(before);
+  if ((t & (kWave - 1)) == 0) s_w[t / kWave] = before;
+  __syncthreads();
+  int32_t tile_base = 0;
+  for (int j = 0; j < kSortWaves; ++j) tile_base += s_w[j];
+  __syncthreads();
+  // blocked: thread t owns kSegIPT consecutive positions
+  const int64_t s0 = (int64_t)blockIdx.x * kSegTile + (int64_t)t * kSegIPT;
+  int32_t r[kSegIPT];
+  bool head[kSegIPT];
+  int32_t cnt = 0;
+  int32_t prev = (s0 > 0 && s0 - 1 < S) ? rows[s0 - 1] : -1;
+#pragma unroll
+  for (int i = 0; i < kSegIPT; ++i) {
+    const int64_t s = s0 + i;
+    r[i] = s < S ? rows[s] : -1;
+    head[i] = s < S && (s == 0 || r[i] != prev);
+    prev = r[i];
+    cnt += head[i] ? 1 : 0;
+  }
+  int32_t u = tile_base + block_exclusive_scan(cnt, s_w) - 1;
+#pragma unroll
+  for (int i = 0; i < kSegIPT; ++i) {
+    const int64_t s = s0 + i;
+    if (s < S) {
+      if (head[i]) {
+        ++u;
+        unique_rows[u] = r[i];
+        seg_offsets[u] = (int32_t)s;
+      }
+      pos_seg[s] = u;
+      if (s == S - 1) {
+        *num_unique = u + 1;
+        seg_offsets[u + 1] = (int32_t)S;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side --------
+static int key_bits(int64_t V) {
+  int bits = 1;
+  while (bits < 32 && (int64_t(1) << bits) < V) ++bits;
+  return bits;
+}
+
+// Items per thread: 8 (2048-key tiles) while that keeps the per-block histogram scan short
+// (<= 256 tiles); larger batches (data-parallel gathered plans) use 32 (8192-key tiles).
+static int plan_ipt(int64_t S) { return S <= 256 * 2048 ? 8 : 32; }
+
+struct PlanLayout {
+  uint32_t* keys[2];
+  int32_t* vals[2];
+  int32_t* hist;
+  int32_t* tile_heads;
+  size_t total;
+};
+
+static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
+  const int ipt = plan_ipt(S);
+  const int64_t n_tiles = ceil_div(std::max<int64_t>(S, 1), kSortThreads * ipt);
+  const int64_t n_seg = ceil_div(std::max<int64_t>(S, 1), kSegTile);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (size_t)align_up((int64_t)bytes, 256);
+    return base ? base + o : nullptr;
+  };
+  for (int j = 0; j < 2; ++j) {
+    L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
+    L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
+  }
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * kRadix * n_tiles));
+  L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
+  L->total = off;
+  return off;
+}
+
+template <int IPT>
+static int run_passes(RadixPass a, int passes, const ctr_sparse_plan* plan, PlanLayout& L,
+                      hipStream_t st) {
+  const unsigned grid = (unsigned)a.n_tiles;
+  for (int p = 0; p < passes; ++p) {
+    const bool first = p == 0, last = p == passes - 1;
+    a.shift = p * kRadixBits;
+    a.keys_in = first ? nullptr : L.keys[(p - 1) & 1];
+    a.vals_in = first ? nullptr : L.vals[(p - 1) & 1];
+    a.keys_out = last ? reinterpret_cast<uint32_t*>(plan->sorted_rows) : L.keys[p & 1];
+    a.vals_out = last ? plan->sorted_slots : L.vals[p & 1];
+    if (first)
+      hipLaunchKernelGGL((radix_hist_kernel<IPT, true>), grid, kSortThreads, 0, st, a);
+    else
+      hipLaunchKernelGGL((radix_hist_kernel<IPT, false>), grid, kSortThreads, 0, st, a);
+    CTR_LAUNCH_CHECK("radix_hist_kernel");
+    if (first && last)
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, true>), grid, kSortThreads, 0, st, a);
+    else if (first)
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, false>), grid, kSortThreads, 0, st, a);
+    else if (last)
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, true>), grid, kSortThreads, 0, st, a);
+    else
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, false>), grid, kSortThreads, 0, st, a);
+    CTR_LAUNCH_CHECK("radix_scatter_kernel");
+  }
+  return CTR_OK;
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+static bool plan_ok(const ctr_sparse_plan* p) {
+  return p && p->S >= 0 && p->sorted_slots && p->sorted_rows && p->pos_seg && p->unique_rows &&
+         p->seg_offsets && p->num_unique;
+}
+
+extern "C" int64_t ctr_sparse_plan_workspace_bytes(int64_t S, int64_t V) {
+  if (S < 0 || V <= 0 || S >= (int64_t(1) << 24)) {
+    set_error("ctr_sparse_plan_workspace_bytes: bad sizes (need 0 <= S < 2^24, V > 0)");
+    return -1;
+  }
+  PlanLayout L;
+  return (int64_t)plan_layout(S, nullptr, &L);
+}
+
+extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
+                                     const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,
+                                     int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_sparse_plan_build: incomplete plan");
+  CTR_REQUIRE(idx || plan->S == 0, "ctr_sparse_plan_build: null idx");
+  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && plan->S < (int64_t(1) << 24),
+              "ctr_sparse_plan_build: bad sizes (need V < 2^31, S < 2^24)");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  hipStream_t st = as_stream(stream);
+  const int64_t S = plan->S;
+  if (S == 0) {
+    CTR_HIP_CHECK(hipMemsetAsync(plan->num_unique, 0, sizeof(int32_t), st));
+    CTR_HIP_CHECK(hipMemsetAsync(plan->seg_offsets, 0, sizeof(int32_t), st));
+    return CTR_OK;
+  }
+  PlanLayout L;
+  const size_t need = plan_layout(S, static_cast<char*>(ws), &L);
+  if (!ws || ws_bytes < (int64_t)need) {
+    set_error("ctr_sparse_plan_build: workspace %lld < %lld bytes", (long long)ws_bytes,
+              (long long)need);
+    return CTR_ERR_WORKSPACE;
+  }
+  const int ipt = plan_ipt(S);
+  RadixPass a;
+  memset(&a, 0, sizeof(a));
+  a.idx = idx;
+  a.idx_type = idx_type;
+  a.V = V;
+  a.hist = L.hist;
+  a.S = S;
+  a.n_tiles = (int)ceil_div(S, kSortThreads * ipt);
+  a.err = err_flag;
+  const int passes = (int)ceil_div(key_bits(V), kRadixBits);
+  const int rc = ipt == 8 ? run_passes<8>(a, passes, plan, L, st)
+                          : run_passes<32>(a, passes, plan, L, st);
+  if (rc != CTR_OK) return rc;
+  const unsigned gs = (unsigned)ceil_div(S, kSegTile);
+  hipLaunchKernelGGL(seg_count_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,
+                     L.tile_heads);
+  CTR_LAUNCH_CHECK("seg_count_kernel");
+  hipLaunchKernelGGL(seg_write_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,
+                     L.tile_heads, (int)gs, plan->pos_seg, plan->unique_rows, plan->seg_offsets,
+                     plan->num_unique);
+  CTR_LAUNCH_CHECK("seg_write_kernel");
+  return CTR_OK;
+}

@@ -30,7 +30,9 @@ def _ids(rng, B, F, V, hot=True):
 
 # ----------------------------------------------------------------- sparse plan ------
 @pytest.mark.parametrize("B,F,V", [(1, 1, 1), (3, 5, 2), (64, 26, 1000), (257, 13, 50),
-                                   (4096, 26, 1_000_000), (1000, 39, 1508), (33, 16, 7)])
+                                   (4096, 26, 1_000_000), (1000, 39, 1508), (33, 16, 7),
+                                   (8192, 26, 10_000_000), (20165, 26, 2),
+                                   (65536, 26, 40_000_000), (777, 22, 2**31 - 1)])
 @pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
 def test_sparse_plan_bit_exact(cuda, B, F, V, dtype):
     H = _hip()

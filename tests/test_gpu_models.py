@@ -348,10 +348,12 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     assert loss == pytest.approx(lref, rel=1e-5)
     gE, gw, dense = _fused_grads(tr)
     tr.flush()
+    n_terms = np.bincount(np.asarray(x).reshape(-1), minlength=V)
     assert_grad_close(gE, params_cpu["feature_embedding.weight"].grad.numpy(),
-                      cond=cond["feature_embedding.weight"].numpy(), err_msg="grad E")
+                      cond=cond["feature_embedding.weight"].numpy(), n_terms=n_terms,
+                      err_msg="grad E")
     assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(),
-                      cond=cond["linear.weight"].numpy(), err_msg="grad w")
+                      cond=cond["linear.weight"].numpy(), n_terms=n_terms, err_msg="grad w")
     for k, v in dense.items():
         assert_grad_close(v, params_cpu[k].grad.numpy(), err_msg=f"grad {k}")
     E = m.feature_embedding.weight.detach()

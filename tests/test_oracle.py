@@ -145,8 +145,8 @@ def _toy(name):
 
 
 def test_grad_condition_bounds_the_gradient(golden):
-    """A = sum of |g*s| + |g*e| over a row's slots bounds |grad| elementwise, and for a
-    single-slot row equals |g|*(|s|+|e|) of that slot."""
+    """A = sum of |g|*sum_f|e_f| + |g*e| over a row's slots bounds |grad| elementwise, and
+    for a single-slot row equals |g|*(sum_f|e_f| + |e|) of that slot."""
     g = golden("g_fm.npz")
     params = {"bias": torch.tensor(g["small_b0"]), "linear.weight": torch.tensor(g["small_w0"]),
               "feature_embedding.weight": torch.tensor(g["small_E0"])}
@@ -163,7 +163,7 @@ def test_grad_condition_bounds_the_gradient(golden):
           + 0.5 * ((s.squeeze(1) ** 2) - (e ** 2).sum(1)).sum(1))
     p = torch.sigmoid(zp)
     gz = (p - y.double().reshape(-1)) / x.shape[0]
-    expect = gz.abs().view(-1, 1, 1) * (s.abs() + e.abs())
+    expect = gz.abs().view(-1, 1, 1) * (e.abs().sum(1, keepdim=True) + e.abs())
     flat = x.reshape(-1).numpy()
     single = np.bincount(flat, minlength=gE.shape[0]) == 1
     want = torch.zeros_like(AE).index_add_(0, x.reshape(-1), expect.reshape(-1, E.shape[1]))
