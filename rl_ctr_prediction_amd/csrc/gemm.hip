@@ -66,131 +66,153 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc
   }
 }
 
-// Global->register staging, built so the loads of k-tile t+1 really overlap the MFMAs of
-// k-tile t: no select or branch touches a loaded value until the LDS store that follows
-// the MFMA loop (a select right after a load makes hipcc wait vmcnt there). Addresses are
-// clamped instead: a row beyond M (or a column beyond N) is read from row 0 — it only
-// feeds C entries that are never stored — and the K tail, which feeds every output, is
-// zeroed at LDS-store time. Per-thread row pointers are computed once; a k-tile step is
-// one pointer increment. VEC: 16-B aligned rows, contiguous extents multiple of 4.
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(GemmArgs a) {
+// ------------------------------------------------------------------- the kernel ------
+// Block = WAVES_M x WAVES_N x KSPLIT waves (4: one per SIMD), tile BM x BN x BK=32; a wave
+// owns a WM x WN = (BM/WAVES_M) x (BN/WAVES_N) sub-tile of TM x TN 32x32 accumulators over
+// 1/KSPLIT of every k-tile (the KSPLIT partial tiles are added in wave order through LDS
+// at the end: deterministic). Tiles are sized per GEMM shape so that the grid is about one
+// round of the 256 CUs (choose_tiles): e.g. 64x160 (k-split 2) for the 8192x300 forward,
+// 128x416 for the 8192x1664 input gradient, 160x128 (split-K 9) for the 300x1664 weight
+// gradient — tile quantisation, not the MFMA loop, was what the previous 64/128-only
+// tilings lost.
+//
+// LDS images, per operand:
+//  - k-contiguous in memory (A [M][K], nn.Linear weights [N][K]): row-major [rows][36]; a
+//    lane reads its row's 4 consecutive k with one ds_read_b128 (conflict-free at stride
+//    36) and feeds 4 MFMA k-steps. The MFMA's k order inside each 8-wide group is permuted
+//    (step j, lane half h -> k = 8g + 4h + j) identically for A and B, so every product
+//    A[m,k]B[k,n] is formed once; only the accumulation order differs from plain k order.
+//  - rows-contiguous (A^T, B [K][N]): k-major [32][rows+4]; ds_read_b32 per k-step at the
+//    permuted k (32 consecutive rows per half-wave: conflict-free).
+// Global loads of k-tile t+1 are in flight (registers) while the MFMAs of k-tile t run;
+// rows beyond M/N are clamped to row 0 (never stored), the K tail is zeroed at LDS store.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int KSPLIT, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel(GemmArgs a) {
   constexpr int BK = 32;
-  constexpr int PADA = TA ? 4 : 1;  // k-major images; odd stride for transposed writes
-  constexpr int PADB = TB ? 1 : 4;
-  constexpr int SA = BM + PADA, SB = BN + PADB;
-  constexpr int WAVES_N = BN / WN;
-  constexpr int NT = (BM / WM) * (BN / WN) * 64;  // 4 waves (1/SIMD) or 8 (2/SIMD)
+  constexpr int NT = WAVES_M * WAVES_N * KSPLIT * 64;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int NA = BM * BK / 4 / NT;  // float4 loads per thread per k-tile
-  constexpr int NB = BN * BK / 4 / NT;
-  static_assert(NT == 256 || NT == 512, "4 or 8 waves per block");
-  static_assert(NA >= 1 && NB >= 1, "tile too small for the block");
-
-  // two LDS stages: the next k-tile is written while the current one feeds the MFMAs,
-  // one barrier per k-tile
-  __shared__ __attribute__((aligned(16))) float As[2][BK * SA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * SB];
+  constexpr bool A_KC = !TA, B_KC = TB;
+  constexpr int SKC = BK + 4;
+  constexpr int SA = A_KC ? SKC : BM + 4;
+  constexpr int SB = B_KC ? SKC : BN + 4;
+  constexpr int A_IMG = A_KC ? BM * SKC : BK * (BM + 4);
+  constexpr int B_IMG = B_KC ? BN * SKC : BK * (BN + 4);
+  constexpr int NA = BM * BK / 4 / NT, NB = BN * BK / 4 / NT;
+  constexpr int GPW = (BK / 8) / KSPLIT;  // 8-k groups per wave per k-tile
+  static_assert(WM % 32 == 0 && WN % 32 == 0, "wave tile in 32x32 MFMA blocks");
+  static_assert(NA * NT * 4 == BM * BK && NB * NT * 4 == BN * BK, "loads split evenly");
+  static_assert(GPW * KSPLIT == BK / 8, "k-split divides the 4 groups of a k-tile");
+  static_assert((KSPLIT - 1) * WAVES_M * WAVES_N * WM * WN <= 2 * (A_IMG + B_IMG),
+                "k-split partials fit the tile buffers");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_IMG + B_IMG)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm0 = (wave / WAVES_N) * WM;
-  const int wn0 = (wave % WAVES_N) * WN;
-  const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  const int kw = wave / (WAVES_M * WAVES_N);
+  const int wmn = wave % (WAVES_M * WAVES_N);
+  const int wm0 = (wmn / WAVES_N) * WM;
+  const int wn0 = (wmn % WAVES_N) * WN;
+  const int h = lane >> 5, il = lane & 31;
+
+  // tile of this block: tiles sharing A rows are consecutive, and consecutive tiles are
+  // kept on one XCD (blocks b, b+8, b+16... share an XCD under round-robin dispatch)
+  const int64_t gn = (a.N + BN - 1) / BN;
+  const int64_t T = gridDim.x;
+  int64_t tix = blockIdx.x;
+  if (T % 8 == 0) tix = (tix % 8) * (T / 8) + tix / 8;
+  const int64_t m0 = (tix / gn) * BM;
+  const int64_t n0 = (tix % gn) * BN;
   const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
   const int64_t ke = min(a.K, kb + a.k_per_split);
 
-  // per-thread fixed tile coordinates and row pointers (at k = kb)
+  // per-thread load coordinates: (row, k-offset) of each float4 it stages
   const float* pa[NA];
   const float* pb[NB];
-  int ka[NA], kbv[NB];  // k offset inside the tile this thread's float4 starts at
+  int ka[NA], kbv[NB], la[NA], lb[NB];  // k offset in the tile; LDS float offset
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int q = tid + NT * i;
-    if (!TA) {  // A[m][k], k contiguous
-      const int m = q / (BK / 4), k4 = q % (BK / 4);
-      const int64_t gm = m0 + m;
+    if (A_KC) {
+      const int r = q / (BK / 4), k4 = q % (BK / 4);
+      const int64_t gm = m0 + r;
       ka[i] = k4 * 4;
+      la[i] = r * SKC + k4 * 4;
       pa[i] = a.A + (gm < a.M ? gm : 0) * a.lda + kb + ka[i];
-    } else {  // A stored [k][m], m contiguous
-      const int k = q / (BM / 4), m4 = q % (BM / 4);
-      const int64_t gm = m0 + m4 * 4;
+    } else {
+      const int k = q / (BM / 4), r4 = q % (BM / 4);
+      const int64_t gm = m0 + r4 * 4;
       ka[i] = k;
+      la[i] = k * SA + r4 * 4;
       pa[i] = a.A + (kb + k) * a.lda + (gm < a.M ? gm : 0);
     }
   }
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int q = tid + NT * i;
-    if (!TB) {  // B[k][n], n contiguous
-      const int k = q / (BN / 4), n4 = q % (BN / 4);
-      const int64_t gn = n0 + n4 * 4;
-      kbv[i] = k;
-      pb[i] = a.B + (kb + k) * a.ldb + (gn < a.N ? gn : 0);
-    } else {  // B stored [n][k] (nn.Linear weight), k contiguous
-      const int n = q / (BK / 4), k4 = q % (BK / 4);
-      const int64_t gn = n0 + n;
+    if (B_KC) {
+      const int r = q / (BK / 4), k4 = q % (BK / 4);
+      const int64_t gnn = n0 + r;
       kbv[i] = k4 * 4;
-      pb[i] = a.B + (gn < a.N ? gn : 0) * a.ldb + kb + kbv[i];
+      lb[i] = r * SKC + k4 * 4;
+      pb[i] = a.B + (gnn < a.N ? gnn : 0) * a.ldb + kb + kbv[i];
+    } else {
+      const int k = q / (BN / 4), r4 = q % (BN / 4);
+      const int64_t gnn = n0 + r4 * 4;
+      kbv[i] = k;
+      lb[i] = k * SB + r4 * 4;
+      pb[i] = a.B + (kb + k) * a.ldb + (gnn < a.N ? gnn : 0);
     }
   }
-  const int64_t stepA = TA ? BK * a.lda : BK;  // pointer advance per k-tile
-  const int64_t stepB = TB ? BK : BK * a.ldb;
+  const int64_t stepA = A_KC ? BK : BK * a.lda;
+  const int64_t stepB = B_KC ? BK : BK * a.ldb;
 
   float4 ra[NA], rb[NB];
-  auto load_tile = [&](int t) {  // k-tile t of this split, rows clamped, K tail not masked
+  auto load_tile = [&](int t) {
     const int64_t k0 = kb + (int64_t)t * BK;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const float* p = pa[i] + t * stepA;
+      const bool okk = k0 + ka[i] < ke;
       if (VEC) {
-        // a float4 wholly past the K end reads the split's first tile instead (masked later)
-        const bool okk = k0 + ka[i] < ke;
         ra[i] = *reinterpret_cast<const float4*>(okk ? p : pa[i]);
       } else {
-        const int kl0 = (int)(k0 + ka[i] - kb);
         float4 v;
-        if (!TA) {
+        if (A_KC) {
           v.x = (k0 + ka[i] + 0 < ke) ? p[0] : 0.f;
           v.y = (k0 + ka[i] + 1 < ke) ? p[1] : 0.f;
           v.z = (k0 + ka[i] + 2 < ke) ? p[2] : 0.f;
           v.w = (k0 + ka[i] + 3 < ke) ? p[3] : 0.f;
         } else {
-          const int q = tid + NT * i;
-          const int64_t gm = m0 + (q % (BM / 4)) * 4;
-          const bool okk = k0 + ka[i] < ke;
+          const int64_t gm = m0 + (((tid + NT * i) % (BM / 4)) * 4);
           v.x = (okk && gm + 0 < a.M) ? p[0] : 0.f;
           v.y = (okk && gm + 1 < a.M) ? p[1] : 0.f;
           v.z = (okk && gm + 2 < a.M) ? p[2] : 0.f;
           v.w = (okk && gm + 3 < a.M) ? p[3] : 0.f;
         }
-        (void)kl0;
         ra[i] = v;
       }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const float* p = pb[i] + t * stepB;
+      const bool okk = k0 + kbv[i] < ke;
       if (VEC) {
-        const bool okk = k0 + kbv[i] < ke;
         rb[i] = *reinterpret_cast<const float4*>(okk ? p : pb[i]);
       } else {
         float4 v;
-        if (TB) {
+        if (B_KC) {
           v.x = (k0 + kbv[i] + 0 < ke) ? p[0] : 0.f;
           v.y = (k0 + kbv[i] + 1 < ke) ? p[1] : 0.f;
           v.z = (k0 + kbv[i] + 2 < ke) ? p[2] : 0.f;
           v.w = (k0 + kbv[i] + 3 < ke) ? p[3] : 0.f;
         } else {
-          const int q = tid + NT * i;
-          const int64_t gn = n0 + (q % (BN / 4)) * 4;
-          const bool okk = k0 + kbv[i] < ke;
-          v.x = (okk && gn + 0 < a.N) ? p[0] : 0.f;
-          v.y = (okk && gn + 1 < a.N) ? p[1] : 0.f;
-          v.z = (okk && gn + 2 < a.N) ? p[2] : 0.f;
-          v.w = (okk && gn + 3 < a.N) ? p[3] : 0.f;
+          const int64_t gnn = n0 + (((tid + NT * i) % (BN / 4)) * 4);
+          v.x = (okk && gnn + 0 < a.N) ? p[0] : 0.f;
+          v.y = (okk && gnn + 1 < a.N) ? p[1] : 0.f;
+          v.z = (okk && gnn + 2 < a.N) ? p[2] : 0.f;
+          v.w = (okk && gnn + 3 < a.N) ? p[3] : 0.f;
         }
         rb[i] = v;
       }
@@ -199,39 +221,19 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(Ge
 
   auto store_tile = [&](int buf, int t) {
     const int64_t k0 = kb + (int64_t)t * BK;
-    float* as = As[buf];
-    float* bs = Bs[buf];
+    float* as = smem + buf * (A_IMG + B_IMG);
+    float* bs = as + A_IMG;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int q = tid + NT * i;
       float4 v = ra[i];
       if (VEC && !(k0 + ka[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // K tail
-      if (!TA) {
-        const int m = q / (BK / 4), k4 = q % (BK / 4);
-        as[(k4 * 4 + 0) * SA + m] = v.x;
-        as[(k4 * 4 + 1) * SA + m] = v.y;
-        as[(k4 * 4 + 2) * SA + m] = v.z;
-        as[(k4 * 4 + 3) * SA + m] = v.w;
-      } else {
-        const int k = q / (BM / 4), m4 = q % (BM / 4);
-        *reinterpret_cast<float4*>(&as[k * SA + m4 * 4]) = v;
-      }
+      *reinterpret_cast<float4*>(as + la[i]) = v;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int q = tid + NT * i;
       float4 v = rb[i];
       if (VEC && !(k0 + kbv[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!TB) {
-        const int k = q / (BN / 4), n4 = q % (BN / 4);
-        *reinterpret_cast<float4*>(&bs[k * SB + n4 * 4]) = v;
-      } else {
-        const int n = q / (BK / 4), k4 = q % (BK / 4);
-        bs[(k4 * 4 + 0) * SB + n] = v.x;
-        bs[(k4 * 4 + 1) * SB + n] = v.y;
-        bs[(k4 * 4 + 2) * SB + n] = v.z;
-        bs[(k4 * 4 + 3) * SB + n] = v.w;
-      }
+      *reinterpret_cast<float4*>(bs + lb[i]) = v;
     }
   };
 
@@ -243,8 +245,34 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(Ge
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int kl = lane >> 5;  // k within the MFMA's K=2
-  const int il = lane & 31;
+  // fragments of one 8-k group: [operand tile][k-step]
+  auto read_frags = [&](float (&af)[TM][4], float (&bf)[TN][4], const float* as, const float* bs,
+                        int g) {
+    const int k0 = g * 8;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (A_KC) {
+        const float4 v =
+            *reinterpret_cast<const float4*>(as + (wm0 + i * 32 + il) * SKC + k0 + 4 * h);
+        af[i][0] = v.x; af[i][1] = v.y; af[i][2] = v.z; af[i][3] = v.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) af[i][j] = as[(k0 + 4 * h + j) * SA + wm0 + i * 32 + il];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      if (B_KC) {
+        const float4 v =
+            *reinterpret_cast<const float4*>(bs + (wn0 + t * 32 + il) * SKC + k0 + 4 * h);
+        bf[t][0] = v.x; bf[t][1] = v.y; bf[t][2] = v.z; bf[t][3] = v.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[t][j] = bs[(k0 + 4 * h + j) * SB + wn0 + t * 32 + il];
+      }
+    }
+  };
+
   if (kb < ke) {
     const int nt = (int)((ke - kb + BK - 1) / BK);
     load_tile(0);
@@ -254,31 +282,61 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(Ge
       const int buf = t & 1;
       const bool more = t + 1 < nt;
       if (more) load_tile(t + 1);  // in flight under the MFMAs below
-      const float* as = As[buf] + kl * SA + wm0 + il;
-      const float* bs = Bs[buf] + kl * SB + wn0 + il;
-      // every fragment of the k-tile is read first; the MFMA chain then only waits for
-      // the reads it consumes (progressive lgkmcnt), not a full LDS round trip per step
-      float af[BK / 2][TM], bf[BK / 2][TN];
+      const float* as = smem + buf * (A_IMG + B_IMG);
+      const float* bs = as + A_IMG;
+      float afc[TM][4], bfc[TN][4];
+      read_frags(afc, bfc, as, bs, kw * GPW);
 #pragma unroll
-      for (int kk = 0; kk < BK / 2; ++kk) {
+      for (int gg = 0; gg < GPW; ++gg) {
+        float afn[TM][4], bfn[TN][4];  // next group's fragments, read under these MFMAs
+        if (gg + 1 < GPW) read_frags(afn, bfn, as, bs, kw * GPW + gg + 1);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[kk][i] = as[kk * 2 * SA + i * 32];
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf[kk][j] = bs[kk * 2 * SB + j * 32];
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+              acc[i][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(afc[i][j], bfc[tn][j],
+                                                                acc[i][tn], 0, 0, 0);
+        if (gg + 1 < GPW) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) afc[i][j] = afn[i][j];
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfc[tn][j] = bfn[tn][j];
+        }
       }
-      // keep the reads ahead of the chain: hipcc's scheduler otherwise re-interleaves them
-      // with an lgkmcnt(0) before every MFMA group
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < BK / 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk][i], bf[kk][j], acc[i][j],
-                                                             0, 0, 0);
       if (more) store_tile(buf ^ 1, t + 1);  // the other stage: last read one barrier ago
       __syncthreads();
+    }
+  }
+
+  // in-block k-split: waves kw > 0 hand their partial tiles to wave kw = 0 through LDS
+  if (KSPLIT > 1) {
+    constexpr int PW = WM * WN;  // floats per wave partial, stored [i][t][r][lane]
+    if (kw > 0) {
+      float* dst = smem + ((kw - 1) * WAVES_M * WAVES_N + wmn) * PW;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * TN + tn) * 16 + r) * 64 + lane] = acc[i][tn][r];
+    }
+    __syncthreads();
+    if (kw > 0) return;
+#pragma unroll
+    for (int s = 1; s < KSPLIT; ++s) {
+      const float* src = smem + ((s - 1) * WAVES_M * WAVES_N + wmn) * PW;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][tn][r] += src[((i * TN + tn) * 16 + r) * 64 + lane];
     }
   }
 
@@ -288,12 +346,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_f32_kernel(Ge
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        const int64_t n = n0 + wn0 + j * 32 + il;
-        if (m < a.M && n < a.N) C[m * a.ldc + n] = apply_epi(a, epi, acc[i][j][r], m, n);
+        const int64_t m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = n0 + wn0 + tn * 32 + il;
+        if (m < a.M && n < a.N) C[m * a.ldc + n] = apply_epi(a, epi, acc[i][tn][r], m, n);
       }
 }
 
@@ -310,31 +368,34 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
   }
 }
 
+// Compiled tilings: (BM, BN, WAVES_M, WAVES_N, KSPLIT), 4 waves each.
+struct TileDef {
+  int bm, bn, wm, wn, ks;
+  double eff;  // sustained fraction of the 0.614 TFLOP/s per-CU fp32 MFMA peak (MI355X)
+};
+static const TileDef kTiles[] = {
+    {64, 64, 2, 2, 1, 0.40},   {64, 128, 2, 2, 1, 0.50},  {128, 64, 2, 2, 1, 0.50},
+    {128, 128, 2, 2, 1, 0.60}, {64, 160, 2, 1, 2, 0.62},  {128, 416, 4, 1, 1, 0.72},
+    {160, 128, 1, 4, 1, 0.62}, {64, 224, 2, 1, 2, 0.60},
+};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
 struct TileCfg {
-  int bm, bn;
+  int tile;  // index into kTiles
   int splits;
   int64_t kps;
-  int waves;  // 4 (one per SIMD) or 8 (two per SIMD)
 };
 
-// Pick (tile, split-K, waves) by a makespan model calibrated on MI355X (tools/gemm_bench.py,
-// profiles/r01_gemm_tuning.txt): every tiling sustains about the same per-CU rate
-// (~0.36 TFLOP/s), so the choice is about load balance — blocks are dealt to 256 CUs in
-// rounds, a round costs one block's flops at that rate plus ~1.5 us of prologue/epilogue,
-// and split-K adds its fp32 slab round trip (2 * splits * M * N * 4 B at ~5 TB/s) and a
-// reduce launch. CTR_GEMM_CFG="bm,bn,splits[,waves]" forces a choice (tuning only).
+// Pick (tiling, split-K) by a makespan model: blocks are dealt to the 256 CUs in rounds;
+// a round costs one block's padded flops at the tiling's sustained per-CU rate plus ~2 us
+// of prologue/epilogue; split-K adds its fp32 slab round trip (2 * splits * M * N * 4 B at
+// ~5 TB/s) and a reduce launch. CTR_GEMM_CFG="tile,splits" forces a choice (tuning only).
 static TileCfg choose_tiles(int64_t M, int64_t N, int64_t K) {
-  static const struct { int bm, bn, waves; } cands[] = {
-      {128, 128, 4}, {128, 64, 4}, {64, 128, 4}, {64, 64, 4}, {128, 64, 8}, {64, 128, 8}};
-  const double cu_tflops = 0.36;
-  TileCfg best{64, 64, 1, std::max<int64_t>(K, 1), 4};
-  double best_t = 1e30;
+  TileCfg best{0, 1, std::max<int64_t>(K, 1)};
   if (const char* env = getenv("CTR_GEMM_CFG")) {
-    int bm = 0, bn = 0, sp = 0, wv = 4;
-    const int nf = sscanf(env, "%d,%d,%d,%d", &bm, &bn, &sp, &wv);
-    if (nf >= 3 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128) && sp >= 1 &&
-        (wv == 4 || (wv == 8 && bm * bn >= 128 * 64))) {
-      TileCfg c{bm, bn, 1, std::max<int64_t>(K, 1), wv};
+    int ti = -1, sp = 1;
+    if (sscanf(env, "%d,%d", &ti, &sp) >= 1 && ti >= 0 && ti < kNumTiles && sp >= 1) {
+      TileCfg c{ti, 1, std::max<int64_t>(K, 1)};
       if (sp > 1 && K >= 64) {
         c.kps = align_up(ceil_div(K, sp), 32);
         c.splits = (int)ceil_div(K, c.kps);
@@ -342,8 +403,10 @@ static TileCfg choose_tiles(int64_t M, int64_t N, int64_t K) {
       return c;
     }
   }
-  for (const auto& cd : cands) {
-    const int64_t tiles = ceil_div(M, cd.bm) * ceil_div(N, cd.bn);
+  double best_t = 1e30;
+  for (int ti = 0; ti < kNumTiles; ++ti) {
+    const TileDef& d = kTiles[ti];
+    const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
     for (int s = 1; s <= 32; ++s) {
       if (s > 1 && K / s < 256) break;  // keep >= 8 k-tiles per split
       const int64_t kps = s == 1 ? K : align_up(ceil_div(K, s), 32);
@@ -351,37 +414,51 @@ static TileCfg choose_tiles(int64_t M, int64_t N, int64_t K) {
       if (splits != s) continue;
       const int64_t blocks = tiles * splits;
       const double rounds = (double)ceil_div(blocks, 256);
-      const double t_block = 2.0 * cd.bm * cd.bn * (double)kps / (cu_tflops * 1e6) + 1.5;
+      const double kpad = (double)align_up(std::max<int64_t>(kps, 1), 32);
+      const double t_block = 2.0 * d.bm * d.bn * kpad / (0.614 * d.eff * 1e6) + 2.0;
       double t = rounds * t_block;
       if (splits > 1) t += 2.0 * splits * (double)M * N * 4 / 5e6 + 3.0;  // us
       if (t < best_t * 0.98) {
         best_t = t;
-        best = TileCfg{cd.bm, cd.bn, splits, splits > 1 ? kps : std::max<int64_t>(K, 1), cd.waves};
+        best = TileCfg{ti, splits, splits > 1 ? kps : std::max<int64_t>(K, 1)};
       }
     }
   }
   return best;
 }
 
-template <int BM, int BN, int WM, int WN, bool VEC>
+template <int BM, int BN, int WMW, int WNW, int KS, bool VEC>
 static void launch_vec(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
-  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  constexpr int NT = WMW * WNW * KS * 64;
   if (!ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, VEC>), grid, NT, 0, st, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, false, false, VEC>), grid, NT, 0, st, a);
   else if (!ta && tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true, VEC>), grid, NT, 0, st, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, false, true, VEC>), grid, NT, 0, st, a);
   else if (ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false, VEC>), grid, NT, 0, st, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, true, false, VEC>), grid, NT, 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true, VEC>), grid, NT, 0, st, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, true, true, VEC>), grid, NT, 0, st, a);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WMW, int WNW, int KS>
 static void launch_cfg(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
   if (a.vec_a && a.vec_b)
-    launch_vec<BM, BN, WM, WN, true>(a, ta, tb, grid, st);
+    launch_vec<BM, BN, WMW, WNW, KS, true>(a, ta, tb, grid, st);
   else
-    launch_vec<BM, BN, WM, WN, false>(a, ta, tb, grid, st);
+    launch_vec<BM, BN, WMW, WNW, KS, false>(a, ta, tb, grid, st);
+}
+
+static void launch_tile(int ti, const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
+  switch (ti) {
+    case 0: launch_cfg<64, 64, 2, 2, 1>(a, ta, tb, grid, st); break;
+    case 1: launch_cfg<64, 128, 2, 2, 1>(a, ta, tb, grid, st); break;
+    case 2: launch_cfg<128, 64, 2, 2, 1>(a, ta, tb, grid, st); break;
+    case 3: launch_cfg<128, 128, 2, 2, 1>(a, ta, tb, grid, st); break;
+    case 4: launch_cfg<64, 160, 2, 1, 2>(a, ta, tb, grid, st); break;
+    case 5: launch_cfg<128, 416, 4, 1, 1>(a, ta, tb, grid, st); break;
+    case 6: launch_cfg<160, 128, 1, 4, 1>(a, ta, tb, grid, st); break;
+    case 7: launch_cfg<64, 224, 2, 1, 2>(a, ta, tb, grid, st); break;
+  }
 }
 
 }  // namespace ctr
@@ -448,17 +525,9 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
     a.ldc = N;
     a.slab_stride = M * N;
   }
-  const dim3 grid((unsigned)ceil_div(N, c.bn), (unsigned)ceil_div(M, c.bm), (unsigned)c.splits);
-  const bool ta = trans_a != 0, tb = trans_b != 0;
-  if (c.waves == 8) {  // two waves per SIMD: one's LDS-store/barrier phase hides under the
-                      // other's MFMA chain
-    if (c.bm == 128 && c.bn == 128) launch_cfg<128, 128, 64, 32>(a, ta, tb, grid, st);
-    else if (c.bm == 128) launch_cfg<128, 64, 32, 32>(a, ta, tb, grid, st);
-    else launch_cfg<64, 128, 32, 32>(a, ta, tb, grid, st);
-  } else if (c.bm == 128 && c.bn == 128) launch_cfg<128, 128, 64, 64>(a, ta, tb, grid, st);
-  else if (c.bm == 128) launch_cfg<128, 64, 64, 32>(a, ta, tb, grid, st);
-  else if (c.bn == 128) launch_cfg<64, 128, 32, 64>(a, ta, tb, grid, st);
-  else launch_cfg<64, 64, 32, 32>(a, ta, tb, grid, st);
+  const TileDef& d = kTiles[c.tile];
+  const dim3 grid((unsigned)(ceil_div(N, d.bn) * ceil_div(M, d.bm)), 1, (unsigned)c.splits);
+  launch_tile(c.tile, a, trans_a != 0, trans_b != 0, grid, st);
   CTR_LAUNCH_CHECK("gemm_f32_kernel");
   if (c.splits > 1) {
     GemmArgs r = a;

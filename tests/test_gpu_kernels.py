@@ -167,6 +167,34 @@ def test_gemm_vs_fp64(cuda, ta, tb, M, N, K):
     assert ((C - ref).abs() <= tol * bound + 1e-30).all()
 
 
+@pytest.mark.parametrize("tile", range(8))  # every compiled tiling of csrc/gemm.hip (kTiles)
+def test_gemm_every_tiling(cuda, tile, monkeypatch):
+    """Force each tiling (and split-K) on shapes with M/N edges and K tails, both the float4
+    path (extents % 4 == 0) and the scalar path, every transpose: fp32 parity vs fp64."""
+    H = _hip()
+    g = torch.Generator().manual_seed(tile)
+    for splits in (1, 3):
+        monkeypatch.setenv("CTR_GEMM_CFG", f"{tile},{splits}")
+        for (M, N, K) in ((333, 452, 1060), (97, 451, 259)):
+            A = torch.randn(M, K, generator=g)
+            Bm = torch.randn(K, N, generator=g)
+            ref = A.double() @ Bm.double()
+            bound = A.double().abs() @ Bm.double().abs()
+            for ta in (False, True):
+                for tb in (False, True):
+                    a = (A.t() if ta else A).contiguous().to(cuda)
+                    b = (Bm.t() if tb else Bm).contiguous().to(cuda)
+                    C = H.gemm(a, b, ta, tb).cpu().double()
+                    bad = (C - ref).abs() > 2e-6 * bound + 1e-30
+                    assert not bad.any(), (tile, splits, M, N, K, ta, tb, int(bad.sum()))
+        bias = torch.randn(452, generator=g)
+        A = torch.randn(333, 1060, generator=g)
+        W = torch.randn(452, 1060, generator=g)
+        y = H.linear(A.to(cuda), W.to(cuda), bias.to(cuda), relu=True).cpu().double()
+        r = (A.double() @ W.double().t() + bias.double()).clamp(min=0)
+        np.testing.assert_allclose(y.numpy(), r.numpy(), rtol=1e-5, atol=1e-4)
+
+
 def test_gemm_epilogues(cuda):
     H = _hip()
     g = torch.Generator().manual_seed(0)

@@ -2,7 +2,8 @@
 
     python tools/gemm_bench.py [--reps 20] [--configs auto,128x128x1,...]
 
-Uses CTR_GEMM_CFG to force a (BM, BN, splits) choice; 'auto' = the built-in chooser.
+Uses CTR_GEMM_CFG="tile,splits" to force a tiling of csrc/gemm.hip's kTiles and a split-K
+count; 'auto' = the built-in chooser.
 Prints one JSON line per (shape, config) with microseconds and TFLOP/s.
 """
 from __future__ import annotations
@@ -32,10 +33,8 @@ SHAPES = {  # name: (M, N, K, trans_a, trans_b)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--configs", default="auto,128x128x1,128x128x1x8,128x64x1x8,64x128x1x8,"
-                                         "64x64x1,128x128x4,128x128x4x8,64x64x4,128x64x2x8,"
-                                         "64x128x2x8,128x64x4x8,64x64x8,128x128x16x8,"
-                                         "128x64x8x8,64x128x8x8,64x64x16,128x64x16x8")
+    ap.add_argument("--configs", default="auto," + ",".join(
+        f"{t}x{s}" for t in range(8) for s in (1, 2, 4, 8, 9, 16)))
     ap.add_argument("--square", type=int, default=0,
                     help="time only an NxNxN NN product (kernel's intrinsic rate)")
     args = ap.parse_args()
@@ -57,12 +56,10 @@ def main():
             if cfg == "auto":
                 os.environ.pop("CTR_GEMM_CFG", None)
             else:
-                parts = cfg.split("x")
-                bm, bn, sp = parts[:3]
-                wv = parts[3] if len(parts) > 3 else "4"
+                tile, sp = cfg.split("x")
                 if int(sp) > 1 and K < 512:
                     continue
-                os.environ["CTR_GEMM_CFG"] = f"{bm},{bn},{sp},{wv}"
+                os.environ["CTR_GEMM_CFG"] = f"{tile},{sp}"
             for _ in range(3):
                 H.gemm(a, b, ta, tb, out=out)
             torch.cuda.synchronize()
