@@ -42,6 +42,7 @@ struct GemmArgs {
   int64_t k_per_split;
   int64_t slab_stride;  // elements between split-K slabs (0: no split)
   bool vec_a, vec_b;
+  bool vec_c;  // C rows 16-B aligned (float4 epilogue stores)
 };
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc, int64_t m,
@@ -72,40 +73,91 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc
 // 1/KSPLIT of every k-tile (the KSPLIT partial tiles are added in wave order through LDS
 // at the end: deterministic). Tiles are sized per GEMM shape so that the grid is about one
 // round of the 256 CUs (choose_tiles): e.g. 64x160 (k-split 2) for the 8192x300 forward,
-// 128x416 for the 8192x1664 input gradient, 160x128 (split-K 9) for the 300x1664 weight
-// gradient — tile quantisation, not the MFMA loop, was what the previous 64/128-only
-// tilings lost.
+// 128x416 for the 8192x1664 input gradient, 160x128 (split-K) for the 300x1664 weight
+// gradient — tile quantisation was what 64/128-only tilings lost on these shapes.
 //
-// LDS images, per operand:
-//  - k-contiguous in memory (A [M][K], nn.Linear weights [N][K]): row-major [rows][36]; a
-//    lane reads its row's 4 consecutive k with one ds_read_b128 (conflict-free at stride
-//    36) and feeds 4 MFMA k-steps. The MFMA's k order inside each 8-wide group is permuted
-//    (step j, lane half h -> k = 8g + 4h + j) identically for A and B, so every product
-//    A[m,k]B[k,n] is formed once; only the accumulation order differs from plain k order.
-//  - rows-contiguous (A^T, B [K][N]): k-major [32][rows+4]; ds_read_b32 per k-step at the
-//    permuted k (32 consecutive rows per half-wave: conflict-free).
-// Global loads of k-tile t+1 are in flight (registers) while the MFMAs of k-tile t run;
-// rows beyond M/N are clamped to row 0 (never stored), the K tail is zeroed at LDS store.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int KSPLIT, bool TA, bool TB, bool VEC>
+// LDS images (unpadded, so LDS-DMA can fill them lane-linearly), per operand:
+//  - k-contiguous in memory (A [M][K], nn.Linear weights [N][K]): [rows][32] with the 16-B
+//    chunk c of row r stored at chunk c ^ ((r >> 1) & 7); a lane reads its row's 4
+//    consecutive k with one conflict-free ds_read_b128 and feeds 4 MFMA k-steps. The MFMA's
+//    k order inside each 8-wide group is permuted (step j, lane half h -> k = 8g + 4h + j)
+//    identically for A and B, so every product A[m,k]B[k,n] is formed once; only the
+//    accumulation order differs from plain k order.
+//  - rows-contiguous (A^T, B [K][N]): [32][rows]; ds_read_b32 per k-step at the permuted k
+//    (32 consecutive rows per half-wave: conflict-free).
+// Staging (VEC = 16-B aligned operands whose contiguous extents are multiples of 4):
+// global_load_lds_dwordx4 into a STAGES-deep LDS ring (the swizzle is applied to the
+// per-lane SOURCE address), counted s_waitcnt vmcnt + raw s_barrier, so STAGES-1 k-tiles
+// are in flight while one is multiplied; otherwise a register-staged path with the same
+// images. Rows beyond M/N read row 0 (never stored); the K tail of the last k-tile is
+// zeroed in LDS before use.
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// global_load_lds_dwordx4 in inline asm: hipcc (ROCm 7.2) treats the builtin's LDS write
+// as aliasing every later ds_read and puts an s_waitcnt vmcnt(0) before the first fragment
+// read of each k-tile, draining the ring; hidden from its waitcnt model, the ring is
+// retired only by the counted waits below. `lds` is the wave-uniform LDS byte address.
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(lds_void_ptr)p;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16-B chunk swizzle of a k-contiguous image row (BK/4 chunks): conflict-free ds_read_b128
+// of one logical chunk by 32 consecutive rows (the 4x16-lane groups of gfx950's b128 read).
+template <int BK>
+__device__ __forceinline__ int kc_swz(int r) {
+  return BK == 32 ? ((r >> 1) & 7) : (r & 15);
+}
+
+template <int BM, int BN, int BK, int WAVES_M, int WAVES_N, int KSPLIT, int STAGES, bool TA,
+          bool TB, bool VEC>
 __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel(GemmArgs a) {
-  constexpr int BK = 32;
-  constexpr int NT = WAVES_M * WAVES_N * KSPLIT * 64;
+  static_assert(BK == 32 || BK == 64, "k-tile of 32 or 64");
+  constexpr int CPR = BK / 4;     // 16-B chunks per k-contiguous image row
+  constexpr int RPP = 256 / BK;   // image rows per 1-KB DMA piece
+  constexpr int NW = WAVES_M * WAVES_N * KSPLIT;
+  constexpr int NT = NW * 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr bool A_KC = !TA, B_KC = TB;
-  constexpr int SKC = BK + 4;
-  constexpr int SA = A_KC ? SKC : BM + 4;
-  constexpr int SB = B_KC ? SKC : BN + 4;
-  constexpr int A_IMG = A_KC ? BM * SKC : BK * (BM + 4);
-  constexpr int B_IMG = B_KC ? BN * SKC : BK * (BN + 4);
-  constexpr int NA = BM * BK / 4 / NT, NB = BN * BK / 4 / NT;
-  constexpr int GPW = (BK / 8) / KSPLIT;  // 8-k groups per wave per k-tile
+  constexpr int A_IMG = BM * BK, B_IMG = BN * BK;
+  constexpr int STAGE = A_IMG + B_IMG;
+  constexpr int NS = VEC ? STAGES : 2;  // LDS stages
+  constexpr int IA = A_IMG / 256 / NW, IB = B_IMG / 256 / NW;  // DMA instr per wave per tile
+  constexpr int G = IA + IB;
+  constexpr int NA = A_IMG / 4 / NT, NB = B_IMG / 4 / NT;  // register path: float4 per thread
+  constexpr int GPW = (BK / 8) / KSPLIT;                   // 8-k groups per wave per k-tile
   static_assert(WM % 32 == 0 && WN % 32 == 0, "wave tile in 32x32 MFMA blocks");
-  static_assert(NA * NT * 4 == BM * BK && NB * NT * 4 == BN * BK, "loads split evenly");
-  static_assert(GPW * KSPLIT == BK / 8, "k-split divides the 4 groups of a k-tile");
-  static_assert((KSPLIT - 1) * WAVES_M * WAVES_N * WM * WN <= 2 * (A_IMG + B_IMG),
-                "k-split partials fit the tile buffers");
-  __shared__ __attribute__((aligned(16))) float smem[2 * (A_IMG + B_IMG)];
+  static_assert(IA * NW * 256 == A_IMG && IB * NW * 256 == B_IMG, "DMA pieces split evenly");
+  static_assert(NA * NT * 4 == A_IMG && NB * NT * 4 == B_IMG, "loads split evenly");
+  static_assert(GPW * KSPLIT == BK / 8, "k-split divides the 8-k groups of a k-tile");
+  static_assert(G <= 63, "vmcnt range");
+  static_assert((KSPLIT - 1) * WAVES_M * WAVES_N * WM * WN <= NS * STAGE, "k-split partials fit");
+  static_assert(NW * 32 * 36 <= NS * STAGE, "epilogue tiles fit");
+  __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -126,114 +178,34 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
   const int64_t n0 = (tix % gn) * BN;
   const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
   const int64_t ke = min(a.K, kb + a.k_per_split);
+  const int nt = kb < ke ? (int)((ke - kb + BK - 1) / BK) : 0;
 
-  // per-thread load coordinates: (row, k-offset) of each float4 it stages
-  const float* pa[NA];
-  const float* pb[NB];
-  int ka[NA], kbv[NB], la[NA], lb[NB];  // k offset in the tile; LDS float offset
+  // ---- fragments of one 8-k group: [operand tile][k-step] ---------------------------
+  auto read_frags = [&](float (&af)[TM][4], float (&bf)[TN][4], const float* as, const float* bs,
+                        int g) {
 #pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int q = tid + NT * i;
-    if (A_KC) {
-      const int r = q / (BK / 4), k4 = q % (BK / 4);
-      const int64_t gm = m0 + r;
-      ka[i] = k4 * 4;
-      la[i] = r * SKC + k4 * 4;
-      pa[i] = a.A + (gm < a.M ? gm : 0) * a.lda + kb + ka[i];
-    } else {
-      const int k = q / (BM / 4), r4 = q % (BM / 4);
-      const int64_t gm = m0 + r4 * 4;
-      ka[i] = k;
-      la[i] = k * SA + r4 * 4;
-      pa[i] = a.A + (kb + k) * a.lda + (gm < a.M ? gm : 0);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int q = tid + NT * i;
-    if (B_KC) {
-      const int r = q / (BK / 4), k4 = q % (BK / 4);
-      const int64_t gnn = n0 + r;
-      kbv[i] = k4 * 4;
-      lb[i] = r * SKC + k4 * 4;
-      pb[i] = a.B + (gnn < a.N ? gnn : 0) * a.ldb + kb + kbv[i];
-    } else {
-      const int k = q / (BN / 4), r4 = q % (BN / 4);
-      const int64_t gnn = n0 + r4 * 4;
-      kbv[i] = k;
-      lb[i] = k * SB + r4 * 4;
-      pb[i] = a.B + (kb + k) * a.ldb + (gnn < a.N ? gnn : 0);
-    }
-  }
-  const int64_t stepA = A_KC ? BK : BK * a.lda;
-  const int64_t stepB = B_KC ? BK : BK * a.ldb;
-
-  float4 ra[NA], rb[NB];
-  auto load_tile = [&](int t) {
-    const int64_t k0 = kb + (int64_t)t * BK;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const float* p = pa[i] + t * stepA;
-      const bool okk = k0 + ka[i] < ke;
-      if (VEC) {
-        ra[i] = *reinterpret_cast<const float4*>(okk ? p : pa[i]);
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm0 + i * 32 + il;
+      if (A_KC) {
+        const float4 v = *reinterpret_cast<const float4*>(
+            as + r * BK + 4 * ((2 * g + h) ^ kc_swz<BK>(r)));
+        af[i][0] = v.x; af[i][1] = v.y; af[i][2] = v.z; af[i][3] = v.w;
       } else {
-        float4 v;
-        if (A_KC) {
-          v.x = (k0 + ka[i] + 0 < ke) ? p[0] : 0.f;
-          v.y = (k0 + ka[i] + 1 < ke) ? p[1] : 0.f;
-          v.z = (k0 + ka[i] + 2 < ke) ? p[2] : 0.f;
-          v.w = (k0 + ka[i] + 3 < ke) ? p[3] : 0.f;
-        } else {
-          const int64_t gm = m0 + (((tid + NT * i) % (BM / 4)) * 4);
-          v.x = (okk && gm + 0 < a.M) ? p[0] : 0.f;
-          v.y = (okk && gm + 1 < a.M) ? p[1] : 0.f;
-          v.z = (okk && gm + 2 < a.M) ? p[2] : 0.f;
-          v.w = (okk && gm + 3 < a.M) ? p[3] : 0.f;
-        }
-        ra[i] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) af[i][j] = as[(8 * g + 4 * h + j) * BM + r];
       }
     }
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const float* p = pb[i] + t * stepB;
-      const bool okk = k0 + kbv[i] < ke;
-      if (VEC) {
-        rb[i] = *reinterpret_cast<const float4*>(okk ? p : pb[i]);
+    for (int t = 0; t < TN; ++t) {
+      const int r = wn0 + t * 32 + il;
+      if (B_KC) {
+        const float4 v = *reinterpret_cast<const float4*>(
+            bs + r * BK + 4 * ((2 * g + h) ^ kc_swz<BK>(r)));
+        bf[t][0] = v.x; bf[t][1] = v.y; bf[t][2] = v.z; bf[t][3] = v.w;
       } else {
-        float4 v;
-        if (B_KC) {
-          v.x = (k0 + kbv[i] + 0 < ke) ? p[0] : 0.f;
-          v.y = (k0 + kbv[i] + 1 < ke) ? p[1] : 0.f;
-          v.z = (k0 + kbv[i] + 2 < ke) ? p[2] : 0.f;
-          v.w = (k0 + kbv[i] + 3 < ke) ? p[3] : 0.f;
-        } else {
-          const int64_t gnn = n0 + (((tid + NT * i) % (BN / 4)) * 4);
-          v.x = (okk && gnn + 0 < a.N) ? p[0] : 0.f;
-          v.y = (okk && gnn + 1 < a.N) ? p[1] : 0.f;
-          v.z = (okk && gnn + 2 < a.N) ? p[2] : 0.f;
-          v.w = (okk && gnn + 3 < a.N) ? p[3] : 0.f;
-        }
-        rb[i] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[t][j] = bs[(8 * g + 4 * h + j) * BN + r];
       }
-    }
-  };
-
-  auto store_tile = [&](int buf, int t) {
-    const int64_t k0 = kb + (int64_t)t * BK;
-    float* as = smem + buf * (A_IMG + B_IMG);
-    float* bs = as + A_IMG;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      float4 v = ra[i];
-      if (VEC && !(k0 + ka[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // K tail
-      *reinterpret_cast<float4*>(as + la[i]) = v;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      float4 v = rb[i];
-      if (VEC && !(k0 + kbv[i] < ke)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(bs + lb[i]) = v;
     }
   };
 
@@ -245,74 +217,239 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // fragments of one 8-k group: [operand tile][k-step]
-  auto read_frags = [&](float (&af)[TM][4], float (&bf)[TN][4], const float* as, const float* bs,
-                        int g) {
-    const int k0 = g * 8;
+  // one k-tile: MFMAs over one LDS stage, fragments read one 8-k group ahead
+  auto compute_tile = [&](const float* as) {
+    const float* bs = as + A_IMG;
+    float afc[TM][4], bfc[TN][4];
+    read_frags(afc, bfc, as, bs, kw * GPW);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (A_KC) {
-        const float4 v =
-            *reinterpret_cast<const float4*>(as + (wm0 + i * 32 + il) * SKC + k0 + 4 * h);
-        af[i][0] = v.x; af[i][1] = v.y; af[i][2] = v.z; af[i][3] = v.w;
-      } else {
+    for (int gg = 0; gg < GPW; ++gg) {
+      float afn[TM][4], bfn[TN][4];  // next group's fragments, read under these MFMAs
+      if (gg + 1 < GPW) read_frags(afn, bfn, as, bs, kw * GPW + gg + 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) af[i][j] = as[(k0 + 4 * h + j) * SA + wm0 + i * 32 + il];
-      }
-    }
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int t = 0; t < TN; ++t) {
-      if (B_KC) {
-        const float4 v =
-            *reinterpret_cast<const float4*>(bs + (wn0 + t * 32 + il) * SKC + k0 + 4 * h);
-        bf[t][0] = v.x; bf[t][1] = v.y; bf[t][2] = v.z; bf[t][3] = v.w;
-      } else {
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[t][j] = bs[(k0 + 4 * h + j) * SB + wn0 + t * 32 + il];
+          for (int tn = 0; tn < TN; ++tn)
+            acc[i][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(afc[i][j], bfc[tn][j],
+                                                              acc[i][tn], 0, 0, 0);
+      if (gg + 1 < GPW) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) afc[i][j] = afn[i][j];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bfc[tn][j] = bfn[tn][j];
       }
     }
   };
 
-  if (kb < ke) {
-    const int nt = (int)((ke - kb + BK - 1) / BK);
-    load_tile(0);
-    store_tile(0, 0);
-    __syncthreads();
+  // zero the LDS image positions of k >= ke (last k-tile of a split only)
+  auto zero_k_tail = [&](float* as, int64_t k0) {
+    const int kv = (int)(ke - k0);  // valid k in this tile (< BK)
+    float* bs = as + A_IMG;
+    if (A_KC) {
+      for (int q = tid; q < BM * CPR; q += NT) {
+        const int r = q / CPR, c = q % CPR;
+        if (4 * c >= kv)
+          *reinterpret_cast<float4*>(as + r * BK + 4 * (c ^ kc_swz<BK>(r))) =
+              make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+      for (int q = tid + kv * BM; q < BK * BM; q += NT) as[q] = 0.f;
+    }
+    if (B_KC) {
+      for (int q = tid; q < BN * CPR; q += NT) {
+        const int r = q / CPR, c = q % CPR;
+        if (4 * c >= kv)
+          *reinterpret_cast<float4*>(bs + r * BK + 4 * (c ^ kc_swz<BK>(r))) =
+              make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {
+      for (int q = tid + kv * BN; q < BK * BN; q += NT) bs[q] = 0.f;
+    }
+  };
+
+  if (VEC) {
+    // ---- LDS-DMA ring ----------------------------------------------------------------
+    // DMA piece q of an image = 256 consecutive floats of it; wave w issues pieces
+    // w*I .. w*I+I-1. Per lane: the source of its 16 B in piece q at k-tile 0.
+    const float* srcA[IA];
+    const float* srcB[IB];
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int q = wave * IA + j;
+      if (A_KC) {  // piece = RPP rows x CPR chunks; lane -> (row, stored chunk)
+        const int r = RPP * q + lane / CPR, p = lane % CPR;
+        const int c = p ^ kc_swz<BK>(r);
+        const int64_t gm = m0 + r;
+        srcA[j] = a.A + (gm < a.M ? gm : 0) * a.lda + kb + 4 * c;
+      } else {  // piece = floats [256q, 256q+256) of [32][BM]
+        const int idx = 256 * q + 4 * lane;
+        const int k = idx / BM, r = idx % BM;
+        const int64_t gm = m0 + r;
+        srcA[j] = a.A + (kb + k) * a.lda + (gm < a.M ? gm : 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int q = wave * IB + j;
+      if (B_KC) {
+        const int r = RPP * q + lane / CPR, p = lane % CPR;
+        const int c = p ^ kc_swz<BK>(r);
+        const int64_t gnn = n0 + r;
+        srcB[j] = a.B + (gnn < a.N ? gnn : 0) * a.ldb + kb + 4 * c;
+      } else {
+        const int idx = 256 * q + 4 * lane;
+        const int k = idx / BN, r = idx % BN;
+        const int64_t gnn = n0 + r;
+        srcB[j] = a.B + (kb + k) * a.ldb + (gnn < a.N ? gnn : 0);
+      }
+    }
+    const int64_t stepA = A_KC ? BK : BK * a.lda;
+    const int64_t stepB = B_KC ? BK : BK * a.ldb;
+    // k of each lane's float4 inside the tile (for the K tail: never read past K)
+    int kA[IA], kB[IB];
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int q = wave * IA + j;
+      kA[j] = A_KC ? 4 * ((lane % CPR) ^ kc_swz<BK>(RPP * q + lane / CPR)) : (256 * q + 4 * lane) / BM;
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int q = wave * IB + j;
+      kB[j] = B_KC ? 4 * ((lane % CPR) ^ kc_swz<BK>(RPP * q + lane / CPR)) : (256 * q + 4 * lane) / BN;
+    }
+    auto issue = [&](int t) {
+      const float* st = smem + (t % NS) * STAGE;
+      const int64_t k0 = kb + (int64_t)t * BK;
+      const bool tail = k0 + BK > ke;
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const float* src = srcA[j] + t * stepA;
+        if (tail && !(k0 + kA[j] < ke)) src = srcA[j];  // in-bounds; zeroed before use
+        glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(st + (wave * IA + j) * 256)));
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const float* src = srcB[j] + t * stepB;
+        if (tail && !(k0 + kB[j] < ke)) src = srcB[j];
+        glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(st + A_IMG + (wave * IB + j) * 256)));
+      }
+    };
+    // prologue: NS-1 tiles in flight
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nt) issue(s);
     for (int t = 0; t < nt; ++t) {
-      const int buf = t & 1;
-      const bool more = t + 1 < nt;
-      if (more) load_tile(t + 1);  // in flight under the MFMAs below
-      const float* as = smem + buf * (A_IMG + B_IMG);
-      const float* bs = as + A_IMG;
-      float afc[TM][4], bfc[TN][4];
-      read_frags(afc, bfc, as, bs, kw * GPW);
+      // this wave's pieces of k-tile t have landed when at most the later tiles' are pending
+      if (NS == 3 && t + 1 < nt) wait_vmcnt<G>();
+      else wait_vmcnt<0>();
+      block_barrier_lds();  // every wave's pieces landed; stage (t-1)%NS no longer read
+      float* st = smem + (t % NS) * STAGE;
+      if (kb + (int64_t)(t + 1) * BK > ke) {
+        zero_k_tail(st, kb + (int64_t)t * BK);
+        block_barrier_lds();
+      }
+      if (t + NS - 1 < nt) issue(t + NS - 1);
+      compute_tile(st);
+    }
+  } else {
+    // ---- register staging (unaligned / odd extents) ------------------------------------
+    float4 ra[NA], rb[NB];
+    auto load_tile = [&](int t) {
+      const int64_t k0 = kb + (int64_t)t * BK;
 #pragma unroll
-      for (int gg = 0; gg < GPW; ++gg) {
-        float afn[TM][4], bfn[TN][4];  // next group's fragments, read under these MFMAs
-        if (gg + 1 < GPW) read_frags(afn, bfn, as, bs, kw * GPW + gg + 1);
+      for (int i = 0; i < NA; ++i) {
+        const int q = tid + NT * i;
+        float4 v;
+        if (A_KC) {
+          const int r = q / CPR, c = q % CPR;
+          const int64_t gm = m0 + r;
+          const float* p = a.A + (gm < a.M ? gm : 0) * a.lda + k0 + 4 * c;
+          const int64_t k = k0 + 4 * c;
+          v.x = (k + 0 < ke) ? p[0] : 0.f;
+          v.y = (k + 1 < ke) ? p[1] : 0.f;
+          v.z = (k + 2 < ke) ? p[2] : 0.f;
+          v.w = (k + 3 < ke) ? p[3] : 0.f;
+        } else {
+          const int k = q / (BM / 4), r = 4 * (q % (BM / 4));
+          const int64_t gm = m0 + r;
+          const bool okk = k0 + k < ke;
+          const float* p = a.A + (okk ? k0 + k : kb) * a.lda + gm;
+          v.x = (okk && gm + 0 < a.M) ? p[0] : 0.f;
+          v.y = (okk && gm + 1 < a.M) ? p[1] : 0.f;
+          v.z = (okk && gm + 2 < a.M) ? p[2] : 0.f;
+          v.w = (okk && gm + 3 < a.M) ? p[3] : 0.f;
+        }
+        ra[i] = v;
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < NB; ++i) {
+        const int q = tid + NT * i;
+        float4 v;
+        if (B_KC) {
+          const int r = q / CPR, c = q % CPR;
+          const int64_t gnn = n0 + r;
+          const float* p = a.B + (gnn < a.N ? gnn : 0) * a.ldb + k0 + 4 * c;
+          const int64_t k = k0 + 4 * c;
+          v.x = (k + 0 < ke) ? p[0] : 0.f;
+          v.y = (k + 1 < ke) ? p[1] : 0.f;
+          v.z = (k + 2 < ke) ? p[2] : 0.f;
+          v.w = (k + 3 < ke) ? p[3] : 0.f;
+        } else {
+          const int k = q / (BN / 4), r = 4 * (q % (BN / 4));
+          const int64_t gnn = n0 + r;
+          const bool okk = k0 + k < ke;
+          const float* p = a.B + (okk ? k0 + k : kb) * a.ldb + gnn;
+          v.x = (okk && gnn + 0 < a.N) ? p[0] : 0.f;
+          v.y = (okk && gnn + 1 < a.N) ? p[1] : 0.f;
+          v.z = (okk && gnn + 2 < a.N) ? p[2] : 0.f;
+          v.w = (okk && gnn + 3 < a.N) ? p[3] : 0.f;
+        }
+        rb[i] = v;
+      }
+    };
+    auto store_tile = [&](float* st) {
+      float* bs = st + A_IMG;
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-              acc[i][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(afc[i][j], bfc[tn][j],
-                                                                acc[i][tn], 0, 0, 0);
-        if (gg + 1 < GPW) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) afc[i][j] = afn[i][j];
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bfc[tn][j] = bfn[tn][j];
+      for (int i = 0; i < NA; ++i) {
+        const int q = tid + NT * i;
+        if (A_KC) {
+          const int r = q / CPR, c = q % CPR;
+          *reinterpret_cast<float4*>(st + r * BK + 4 * (c ^ kc_swz<BK>(r))) = ra[i];
+        } else {
+          *reinterpret_cast<float4*>(st + 4 * q) = ra[i];
         }
       }
-      if (more) store_tile(buf ^ 1, t + 1);  // the other stage: last read one barrier ago
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int q = tid + NT * i;
+        if (B_KC) {
+          const int r = q / CPR, c = q % CPR;
+          *reinterpret_cast<float4*>(bs + r * BK + 4 * (c ^ kc_swz<BK>(r))) = rb[i];
+        } else {
+          *reinterpret_cast<float4*>(bs + 4 * q) = rb[i];
+        }
+      }
+    };
+    if (nt > 0) {
+      load_tile(0);
+      store_tile(smem);
+      __syncthreads();
+    }
+    for (int t = 0; t < nt; ++t) {
+      const bool more = t + 1 < nt;
+      if (more) load_tile(t + 1);  // in flight under the MFMAs below
+      compute_tile(smem + (t & 1) * STAGE);
+      if (more) store_tile(smem + ((t + 1) & 1) * STAGE);  // stage last read a barrier ago
       __syncthreads();
     }
   }
+  __syncthreads();  // every stage read before the buffers are reused below
 
   // in-block k-split: waves kw > 0 hand their partial tiles to wave kw = 0 through LDS
   if (KSPLIT > 1) {
@@ -327,32 +464,63 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
           for (int r = 0; r < 16; ++r) dst[((i * TN + tn) * 16 + r) * 64 + lane] = acc[i][tn][r];
     }
     __syncthreads();
-    if (kw > 0) return;
+    if (kw == 0) {
 #pragma unroll
-    for (int s = 1; s < KSPLIT; ++s) {
-      const float* src = smem + ((s - 1) * WAVES_M * WAVES_N + wmn) * PW;
+      for (int s = 1; s < KSPLIT; ++s) {
+        const float* src = smem + ((s - 1) * WAVES_M * WAVES_N + wmn) * PW;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
+          for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][tn][r] += src[((i * TN + tn) * 16 + r) * 64 + lane];
+            for (int r = 0; r < 16; ++r)
+              acc[i][tn][r] += src[((i * TN + tn) * 16 + r) * 64 + lane];
+      }
     }
+    __syncthreads();  // partials consumed before the epilogue reuses the buffer
   }
+  if (kw > 0) return;
 
-  // C/D map of the 32x32 f32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Epilogue through a wave-private 32x33 LDS tile per accumulator: the MFMA's C/D map
+  // (col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)) is written out, then read back
+  // in row order for the epilogue and the stores. Keeps the accumulator indexing static (a
+  // per-element epilogue over all TM*TN*16 values put the accumulators in scratch).
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
   const int epi = a.slab_stride ? (int)CTR_EPI_NONE : a.epi;
+  float* et = smem + wmn * (32 * 36);
+  const int er = lane >> 3, ec = 4 * (lane & 7);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
+    for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t n = n0 + wn0 + tn * 32 + il;
-        if (m < a.M && n < a.N) C[m * a.ldc + n] = apply_epi(a, epi, acc[i][tn][r], m, n);
+      for (int r = 0; r < 16; ++r) et[((r & 3) + 8 * (r >> 2) + 4 * h) * 36 + il] = acc[i][tn][r];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
+      __builtin_amdgcn_wave_barrier();
+      // lane -> row er + 8j, columns ec..ec+3: each store instruction covers 8 rows x 128 B
+      const int64_t n = n0 + wn0 + tn * 32 + ec;
+      for (int j = 0; j < 4; ++j) {
+        const int row = er + 8 * j;
+        const int64_t m = m0 + wm0 + i * 32 + row;
+        if (m >= a.M) continue;
+        const float4 v = *reinterpret_cast<const float4*>(et + row * 36 + ec);
+        float* crow = C + m * a.ldc;
+        if (a.vec_c && n + 3 < a.N) {
+          float4 o;
+          o.x = apply_epi(a, epi, v.x, m, n + 0);
+          o.y = apply_epi(a, epi, v.y, m, n + 1);
+          o.z = apply_epi(a, epi, v.z, m, n + 2);
+          o.w = apply_epi(a, epi, v.w, m, n + 3);
+          *reinterpret_cast<float4*>(crow + n) = o;
+        } else {
+          if (n + 0 < a.N) crow[n + 0] = apply_epi(a, epi, v.x, m, n + 0);
+          if (n + 1 < a.N) crow[n + 1] = apply_epi(a, epi, v.y, m, n + 1);
+          if (n + 2 < a.N) crow[n + 2] = apply_epi(a, epi, v.z, m, n + 2);
+          if (n + 3 < a.N) crow[n + 3] = apply_epi(a, epi, v.w, m, n + 3);
+        }
       }
+      __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // Split-K slabs [splits][M][N] -> C with the epilogue, summed in slab order.
@@ -370,13 +538,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const fl
 
 // Compiled tilings: (BM, BN, WAVES_M, WAVES_N, KSPLIT), 4 waves each.
 struct TileDef {
-  int bm, bn, wm, wn, ks;
-  double eff;  // sustained fraction of the 0.614 TFLOP/s per-CU fp32 MFMA peak (MI355X)
+  int bm, bn, bk, wm, wn, ks, stages;
+  double eff;  // sustained fraction of the 0.614 TFLOP/s per-CU fp32 MFMA peak, measured on
+               // MI355X per tiling (tools/gemm_bench.py, profiles/r01_gemm_tuning.txt)
 };
 static const TileDef kTiles[] = {
-    {64, 64, 2, 2, 1, 0.40},   {64, 128, 2, 2, 1, 0.50},  {128, 64, 2, 2, 1, 0.50},
-    {128, 128, 2, 2, 1, 0.60}, {64, 160, 2, 1, 2, 0.62},  {128, 416, 4, 1, 1, 0.72},
-    {160, 128, 1, 4, 1, 0.62}, {64, 224, 2, 1, 2, 0.60},
+    {64, 64, 32, 2, 2, 1, 3, 0.57},   {64, 128, 32, 2, 2, 1, 3, 0.57},
+    {128, 64, 32, 2, 2, 1, 3, 0.57},  {128, 128, 64, 2, 2, 1, 2, 0.70},
+    {64, 160, 64, 2, 1, 2, 2, 0.61},  {128, 416, 32, 4, 1, 1, 2, 0.61},
+    {160, 128, 64, 1, 4, 1, 2, 0.64}, {64, 224, 64, 2, 1, 2, 2, 0.58},
+    {64, 160, 32, 2, 1, 2, 3, 0.57},  {160, 128, 32, 1, 4, 1, 3, 0.65},
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -427,37 +598,39 @@ static TileCfg choose_tiles(int64_t M, int64_t N, int64_t K) {
   return best;
 }
 
-template <int BM, int BN, int WMW, int WNW, int KS, bool VEC>
+template <int BM, int BN, int BK, int WMW, int WNW, int KS, int PF, bool VEC>
 static void launch_vec(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
   constexpr int NT = WMW * WNW * KS * 64;
-  if (!ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, false, false, VEC>), grid, NT, 0, st, a);
-  else if (!ta && tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, false, true, VEC>), grid, NT, 0, st, a);
-  else if (ta && !tb)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, true, false, VEC>), grid, NT, 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WMW, WNW, KS, true, true, VEC>), grid, NT, 0, st, a);
+#define CTR_GEMM_LAUNCH(TA_, TB_)                                                               \
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, BK, WMW, WNW, KS, PF, TA_, TB_, VEC>), grid, NT, \
+                     0, st, a)
+  if (!ta && !tb) CTR_GEMM_LAUNCH(false, false);
+  else if (!ta && tb) CTR_GEMM_LAUNCH(false, true);
+  else if (ta && !tb) CTR_GEMM_LAUNCH(true, false);
+  else CTR_GEMM_LAUNCH(true, true);
+#undef CTR_GEMM_LAUNCH
 }
 
-template <int BM, int BN, int WMW, int WNW, int KS>
+template <int BM, int BN, int BK, int WMW, int WNW, int KS, int PF>
 static void launch_cfg(const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
   if (a.vec_a && a.vec_b)
-    launch_vec<BM, BN, WMW, WNW, KS, true>(a, ta, tb, grid, st);
+    launch_vec<BM, BN, BK, WMW, WNW, KS, PF, true>(a, ta, tb, grid, st);
   else
-    launch_vec<BM, BN, WMW, WNW, KS, false>(a, ta, tb, grid, st);
+    launch_vec<BM, BN, BK, WMW, WNW, KS, PF, false>(a, ta, tb, grid, st);
 }
 
 static void launch_tile(int ti, const GemmArgs& a, bool ta, bool tb, dim3 grid, hipStream_t st) {
   switch (ti) {
-    case 0: launch_cfg<64, 64, 2, 2, 1>(a, ta, tb, grid, st); break;
-    case 1: launch_cfg<64, 128, 2, 2, 1>(a, ta, tb, grid, st); break;
-    case 2: launch_cfg<128, 64, 2, 2, 1>(a, ta, tb, grid, st); break;
-    case 3: launch_cfg<128, 128, 2, 2, 1>(a, ta, tb, grid, st); break;
-    case 4: launch_cfg<64, 160, 2, 1, 2>(a, ta, tb, grid, st); break;
-    case 5: launch_cfg<128, 416, 4, 1, 1>(a, ta, tb, grid, st); break;
-    case 6: launch_cfg<160, 128, 1, 4, 1>(a, ta, tb, grid, st); break;
-    case 7: launch_cfg<64, 224, 2, 1, 2>(a, ta, tb, grid, st); break;
+    case 0: launch_cfg<64, 64, 32, 2, 2, 1, 3>(a, ta, tb, grid, st); break;
+    case 1: launch_cfg<64, 128, 32, 2, 2, 1, 3>(a, ta, tb, grid, st); break;
+    case 2: launch_cfg<128, 64, 32, 2, 2, 1, 3>(a, ta, tb, grid, st); break;
+    case 3: launch_cfg<128, 128, 64, 2, 2, 1, 2>(a, ta, tb, grid, st); break;
+    case 4: launch_cfg<64, 160, 64, 2, 1, 2, 2>(a, ta, tb, grid, st); break;
+    case 5: launch_cfg<128, 416, 32, 4, 1, 1, 2>(a, ta, tb, grid, st); break;
+    case 6: launch_cfg<160, 128, 64, 1, 4, 1, 2>(a, ta, tb, grid, st); break;
+    case 7: launch_cfg<64, 224, 64, 2, 1, 2, 2>(a, ta, tb, grid, st); break;
+    case 8: launch_cfg<64, 160, 32, 2, 1, 2, 3>(a, ta, tb, grid, st); break;
+    case 9: launch_cfg<160, 128, 32, 1, 4, 1, 3>(a, ta, tb, grid, st); break;
   }
 }
 
@@ -510,6 +683,7 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
             ((trans_a ? M : K) % 4 == 0);
   a.vec_b = (reinterpret_cast<uintptr_t>(B) % 16 == 0) && (ldb % 4 == 0) &&
             ((trans_b ? K : N) % 4 == 0);
+  a.vec_c = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
 
   const TileCfg c = choose_tiles(M, N, K);
   a.k_per_split = c.splits > 1 ? c.kps : std::max<int64_t>(K, 1);
@@ -524,6 +698,7 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
     a.C = static_cast<float*>(ws);
     a.ldc = N;
     a.slab_stride = M * N;
+    a.vec_c = (reinterpret_cast<uintptr_t>(ws) % 16 == 0) && (N % 4 == 0) && ((M * N) % 4 == 0);
   }
   const TileDef& d = kTiles[c.tile];
   const dim3 grid((unsigned)(ceil_div(N, d.bn) * ceil_div(M, d.bm)), 1, (unsigned)c.splits);

@@ -109,9 +109,10 @@ class PolicyGradient:
         # dense Adam state over one flat buffer holding every MLP parameter
         self._layers = [m for m in self.policy_net.mlp if isinstance(m, nn.Linear)]
         params = [t for lin in self._layers for t in (lin.weight, lin.bias)]
-        n = sum(p.numel() for p in params)
+        # 16-B aligned views (offsets multiples of 4 floats) for the GEMMs' float4 path
+        n = sum((p.numel() + 3) // 4 * 4 for p in params)
         dev = self._layers[0].weight.device
-        self._flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self._flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self._grad = torch.zeros_like(self._flat)
         self._m, self._v = torch.zeros_like(self._flat), torch.zeros_like(self._flat)
         self._gviews = []
@@ -121,7 +122,7 @@ class PolicyGradient:
             self._flat[off:off + k].copy_(p.data.reshape(-1))
             p.data = self._flat[off:off + k].view_as(p)
             self._gviews.append(self._grad[off:off + k].view_as(p))
-            off += k
+            off += (k + 3) // 4 * 4
         self._step = 0
         self.weight_decay = 1e-5  # PG_model.py:87
         self.betas, self.eps = (0.9, 0.999), 1e-8

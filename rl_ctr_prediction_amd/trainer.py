@@ -83,19 +83,22 @@ class FusedCTRTrainer:
         self.V, self.K = E.shape
         named = dict(model.named_parameters())
         self.dense_names = DEEPFM_DENSE if self.kind == "DeepFM" else FM_DENSE
-        total = sum(named[n].numel() for n in self.dense_names)
-        flat = torch.empty(total, dtype=torch.float32, device=self.device)
+        # 16-B aligned views (offsets multiples of 4 floats): the GEMMs read the weights
+        # through the float4 / LDS-DMA path only when a row start is 16-B aligned
+        self.offsets, total = {}, 0
+        for n in self.dense_names:
+            self.offsets[n] = total
+            total += (named[n].numel() + 3) // 4 * 4
+        flat = torch.zeros(total, dtype=torch.float32, device=self.device)
         self.flat_grad = torch.zeros_like(flat)
         self.views, self.grad_views = {}, {}
-        off = 0
         for n in self.dense_names:
-            p = named[n]
+            p, off = named[n], self.offsets[n]
             k = p.numel()
             flat[off:off + k].copy_(p.data.reshape(-1))
             p.data = flat[off:off + k].view_as(p)
             self.views[n] = p.data
             self.grad_views[n] = self.flat_grad[off:off + k].view_as(p)
-            off += k
         self.flat = flat
         self.m_flat = torch.zeros_like(flat)
         self.v_flat = torch.zeros_like(flat)
@@ -193,11 +196,10 @@ class FusedCTRTrainer:
                                   "params": list(range(len(named)))}]}
 
     def _split(self, flat):
-        out, off = [], 0
+        out = []
         for n in self.dense_names:
-            k = self.views[n].numel()
+            k, off = self.views[n].numel(), self.offsets[n]
             out.append(flat[off:off + k].view_as(self.views[n]))
-            off += k
         return out
 
     # --------------------------------------------------------------------- buffers ---

@@ -167,7 +167,7 @@ def test_gemm_vs_fp64(cuda, ta, tb, M, N, K):
     assert ((C - ref).abs() <= tol * bound + 1e-30).all()
 
 
-@pytest.mark.parametrize("tile", range(8))  # every compiled tiling of csrc/gemm.hip (kTiles)
+@pytest.mark.parametrize("tile", range(10))  # every compiled tiling of csrc/gemm.hip (kTiles)
 def test_gemm_every_tiling(cuda, tile, monkeypatch):
     """Force each tiling (and split-K) on shapes with M/N edges and K tails, both the float4
     path (extents % 4 == 0) and the scalar path, every transpose: fp32 parity vs fp64."""

@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--configs", default="auto," + ",".join(
-        f"{t}x{s}" for t in range(8) for s in (1, 2, 4, 8, 9, 16)))
+        f"{t}x{s}" for t in range(10) for s in (1, 2, 4, 8, 9, 16)))
     ap.add_argument("--square", type=int, default=0,
                     help="time only an NxNxN NN product (kernel's intrinsic rate)")
     args = ap.parse_args()
@@ -75,8 +75,9 @@ def main():
                   flush=True)
             if cfg != "auto" and (best is None or us < best[1]):
                 best = (cfg, us)
-        total_best += best[1]
-        print(json.dumps({"shape": name, "best": best[0], "us": round(best[1], 2)}), flush=True)
+        if best is not None:
+            total_best += best[1]
+            print(json.dumps({"shape": name, "best": best[0], "us": round(best[1], 2)}), flush=True)
     os.environ.pop("CTR_GEMM_CFG", None)
     print(json.dumps({"sum_best_us": round(total_best, 1)}))
     # correctness spot check of the auto path

@@ -1,0 +1,25 @@
+#!/bin/bash
+# PMC passes (no tracing domains) over one GEMM shape/tiling: CFG="tile,splits" SHAPE="M N K ta tb"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc_gemm
+mkdir -p $OUT
+i=0
+for P in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" \
+         "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU" \
+         "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC"; do
+  i=$((i+1))
+  CTR_GEMM_CFG=$CFG timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- \
+    python3 tools/gemm_one.py $SHAPE 20 > $OUT/p$i.log 2>&1 || exit $?
+done
+python3 - <<'PY'
+import csv, glob, collections
+agg = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/pmc_gemm/p*/**/run_counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "gemm_f32_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, v in sorted(agg.items()):
+    print(f"{k:28s} {sum(v)/len(v):16.1f}")
+PY
