@@ -218,6 +218,19 @@ int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, float* lin, 
                             float* v_lin, int64_t V, int K, int32_t* last, int64_t step,
                             const float* step_table, double beta1, double beta2, double eps,
                             double weight_decay, ctr_stream_t stream);
+/* The catch-up of ctr_adam_deferred_rows (grad_rows == NULL) taken straight from a batch's
+ * S feature ids, no sparse plan needed (the plan can then be built concurrently on another
+ * stream): duplicates are resolved through `owner`, a caller-owned int32[V] scratch (no
+ * initialisation needed); the target step is read from device memory (*step_ptr), so the
+ * call can be captured in a HIP graph. Needs K % 4 == 0 and (K/4) | 64.
+ * ctr_step_advance: *step_ptr += 1 on the stream (the device-side step counter). */
+int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float* lin,
+                                  float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
+                                  const void* idx, int idx_type, int64_t S, int32_t* owner,
+                                  const int32_t* step_ptr, const float* step_table, double beta1,
+                                  double beta2, double eps, double weight_decay,
+                                  ctr_stream_t stream);
+int ctr_step_advance(int32_t* step_ptr, ctr_stream_t stream);
 
 /* ------------------------------------------------ A7: Feature_Embedding -------------
  * out[b] = [ <E[x_bi],E[x_bj]> for i<j in row-major pair order ] ++ flat(E[x_b]),

@@ -222,6 +222,58 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
   }
 }
 
+// Catch-up straight from a batch's feature ids, without the sparse plan (so the plan can be
+// built on another stream while the forward runs). Duplicate ids are resolved through a
+// V-sized owner scratch: every slot stores its index at owner[row] (plain stores, one of
+// them survives), then the slot whose index survived replays the row. Who replays is
+// arbitrary; what is computed is not (same adam_elem chain as every other path).
+template <typename IdxT>
+__global__ __launch_bounds__(256) void deferred_mark_kernel(const IdxT* __restrict__ idx,
+                                                            int64_t S, int64_t V,
+                                                            int32_t* __restrict__ owner) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x)
+    owner[load_row(idx, s, V, nullptr)] = (int32_t)s;
+}
+
+template <typename IdxT, int K4>
+__global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
+    int32_t* __restrict__ last, const IdxT* __restrict__ idx, int64_t S, int64_t V,
+    const int32_t* __restrict__ owner, const int32_t* __restrict__ step_ptr,
+    const float* __restrict__ tab, AdamHP h) {
+  const int c = threadIdx.x % K4;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  const int step = *step_ptr;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t s = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; s < S; s += groups) {
+    const int64_t r = load_row(idx, s, V, nullptr);
+    if (owner[r] != (int32_t)s) continue;
+    const int from = last[r];
+    if (from >= step) continue;
+    const int64_t e = r * K4 + c;
+    float4 pp = E[e], mm = mE[e], vv = vE[e];
+    const bool own_lin = w && c == 0;
+    float pw = 0.f, mws = 0.f, vws = 0.f;
+    if (own_lin) {
+      pw = w[r]; mws = mw[r]; vws = vw[r];
+    }
+    for (int t = from + 1; t <= step; ++t) {
+      load_step(h, tab, t);
+      adam_vec(pp, z4, mm, vv, h);
+      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
+    }
+    E[e] = pp; mE[e] = mm; vE[e] = vv;
+    if (own_lin) {
+      w[r] = pw; mw[r] = mws; vw[r] = vws;
+    }
+    if (c == 0) last[r] = step;
+  }
+}
+
+__global__ void step_advance_kernel(int32_t* step_ptr) { *step_ptr += 1; }
+
 // Every row to `step` (epoch end / checkpoint / eval). Rows already current cost 4 B.
 // The per-step scalars of steps 1..step are staged once per block in LDS (one ds_read_b64
 // per replayed step instead of a dependent global load); the linear table has its own
@@ -528,5 +580,67 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
                      v_lin, V, K, last, nullptr, nullptr, nullptr, nullptr, (int)step, step_table,
                      h);
   CTR_LAUNCH_CHECK("deferred_flush_scalar");
+  return CTR_OK;
+}
+
+extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float* lin,
+                                             float* m_lin, float* v_lin, int64_t V, int K,
+                                             int32_t* last, const void* idx, int idx_type,
+                                             int64_t S, int32_t* owner, const int32_t* step_ptr,
+                                             const float* step_table, double beta1, double beta2,
+                                             double eps, double weight_decay,
+                                             ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && owner && step_ptr && step_table,
+              "ctr_adam_deferred_catchup_ids: null pointer");
+  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && K > 0 && S >= 0 && S < (int64_t(1) << 31),
+              "ctr_adam_deferred_catchup_ids: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_catchup_ids: linear table pointers must be all set or all NULL");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, nullptr),
+              "ctr_adam_deferred_catchup_ids: needs K %% 4 == 0, (K/4) | 64 and 16-B rows");
+  if (S == 0) return CTR_OK;
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipStream_t st = as_stream(stream);
+  const unsigned gm = (unsigned)std::min<int64_t>(ceil_div(S, 256), 4096);
+  if (idx_type == CTR_IDX_I64)
+    hipLaunchKernelGGL(deferred_mark_kernel<int64_t>, gm, 256, 0, st,
+                       static_cast<const int64_t*>(idx), S, V, owner);
+  else
+    hipLaunchKernelGGL(deferred_mark_kernel<int32_t>, gm, 256, 0, st,
+                       static_cast<const int32_t*>(idx), S, V, owner);
+  CTR_LAUNCH_CHECK("deferred_mark_kernel");
+  const int K4 = K / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(S * K4, 256), 8192);
+#define CTR_CATCHUP(IT, K4_)                                                                   \
+  hipLaunchKernelGGL((deferred_catchup_ids_vec<IT, K4_>), grid, 256, 0, st,                    \
+                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \
+                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
+                     static_cast<const IT*>(idx), S, V, owner, step_ptr, step_table, h)
+#define CTR_CATCHUP_K(IT)                  \
+  switch (K4) {                            \
+    case 1: CTR_CATCHUP(IT, 1); break;     \
+    case 2: CTR_CATCHUP(IT, 2); break;     \
+    case 4: CTR_CATCHUP(IT, 4); break;     \
+    case 8: CTR_CATCHUP(IT, 8); break;     \
+    case 16: CTR_CATCHUP(IT, 16); break;   \
+    case 32: CTR_CATCHUP(IT, 32); break;   \
+    case 64: CTR_CATCHUP(IT, 64); break;   \
+  }
+  if (idx_type == CTR_IDX_I64) {
+    CTR_CATCHUP_K(int64_t)
+  } else {
+    CTR_CATCHUP_K(int32_t)
+  }
+#undef CTR_CATCHUP_K
+#undef CTR_CATCHUP
+  CTR_LAUNCH_CHECK("deferred_catchup_ids_vec");
+  return CTR_OK;
+}
+
+extern "C" int ctr_step_advance(int32_t* step_ptr, ctr_stream_t stream) {
+  CTR_REQUIRE(step_ptr, "ctr_step_advance: null pointer");
+  hipLaunchKernelGGL(step_advance_kernel, 1, 1, 0, as_stream(stream), step_ptr);
+  CTR_LAUNCH_CHECK("step_advance_kernel");
   return CTR_OK;
 }

@@ -17,7 +17,8 @@ __all__ = [
     "embedding_gather", "fm_forward", "bce_sigmoid", "deepfm_head", "gemm", "linear",
     "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
-    "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush",
+    "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
+    "step_advance",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -371,6 +372,26 @@ def adam_deferred_rows(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "Sparse
                                _p(last), plan.struct(), _p(grad_rows), _p(grad_lin), int(step),
                                _p(tab), float(betas[0]), float(betas[1]), float(eps),
                                float(weight_decay), _stream())
+
+
+def adam_deferred_catchup_ids(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx: torch.Tensor,
+                              owner: torch.Tensor, step_dev: torch.Tensor, table: AdamStepTable,
+                              step_hint: int, betas=(0.9, 0.999), eps=1e-8,
+                              weight_decay=0.0) -> None:
+    """Bring the rows of a batch's ids to the completed step held in step_dev (device int32),
+    no sparse plan needed; owner is an int32[V] scratch. step_hint (>= the device value)
+    sizes the step table."""
+    V, K = emb.shape
+    idx, it = _idx(idx)
+    tab = table.ensure(max(step_hint, 1))
+    lib.ctr_adam_deferred_catchup_ids(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin),
+                                      V, K, _p(last), _p(idx), it, idx.numel(), _p(owner),
+                                      _p(step_dev), _p(tab), float(betas[0]), float(betas[1]),
+                                      float(eps), float(weight_decay), _stream())
+
+
+def step_advance(step_dev: torch.Tensor) -> None:
+    lib.ctr_step_advance(_p(step_dev), _stream())
 
 
 def adam_deferred_flush(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step: int,

@@ -109,8 +109,13 @@ class FusedCTRTrainer:
         if optimizer_mode not in ("deferred", "dense"):
             raise ValueError(f"optimizer_mode must be 'deferred' or 'dense', not {optimizer_mode!r}")
         self.deferred = optimizer_mode == "deferred"
+        # dense mode: row -> compact gradient slot map; deferred mode: the owner scratch of
+        # the plan-free catch-up (csrc/adam.hip deferred_mark_kernel)
         self.rowmap = torch.full((self.V,), -1, dtype=torch.int32, device=self.device)
         self.last = torch.zeros(self.V, dtype=torch.int32, device=self.device)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.device)  # completed steps
+        self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
+        self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -178,6 +183,7 @@ class FusedCTRTrainer:
         for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
             t.zero_()
         self.last.zero_()
+        self.step_dev.zero_()
         self.step_count = 0
 
     def optimizer_state_dict(self) -> dict:
@@ -242,15 +248,33 @@ class FusedCTRTrainer:
         m = self.model
         E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
         gv = self.grad_views
-        t_plan = self._mark("plan")
-        b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
-        self._span("plan", t_plan)
-        if self.deferred and self.step_count > 0:
-            t = self._mark("adam")
-            hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
-                                       b.plan, self.step_count, self.step_table, self.betas,
-                                       self.eps, self.weight_decay)
-            self._span("adam", t)
+        if self._side is not None:
+            # the sparse plan is only needed from the scatter on: build it on a side stream
+            # while the catch-up (plan-free, from the ids) and the forward run here
+            main = torch.cuda.current_stream()
+            self._side.wait_stream(main)  # x ready; previous step's plan users done
+            x.record_stream(self._side)
+            with torch.cuda.stream(self._side):
+                t_plan = self._mark("plan")
+                b.plan.build(x, self.V)
+                self._span("plan", t_plan)
+            if self.step_count > 0:
+                t = self._mark("adam")
+                hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                                                  self.last, x, self.rowmap, self.step_dev,
+                                                  self.step_table, self.step_count, self.betas,
+                                                  self.eps, self.weight_decay)
+                self._span("adam", t)
+        else:
+            t_plan = self._mark("plan")
+            b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
+            self._span("plan", t_plan)
+            if self.deferred and self.step_count > 0:
+                t = self._mark("adam")
+                hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
+                                           b.plan, self.step_count, self.step_table, self.betas,
+                                           self.eps, self.weight_decay)
+                self._span("adam", t)
         if self.kind == "FM":
             t = self._mark("gather")
             hip_ops.fm_forward(x, E, w, bias, want_sum=True, labels=y, mean_div=mean_div,
@@ -260,6 +284,8 @@ class FusedCTRTrainer:
         else:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
         hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)  # the plan
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
@@ -271,6 +297,7 @@ class FusedCTRTrainer:
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
         self.step_count += 1
+        hip_ops.step_advance(self.step_dev)
         t = self._mark("adam")
         if self.deferred:
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
