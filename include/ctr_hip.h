@@ -144,6 +144,18 @@ typedef struct ctr_sparse_plan {
 } ctr_sparse_plan;
 
 int64_t ctr_sparse_plan_workspace_bytes(int64_t S, int64_t V);
+/* Row sharding: rank j owns ids [j*shard_rows, (j+1)*shard_rows).
+ * ctr_plan_slot_to_unique: slot_to_unique[s] = the unique-row ordinal of slot s (int32[S]);
+ *   a forward over the rows received from their owners (compacted in unique order) reads
+ *   them with these ids.
+ * ctr_plan_shard_counts: counts[j] (int64[n_shards]) = how many of the plan's unique rows
+ *   shard j owns; the unique rows are ascending, so they leave grouped by owner. */
+int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique,
+                            ctr_stream_t stream);
+int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows, int n_shards,
+                          int64_t* counts, ctr_stream_t stream);
+/* ids[i] += delta (global row ids <-> shard-local row ids). */
+int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t stream);
 int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
                           void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
 

@@ -7,6 +7,8 @@ running on hand-written gfx950 HIP kernels behind the C ABI in include/ctr_hip.h
 from .feature_embedding import Feature_Embedding
 from .p_model import FM, DeepFM
 from .pg_model import Net, PolicyGradient
+from .sharded import ShardedCTRTrainer
 from .trainer import FusedCTRTrainer
 
-__all__ = ["FM", "DeepFM", "Feature_Embedding", "Net", "PolicyGradient", "FusedCTRTrainer"]
+__all__ = ["FM", "DeepFM", "Feature_Embedding", "Net", "PolicyGradient", "FusedCTRTrainer",
+           "ShardedCTRTrainer"]

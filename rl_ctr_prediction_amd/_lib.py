@@ -48,6 +48,9 @@ SIGNATURES = {
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),
     "ctr_sparse_plan_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sparse_plan_build": (_i32, [_vp, _i32, _i64, _plan_p, _vp, _i64, _vp, _vp]),
+    "ctr_plan_slot_to_unique": (_i32, [_plan_p, _vp, _vp]),
+    "ctr_plan_shard_counts": (_i32, [_plan_p, _i64, _i32, _vp, _vp]),
+    "ctr_ids_add": (_i32, [_vp, _i64, _i32, _vp]),
     "ctr_segment_workspace_bytes": (_i64, [_i64, _i32]),
     "ctr_fm_embedding_grad": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _i64, _vp]),

@@ -248,6 +248,44 @@ __global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
   }
 }
 
+// ------------------------------------------------------------ row sharding -------------
+// slot -> unique-row ordinal (the inverse of the plan's grouping): the forward of a
+// row-sharded step reads the rows it received, compacted in unique order.
+__global__ __launch_bounds__(256) void slot_to_unique_kernel(const int32_t* __restrict__ sorted_slots,
+                                                             const int32_t* __restrict__ pos_seg,
+                                                             int64_t S, int32_t* __restrict__ out) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < S;
+       p += (int64_t)gridDim.x * blockDim.x)
+    out[sorted_slots[p]] = pos_seg[p];
+}
+
+__global__ __launch_bounds__(256) void ids_add_kernel(int32_t* __restrict__ ids, int64_t n,
+                                                      int32_t delta) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    ids[i] += delta;
+}
+
+// Unique rows are ascending, so the rows of shard j (ids in [j*shard_rows, (j+1)*shard_rows))
+// are one contiguous run: counts[j] = its length, found by binary search (one thread per shard).
+__global__ void shard_counts_kernel(const int32_t* __restrict__ unique_rows,
+                                    const int32_t* __restrict__ num_unique, int64_t shard_rows,
+                                    int n_shards, int64_t* __restrict__ counts) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_shards) return;
+  const int U = *num_unique;
+  auto lower = [&](int64_t v) {  // first position with unique_rows[pos] >= v
+    int lo = 0, hi = U;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((int64_t)unique_rows[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  counts[j] = lower((int64_t)(j + 1) * shard_rows) - lower((int64_t)j * shard_rows);
+}
+
 // ------------------------------------------------------------------ host side --------
 static int key_bits(int64_t V) {
   int bits = 1;
@@ -378,5 +416,36 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
                      L.tile_heads, (int)gs, plan->pos_seg, plan->unique_rows, plan->seg_offsets,
                      plan->num_unique);
   CTR_LAUNCH_CHECK("seg_write_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique,
+                                       ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan) && slot_to_unique, "ctr_plan_slot_to_unique: bad arguments");
+  if (plan->S == 0) return CTR_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(plan->S, 256), 4096);
+  hipLaunchKernelGGL(slot_to_unique_kernel, grid, 256, 0, as_stream(stream), plan->sorted_slots,
+                     plan->pos_seg, plan->S, slot_to_unique);
+  CTR_LAUNCH_CHECK("slot_to_unique_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows,
+                                     int n_shards, int64_t* counts, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan) && counts && shard_rows > 0 && n_shards > 0,
+              "ctr_plan_shard_counts: bad arguments");
+  hipLaunchKernelGGL(shard_counts_kernel, (unsigned)ceil_div(n_shards, 64), 64, 0,
+                     as_stream(stream), plan->unique_rows, plan->num_unique, shard_rows, n_shards,
+                     counts);
+  CTR_LAUNCH_CHECK("shard_counts_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t stream) {
+  CTR_REQUIRE(n >= 0 && (ids || n == 0), "ctr_ids_add: bad arguments");
+  if (n == 0) return CTR_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), 4096);
+  hipLaunchKernelGGL(ids_add_kernel, grid, 256, 0, as_stream(stream), ids, n, delta);
+  CTR_LAUNCH_CHECK("ids_add_kernel");
   return CTR_OK;
 }

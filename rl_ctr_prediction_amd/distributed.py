@@ -64,3 +64,38 @@ def allgather_sparse_rows(rows: torch.Tensor, vals: torch.Tensor, lin: torch.Ten
     vals_all = allp[:, :K].contiguous()
     lin_all = allp[:, K].contiguous() if lin is not None else None
     return rows_all, vals_all, lin_all
+
+
+def alltoallv(send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
+              group=None) -> torch.Tensor:
+    """Variable-split all-to-all along dim 0: rank r sends send[sum(send_counts[:j]) ...]
+    (send_counts[j] rows) to rank j and receives recv_counts[j] rows from rank j, in rank
+    order. RCCL (nccl backend) moves device tensors directly over xGMI; the gloo backend
+    (CPU test runs) stages device tensors through host memory."""
+    rank, ws = world()
+    out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype,
+                      device=send.device)
+    if ws == 1:
+        out.copy_(send[:recv_counts[0]])
+        return out
+    n = sum(send_counts)
+    src = send[:n].contiguous()
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        o = out.cpu()
+        dist.all_to_all_single(o, src.cpu(), recv_counts, send_counts, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, src, recv_counts, send_counts, group=group)
+    return out
+
+
+def exchange_counts(counts: torch.Tensor, group=None) -> tuple[list[int], list[int]]:
+    """counts[j] = rows this rank sends to rank j (int64 device tensor) -> (send_counts,
+    recv_counts) host lists. One small all-to-all and one host sync per call: the
+    variable-split collectives need the sizes on the host."""
+    rank, ws = world()
+    if ws == 1:
+        c = counts.tolist()
+        return c, c
+    recv = alltoallv(counts.view(ws, 1), [1] * ws, [1] * ws, group).view(-1)
+    return counts.tolist(), recv.tolist()

@@ -18,7 +18,7 @@ __all__ = [
     "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
-    "step_advance",
+    "step_advance", "ids_add_",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -241,10 +241,13 @@ class SparsePlanBuffers:
         self.S = 0
         self._struct = SparsePlan()
 
-    def struct(self) -> SparsePlan:
+    def struct(self, rows_are_segments: bool = False) -> SparsePlan:
+        """The ctr_sparse_plan of these buffers. rows_are_segments: present each position's
+        unique-row ordinal as its row (a table compacted in unique order, row sharding)."""
         s = self._struct
         s.S = self.S
-        s.sorted_slots, s.sorted_rows = _p(self.sorted_slots), _p(self.sorted_rows)
+        s.sorted_slots = _p(self.sorted_slots)
+        s.sorted_rows = _p(self.pos_seg if rows_are_segments else self.sorted_rows)
         s.pos_seg, s.unique_rows = _p(self.pos_seg), _p(self.unique_rows)
         s.seg_offsets, s.num_unique = _p(self.seg_offsets), _p(self.num_unique)
         return s
@@ -266,13 +269,39 @@ class SparsePlanBuffers:
     def num_unique_host(self) -> int:
         return int(self.num_unique.item())
 
+    def slot_to_unique(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """int32[S]: the unique-row ordinal of every slot."""
+        if out is None:
+            out = torch.empty(max(self.capacity, 1), dtype=torch.int32, device=self.device)
+        lib.ctr_plan_slot_to_unique(self.struct(), _p(out), _stream())
+        return out
+
+    def shard_counts(self, shard_rows: int, n_shards: int,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+        """int64[n_shards]: unique rows owned by each shard (ids // shard_rows)."""
+        if out is None:
+            out = torch.empty(n_shards, dtype=torch.int64, device=self.device)
+        lib.ctr_plan_shard_counts(self.struct(), int(shard_rows), int(n_shards), _p(out), _stream())
+        return out
+
+
+def ids_add_(ids: torch.Tensor, delta: int) -> torch.Tensor:
+    """In place: ids += delta (int32 device ids)."""
+    _dev(ids, "ids")
+    if ids.dtype != torch.int32 or not ids.is_contiguous():
+        raise TypeError("ids_add_: contiguous int32 ids expected")
+    lib.ctr_ids_add(_p(ids), ids.numel(), int(delta), _stream())
+    return ids
+
 
 def _seg_ws(plan: SparsePlanBuffers, K: int):
     return Workspace.get(lib.ctr_segment_workspace_bytes(max(plan.S, 1), K), plan.device)
 
 
 def fm_embedding_grad(plan: SparsePlanBuffers, F: int, emb, gz, sum_e, dx=None, rowmap=None,
-                      grad_rows=None, grad_lin=None):
+                      grad_rows=None, grad_lin=None, compact: bool = False):
+    """Per-unique-row gradient sums. compact: `emb` holds the batch's unique rows in plan
+    order (row sharding) instead of the whole table."""
     V, K = emb.shape
     cap = max(plan.capacity, 1)
     if grad_rows is None:
@@ -280,7 +309,7 @@ def fm_embedding_grad(plan: SparsePlanBuffers, F: int, emb, gz, sum_e, dx=None, 
     if grad_lin is None:
         grad_lin = torch.empty(cap, dtype=torch.float32, device=emb.device)
     ws = _seg_ws(plan, K)
-    lib.ctr_fm_embedding_grad(plan.struct(), int(F), int(K), _p(emb), _p(gz), _p(sum_e), _p(dx),
+    lib.ctr_fm_embedding_grad(plan.struct(compact), int(F), int(K), _p(emb), _p(gz), _p(sum_e), _p(dx),
                               _p(grad_rows), _p(grad_lin), _p(rowmap), _p(ws), ws.numel(),
                               _stream())
     return grad_rows, grad_lin

@@ -1,0 +1,173 @@
+"""Row-sharded data parallelism for the CTR step (BASELINE configs C3 at 8
+GPUs and C5, the 40M-row table "sharded across 8xMI355X with RCCL all-to-all").
+
+Rank r of N owns the embedding rows [r*Vs, (r+1)*Vs), Vs = ceil(V/N): their Adam moments,
+their deferred-replay state and their updates. Every rank trains its own batch (weak
+scaling); per step:
+
+  1. sparse plan of the local batch (global ids); its unique rows are ascending, hence
+     grouped by owner -> per-owner counts (ctr_plan_shard_counts), one tiny all-to-all of
+     counts (the only host sync: variable-split collectives need sizes on the host);
+  2. all-to-all of the unique row ids to their owners (each rank asks for each row once);
+  3. owners bring the requested rows up to date (plan-free deferred catch-up: duplicates
+     across requesters resolved by the owner scratch), gather E[row] and w[row] and send
+     them back (all-to-all): every rank now holds its batch's rows compacted in unique order;
+  4. forward + backward locally over that compact table (slot -> unique ordinal ids), the
+     per-row gradient sums in plan order (the same kernels as the single-GPU step);
+  5. all-to-all of the per-row gradients to the owners, which sum them per row in (source
+     rank, position) order (a sparse plan over the received ids + the deterministic
+     segmented sum) and apply Adam to their rows; the dense MLP gradient goes through one
+     all-reduce as in the replicated path.
+
+Per rank and step at C3 with 8 GPUs: ~61k unique rows out and back (ids 0.25 MB, rows and
+gradients 16 MB each way) instead of all-gathering every rank's 16 MB of row gradients;
+the deferred flush and the catch-up/apply work cover V/N rows. With N = 1 every exchange
+is a local copy and the step is bitwise the single-GPU FusedCTRTrainer step
+(tests/test_gpu_sharded.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import hip_ops
+from .distributed import allreduce_sum_, alltoallv, exchange_counts, world
+from .trainer import FusedCTRTrainer
+
+
+class ShardedCTRTrainer(FusedCTRTrainer):
+    """FusedCTRTrainer over this rank's row shard of the embedding tables (deferred-exact
+    Adam). Rows outside the shard keep their initial values in this rank's copy of the
+    model; gather_tables() assembles the trained tables."""
+
+    def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
+                 eps: float = 1e-8, process_group=None, seed: int | None = None):
+        self.rank, self.world_size = world()
+        V = model.feature_embedding.weight.shape[0]
+        if V < self.world_size:
+            raise ValueError(f"row sharding: vocabulary {V} smaller than world size")
+        self.shard_rows = -(-V // self.world_size)
+        super().__init__(model, lr=lr, weight_decay=weight_decay, betas=betas, eps=eps,
+                         process_group=process_group, seed=seed, optimizer_mode="deferred")
+        if not self._vec_ok:
+            raise ValueError("row sharding needs K % 4 == 0 and (K/4) dividing 64")
+        self._side = None  # the exchange needs the plan before anything else
+        self._slot2u = None
+        self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+
+    def _buffers(self, B: int, F: int):
+        b = super()._buffers(B, F)
+        if b.gplan is None:  # world size 1: the owner-side plan is still needed
+            S = B * F * self.world_size
+            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+            b.gplan = hip_ops.SparsePlanBuffers(S, self.device)
+            b.g_rows, b.g_lin = e(S, self.K), e(S)
+        return b
+
+    def _table_rows(self) -> tuple[int, int]:
+        lo = min(self.rank * self.shard_rows, self.V)
+        return lo, min(lo + self.shard_rows, self.V)
+
+    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
+        B, F = x.shape
+        ws = self.world_size
+        mean_div = float(global_batch if global_batch is not None else B * ws)
+        b = self._buffers(B, F)
+        if self._slot2u is None or self._slot2u.numel() < B * F:
+            self._slot2u = torch.empty(B * F, dtype=torch.int32, device=self.device)
+        y = y.reshape(-1)
+        if y.dtype != torch.float32:
+            y = y.float()
+        y = y.contiguous()
+        bias, gv = self.views["bias"], self.grad_views
+
+        # 1. plan of the local batch, per-owner counts of its unique rows
+        t = self._mark("plan")
+        b.plan.build(x, self.V, err_flag=self.err)
+        b.plan.shard_counts(self.shard_rows, ws, out=self._counts)
+        self._span("plan", t)
+        send_c, recv_c = exchange_counts(self._counts, self.group)
+        # 2. unique row ids to their owners, as shard-local ids
+        t = self._mark("exchange")
+        req = alltoallv(b.plan.unique_rows, send_c, recv_c, self.group)
+        hip_ops.ids_add_(req, -self.row_lo)
+        self._span("exchange", t)
+        # 3. owners: catch the rows up, send them back
+        t = self._mark("adam")
+        hip_ops.adam_deferred_catchup_ids(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                          self.v_w, self.last, req, self.rowmap, self.step_dev,
+                                          self.step_table, self.step_count + 1, self.betas,
+                                          self.eps, self.weight_decay)
+        self._span("adam", t)
+        t = self._mark("exchange")
+        rows = hip_ops.embedding_gather(self.E_tab, req)
+        lin = hip_ops.embedding_gather(self.w_tab, req)
+        T = alltoallv(rows, recv_c, send_c, self.group)
+        T_lin = alltoallv(lin, recv_c, send_c, self.group).view(-1)
+        self._span("exchange", t)
+        # 4. forward + backward over the compact table
+        ids = b.plan.slot_to_unique(out=self._slot2u)[:B * F].view(B, F)
+        if self.kind == "FM":
+            t = self._mark("gather")
+            hip_ops.fm_forward(ids, T, T_lin, bias, want_sum=True, labels=y, mean_div=mean_div,
+                               want_p=False, out=b.fm)
+            self._span("gather", t)
+            gz = b.fm.gz
+        else:
+            gz = self._deepfm_forward_backward(ids, y, b, T, T_lin, bias, mean_div)
+        hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        t = self._mark("scatter")
+        hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
+                                  grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
+        self._span("scatter", t)
+        hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
+        # 5. gradients to the owners, summed per row in (source rank, position) order
+        t = self._mark("exchange")
+        G = alltoallv(b.grad_rows, send_c, recv_c, self.group)
+        G_lin = alltoallv(b.grad_lin, send_c, recv_c, self.group)
+        allreduce_sum_(self.flat_grad, self.group)
+        if ws > 1:
+            allreduce_sum_(b.loss, self.group)
+            b.loss.div_(ws)
+        self._span("exchange", t)
+        t = self._mark("scatter")
+        b.gplan.build(req, self.V_tab)
+        hip_ops.segment_sum_rows(b.gplan, G, G_lin, rowmap=None, out=b.g_rows, out_lin=b.g_lin)
+        self._span("scatter", t)
+        self.step_count += 1
+        hip_ops.step_advance(self.step_dev)
+        t = self._mark("adam")
+        hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                   self.v_w, self.last, b.gplan, self.step_count,
+                                   self.step_table, self.betas, self.eps, self.weight_decay,
+                                   grad_rows=b.g_rows, grad_lin=b.g_lin)
+        self._span("adam", t)
+        self._dirty = True
+        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
+                           self.lr, self.betas, self.eps, self.weight_decay)
+        return b.loss
+
+    def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """Full (E [V,K], w [V,1]) assembled from every rank's shard (after a flush)."""
+        self.flush()
+        E = self.model.feature_embedding.weight.data
+        w = self.model.linear.weight.data
+        if self.world_size == 1:
+            return E.clone(), w.clone()
+        pad = self.shard_rows * self.world_size
+        outE = torch.empty(pad, self.K, dtype=E.dtype, device=E.device)
+        outw = torch.empty(pad, 1, dtype=w.dtype, device=w.device)
+        sendE = torch.zeros(self.shard_rows, self.K, dtype=E.dtype, device=E.device)
+        sendw = torch.zeros(self.shard_rows, 1, dtype=w.dtype, device=w.device)
+        sendE[:self.V_tab] = self.E_tab
+        sendw[:self.V_tab] = self.w_tab
+        if E.is_cuda and dist.get_backend(self.group) == "gloo":
+            oE, ow = outE.cpu(), outw.cpu()
+            dist.all_gather_into_tensor(oE, sendE.cpu(), group=self.group)
+            dist.all_gather_into_tensor(ow, sendw.cpu(), group=self.group)
+            outE.copy_(oE)
+            outw.copy_(ow)
+        else:
+            dist.all_gather_into_tensor(outE, sendE, group=self.group)
+            dist.all_gather_into_tensor(outw, sendw, group=self.group)
+        return outE[:self.V], outw[:self.V]

@@ -98,3 +98,71 @@ def test_sparse_exchange_world2_gloo():
     # both ranks received the same concatenation (rank order), so their re-sums agree bitwise
     np.testing.assert_array_equal(res[0][3], res[1][3])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+# ------------------------------------------------------------ row-sharded exchange ----
+def _shard_worker(rank, world, port, q):
+    """The ShardedCTRTrainer protocol with numpy standing in for the GPU kernels (plan,
+    shard counts, gather, segmented sum): ids to owners, rows back, gradients to owners."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rl_ctr_prediction_amd.distributed import alltoallv, exchange_counts
+        V, K = 1000, 4
+        shard = -(-V // world)
+        lo, hi = rank * shard, min(V, (rank + 1) * shard)
+        table = np.arange(V * K, dtype=np.float32).reshape(V, K)   # the same on every rank
+        rng = np.random.default_rng(7 + rank)
+        ids = rng.integers(0, V, size=500 + 111 * rank)
+        ids[:50] = 3                                               # a hot row on every rank
+        uniq = np.unique(ids)                                      # the plan's unique rows
+        counts = np.array([((uniq >= j * shard) & (uniq < (j + 1) * shard)).sum()
+                           for j in range(world)], dtype=np.int64)  # ctr_plan_shard_counts
+        send_c, recv_c = exchange_counts(torch.tensor(counts))
+        req = alltoallv(torch.tensor(uniq, dtype=torch.int32), send_c, recv_c)
+        loc = req.numpy() - lo
+        assert ((loc >= 0) & (loc < hi - lo)).all()                # every request is mine
+        rows = torch.tensor(table[lo:hi][loc])                     # owner gathers its rows
+        got = alltoallv(rows, recv_c, send_c).numpy()
+        np.testing.assert_array_equal(got, table[uniq])            # rows back in unique order
+        # per-row gradient of this rank: count of the row in the batch x (rank + 1)
+        cnt = np.array([(ids == u).sum() for u in uniq], dtype=np.float32)
+        grads = torch.tensor(np.repeat((cnt * (rank + 1))[:, None], K, axis=1))
+        G = alltoallv(grads, send_c, recv_c).numpy()
+        keys = req.numpy()
+        u_o = np.unique(keys)
+        sums = np.stack([G[keys == u].sum(0) for u in u_o]) if u_o.size else np.zeros((0, K))
+        q.put((rank, u_o, sums))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_exchange_world3_gloo():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    V, K = 1000, 4
+    shard = -(-V // world)
+    expect = np.zeros(V)
+    for rank in range(world):
+        rng = np.random.default_rng(7 + rank)
+        ids = rng.integers(0, V, size=500 + 111 * rank)
+        ids[:50] = 3
+        np.add.at(expect, ids, rank + 1)
+    for rank in range(world):
+        u_o, sums = res[rank]
+        assert ((u_o >= rank * shard) & (u_o < (rank + 1) * shard)).all()
+        np.testing.assert_array_equal(u_o, np.nonzero(expect[rank * shard:(rank + 1) * shard])[0]
+                                      + rank * shard)
+        np.testing.assert_allclose(sums[:, 0], expect[u_o])
