@@ -125,6 +125,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         t = self._mark("exchange")
         G = alltoallv(b.grad_rows, send_c, recv_c, self.group)
         G_lin = alltoallv(b.grad_lin, send_c, recv_c, self.group)
+        self._join_wgrad()
         allreduce_sum_(self.flat_grad, self.group)
         if ws > 1:
             allreduce_sum_(b.loss, self.group)

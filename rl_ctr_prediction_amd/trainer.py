@@ -35,6 +35,14 @@ from . import hip_ops
 from .distributed import allgather_sparse_rows, allreduce_sum_, world
 from .p_model import FM, DeepFM
 
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
 DEEPFM_DENSE = ("bias", "mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bias",
                 "mlp.6.weight", "mlp.6.bias")
 FM_DENSE = ("bias",)
@@ -122,6 +130,7 @@ class FusedCTRTrainer:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.device)  # completed steps
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
+        self._wgrad_stream = torch.cuda.Stream(device=self.device) if self.kind == "DeepFM" else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -302,6 +311,7 @@ class FusedCTRTrainer:
         hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         grad_rows, grad_lin, plan = b.grad_rows, b.grad_lin, b.plan
         if ws > 1:
+            self._join_wgrad()  # the exchange all-reduces the dense gradient
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
         self.step_count += 1
@@ -318,6 +328,7 @@ class FusedCTRTrainer:
                                    grad_rows, grad_lin, self.step_count, self.lr, self.betas,
                                    self.eps, self.weight_decay)
         self._span("adam", t)
+        self._join_wgrad()
         hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
                            self.lr, self.betas, self.eps, self.weight_decay)
         return b.loss
@@ -343,19 +354,32 @@ class FusedCTRTrainer:
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]
-        # Linear(200,1): dW = gz^T H2, db = sum gz
-        hip_ops.colsum(b.h2, row_w=gz, out=gv["mlp.6.weight"].view(-1))
-        hip_ops.tensor_sum(gz, out=gv["mlp.6.bias"].view(1))
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
                    scale=1.0 / (1.0 - p0), out=b.dh1)
-        self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
-        hip_ops.colsum(dh2, out=gv["mlp.3.bias"])
-        # Linear(F*K,300): dX = dH1 @ W0 (the MLP-input gradient), dW0 = dH1^T X
+        # Linear(F*K,300): dX = dH1 @ W0, the MLP-input gradient the scatter needs
         self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
-        self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
-        hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
+        # the weight / bias gradients are needed only by the dense Adam at the end of the
+        # step: on the side stream they run under the scatter and the embedding Adam
+        side = self._wgrad_stream
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            # Linear(200,1): dW = gz^T H2, db = sum gz
+            hip_ops.colsum(b.h2, row_w=gz, out=gv["mlp.6.weight"].view(-1))
+            hip_ops.tensor_sum(gz, out=gv["mlp.6.bias"].view(1))
+            # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2
+            self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
+            hip_ops.colsum(dh2, out=gv["mlp.3.bias"])
+            # Linear(F*K,300): dW0 = dH1^T X, db0 = colsum dH1
+            self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
+            hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
         return gz
+
+    def _join_wgrad(self) -> None:
+        """The dense-parameter gradients are complete on the current stream after this."""
+        if self._wgrad_stream is not None and self.kind == "DeepFM":
+            torch.cuda.current_stream().wait_stream(self._wgrad_stream)
 
     def _exchange(self, b: _Bufs):
         """Sum embedding-row gradients over ranks (deterministic, identical everywhere)."""
