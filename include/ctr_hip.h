@@ -101,7 +101,9 @@ int ctr_deepfm_head(const float* h, int64_t B, int H, const float* w_out, const 
  * trans_a = 0: A stored [M,K] (lda >= K); 1: A stored [K,M] (lda >= M).
  * trans_b = 0: B stored [K,N] (ldb >= N); 1: B stored [N,K] (ldb >= K)  (nn.Linear weight).
  * Dropout keeps element (m,n) iff hash(seed, offset + m*N + n) >= p*2^32 and scales by
- * 1/(1-p). `scale` is used by CTR_EPI_GRAD_MASK. Split-K (long K, few tiles) uses `ws`.
+ * 1/(1-p), where offset += (*step_ptr) << 32 when step_ptr != NULL (a per-step mask read
+ * on the device, for HIP-graph replay). `scale` is used by CTR_EPI_GRAD_MASK. Split-K
+ * (long K, few tiles) uses `ws`.
  * Replaces: nn.Linear / ReLU / Dropout of DeepFM.mlp (p_model.py:276-293) and of
  * PG_model.Net.mlp (PG_model.py:41-51), forward and autograd backward (dX and dW). */
 int64_t ctr_gemm_f32_workspace_bytes(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K);
@@ -109,7 +111,7 @@ int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                  const float* A, int64_t lda, const float* B, int64_t ldb,
                  float* C, int64_t ldc, int epi, const float* bias,
                  const float* aux, int64_t ldaux, float scale,
-                 float drop_p, uint64_t seed, uint64_t offset,
+                 float drop_p, uint64_t seed, uint64_t offset, const int32_t* step_ptr,
                  void* ws, int64_t ws_bytes, ctr_stream_t stream);
 
 /* Deterministic reductions (fixed order; identical bits run to run).
@@ -197,15 +199,21 @@ int ctr_rows_to_dense(const ctr_sparse_plan* plan, int K, const float* grad_rows
  * ctr_adam_embedding: the embedding table E[V,K] and the linear table w[V] in one pass;
  *   the gradient of row r is grad_rows[rowmap[r]] when rowmap[r] >= 0, else 0; rowmap
  *   entries read >= 0 are reset to -1. lin/m_lin/v_lin may be NULL (Feature tables w/o
- *   a linear term). Replaces: torch.optim.Adam.step at all_main/pretrain_main.py:78,153. */
+ *   a linear term).
+ * Device step (HIP-graph replay): with step_ptr != NULL the step t = *step_ptr is read on
+ * the device and the scalars come from step_table (layout of ctr_adam_deferred_rows
+ * below); step_size / bc2_sqrt are then ignored.
+ * Replaces: torch.optim.Adam.step at all_main/pretrain_main.py:78,153. */
 int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n, double step_size,
-                   double bc2_sqrt, double beta1, double beta2, double eps, double weight_decay,
+                   double bc2_sqrt, const float* step_table, const int32_t* step_ptr,
+                   double beta1, double beta2, double eps, double weight_decay,
                    ctr_stream_t stream);
 int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                        float* v_lin, int64_t V, int K, int32_t* rowmap,
                        const float* grad_rows, const float* grad_lin, double step_size,
-                       double bc2_sqrt, double beta1, double beta2, double eps,
-                       double weight_decay, ctr_stream_t stream);
+                       double bc2_sqrt, const float* step_table, const int32_t* step_ptr,
+                       double beta1, double beta2, double eps, double weight_decay,
+                       ctr_stream_t stream);
 
 /* Deferred-exact dense Adam (temporal blocking) — same results as ctr_adam_embedding,
  * bitwise. A row absent from a batch is updated with g = wd*p, a function of its own state;
@@ -219,13 +227,14 @@ int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float
  *     with their gradient (grad_rows[u], grad_lin[u] for unique row u);
  *   ctr_adam_deferred_flush: bring every row to `step` (before anything else reads the
  *     tables: epoch end, checkpoint, evaluation).
+ * ctr_adam_deferred_rows reads the step from *step_ptr on the device when step_ptr != NULL.
  * Replaces: torch.optim.Adam.step at all_main/pretrain_main.py:78 over nn.Embedding weights. */
 int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                            float* v_lin, int64_t V, int K, int32_t* last,
                            const ctr_sparse_plan* plan, const float* grad_rows,
-                           const float* grad_lin, int64_t step, const float* step_table,
-                           double beta1, double beta2, double eps, double weight_decay,
-                           ctr_stream_t stream);
+                           const float* grad_lin, int64_t step, const int32_t* step_ptr,
+                           const float* step_table, double beta1, double beta2, double eps,
+                           double weight_decay, ctr_stream_t stream);
 int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                             float* v_lin, int64_t V, int K, int32_t* last, int64_t step,
                             const float* step_table, double beta1, double beta2, double eps,

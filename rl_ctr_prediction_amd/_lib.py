@@ -42,7 +42,7 @@ SIGNATURES = {
                                _vp, _vp, _vp]),
     "ctr_gemm_f32_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
     "ctr_gemm_f32": (_i32, [_i32, _i32, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i32,
-                            _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _i64, _vp]),
+                            _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp, _i64, _vp]),
     "ctr_reduce_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sum_f32": (_i32, [_vp, _i64, _f32, _vp, _vp, _i64, _vp]),
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),
@@ -56,11 +56,12 @@ SIGNATURES = {
                                      _vp, _i64, _vp]),
     "ctr_segment_sum_rows": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "ctr_rows_to_dense": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp]),
-    "ctr_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _f64, _f64, _f64, _f64, _vp]),
+    "ctr_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp, _vp, _f64, _f64, _f64,
+                              _f64, _vp]),
     "ctr_adam_embedding": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _f64,
-                                  _f64, _f64, _f64, _f64, _f64, _vp]),
+                                  _f64, _vp, _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_rows": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _plan_p, _vp,
-                                      _vp, _i64, _vp, _f64, _f64, _f64, _f64, _vp]),
+                                      _vp, _i64, _vp, _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_catchup_ids": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
                                              _i32, _i64, _vp, _vp, _vp, _f64, _f64, _f64, _f64,
                                              _vp]),

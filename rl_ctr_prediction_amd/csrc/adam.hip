@@ -59,11 +59,16 @@ __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4&
 }
 
 // ------------------------------------------------------------------ dense -----------
+// step_ptr != NULL: the step's scalars come from the device step table (HIP-graph replay)
+__device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s);
+
 __global__ __launch_bounds__(256) void adam_dense_vec(float4* __restrict__ p,
                                                       const float4* __restrict__ g,
                                                       float4* __restrict__ m,
                                                       float4* __restrict__ v, int64_t n4,
-                                                      AdamHP h) {
+                                                      AdamHP h, const float* __restrict__ tab,
+                                                      const int32_t* __restrict__ step_ptr) {
+  if (step_ptr) load_step(h, tab, *step_ptr);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = p[i], mm = m[i], vv = v[i];
@@ -78,7 +83,10 @@ __global__ __launch_bounds__(256) void adam_dense_scalar(float* __restrict__ p,
                                                          const float* __restrict__ g,
                                                          float* __restrict__ m,
                                                          float* __restrict__ v, int64_t lo,
-                                                         int64_t n, AdamHP h) {
+                                                         int64_t n, AdamHP h,
+                                                         const float* __restrict__ tab,
+                                                         const int32_t* __restrict__ step_ptr) {
+  if (step_ptr) load_step(h, tab, *step_ptr);
   for (int64_t i = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pp = p[i], mm = m[i], vv = v[i];
@@ -100,7 +108,9 @@ __global__ __launch_bounds__(256) void adam_embedding_vec(
     float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
     float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
     int32_t* __restrict__ rowmap, const float4* __restrict__ grows,
-    const float* __restrict__ glin, AdamHP h) {
+    const float* __restrict__ glin, AdamHP h, const float* __restrict__ tab,
+    const int32_t* __restrict__ step_ptr) {
+  if (step_ptr) load_step(h, tab, *step_ptr);
   constexpr int RPI = kWave / K4;  // rows per wave-instruction
   constexpr int ITERS = kWave / RPI;
   const int lane = threadIdx.x & (kWave - 1);
@@ -146,7 +156,9 @@ __global__ __launch_bounds__(256) void adam_embedding_scalar(
     float* __restrict__ E, float* __restrict__ mE, float* __restrict__ vE, float* __restrict__ w,
     float* __restrict__ mw, float* __restrict__ vw, int64_t V, int K,
     int32_t* __restrict__ rowmap, const float* __restrict__ grows,
-    const float* __restrict__ glin, AdamHP h) {
+    const float* __restrict__ glin, AdamHP h, const float* __restrict__ tab,
+    const int32_t* __restrict__ step_ptr) {
+  if (step_ptr) load_step(h, tab, *step_ptr);
   for (int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; row < V;
        row += (int64_t)gridDim.x * blockDim.x) {
     const int32_t u = rowmap[row];
@@ -187,10 +199,12 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
     float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
     int32_t* __restrict__ last, const int32_t* __restrict__ rows,
     const int32_t* __restrict__ num_unique, const float4* __restrict__ grows,
-    const float* __restrict__ glin, int step, const float* __restrict__ tab, AdamHP h) {
+    const float* __restrict__ glin, int step_val, const int32_t* __restrict__ step_ptr,
+    const float* __restrict__ tab, AdamHP h) {
   const int c = threadIdx.x % K4;
   const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
   const int U = *num_unique;
+  const int step = step_ptr ? *step_ptr : step_val;
   const int target = APPLY ? step - 1 : step;
   for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; u < U; u += groups) {
     const int64_t r = rows[u];
@@ -336,7 +350,9 @@ __global__ __launch_bounds__(256) void deferred_scalar(
     float* __restrict__ mw, float* __restrict__ vw, int64_t n_rows, int K,
     int32_t* __restrict__ last, const int32_t* __restrict__ rows,
     const int32_t* __restrict__ num_unique, const float* __restrict__ grows,
-    const float* __restrict__ glin, int step, const float* __restrict__ tab, AdamHP h) {
+    const float* __restrict__ glin, int step_val, const int32_t* __restrict__ step_ptr,
+    const float* __restrict__ tab, AdamHP h) {
+  const int step = step_ptr ? *step_ptr : step_val;
   const int64_t n = rows ? (int64_t)*num_unique : n_rows;
   const int target = APPLY ? step - 1 : step;
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < n;
@@ -393,13 +409,16 @@ static AdamHP make_hp(double step_size, double bc2_sqrt, double beta1, double be
 using namespace ctr;
 
 extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n,
-                              double step_size, double bc2_sqrt, double beta1, double beta2,
-                              double eps, double weight_decay, ctr_stream_t stream) {
+                              double step_size, double bc2_sqrt, const float* step_table,
+                              const int32_t* step_ptr, double beta1, double beta2, double eps,
+                              double weight_decay, ctr_stream_t stream) {
   CTR_REQUIRE(n >= 0, "ctr_adam_dense: n < 0");
   if (n == 0) return CTR_OK;
   CTR_REQUIRE(p && g && m && v, "ctr_adam_dense: null pointer");
-  CTR_REQUIRE(bc2_sqrt > 0.0, "ctr_adam_dense: bc2_sqrt must be > 0");
-  const AdamHP h = make_hp(step_size, bc2_sqrt, beta1, beta2, eps, weight_decay);
+  CTR_REQUIRE(step_ptr ? step_table != nullptr : bc2_sqrt > 0.0,
+              "ctr_adam_dense: bc2_sqrt must be > 0 (or step_table given with step_ptr)");
+  const AdamHP h = make_hp(step_ptr ? 1.0 : step_size, step_ptr ? 1.0 : bc2_sqrt, beta1, beta2,
+                           eps, weight_decay);
   hipStream_t st = as_stream(stream);
   const bool al = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
   int64_t done = 0;
@@ -408,13 +427,14 @@ extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int6
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 4096);
     hipLaunchKernelGGL(adam_dense_vec, grid, 256, 0, st, reinterpret_cast<float4*>(p),
                        reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m),
-                       reinterpret_cast<float4*>(v), n4, h);
+                       reinterpret_cast<float4*>(v), n4, h, step_table, step_ptr);
     CTR_LAUNCH_CHECK("adam_dense_vec");
     done = n4 * 4;
   }
   if (done < n) {
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n - done, 256), 4096);
-    hipLaunchKernelGGL(adam_dense_scalar, grid, 256, 0, st, p, g, m, v, done, n, h);
+    hipLaunchKernelGGL(adam_dense_scalar, grid, 256, 0, st, p, g, m, v, done, n, h, step_table,
+                       step_ptr);
     CTR_LAUNCH_CHECK("adam_dense_scalar");
   }
   return CTR_OK;
@@ -423,14 +443,17 @@ extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int6
 extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                                   float* v_lin, int64_t V, int K, int32_t* rowmap,
                                   const float* grad_rows, const float* grad_lin,
-                                  double step_size, double bc2_sqrt, double beta1, double beta2,
+                                  double step_size, double bc2_sqrt, const float* step_table,
+                                  const int32_t* step_ptr, double beta1, double beta2,
                                   double eps, double weight_decay, ctr_stream_t stream) {
   CTR_REQUIRE(emb && m_emb && v_emb && rowmap && grad_rows, "ctr_adam_embedding: null pointer");
   CTR_REQUIRE(V > 0 && K > 0, "ctr_adam_embedding: bad sizes");
   CTR_REQUIRE((lin && m_lin && v_lin && grad_lin) || (!lin && !m_lin && !v_lin),
               "ctr_adam_embedding: linear table pointers must be all set or all NULL");
-  CTR_REQUIRE(bc2_sqrt > 0.0, "ctr_adam_embedding: bc2_sqrt must be > 0");
-  const AdamHP h = make_hp(step_size, bc2_sqrt, beta1, beta2, eps, weight_decay);
+  CTR_REQUIRE(step_ptr ? step_table != nullptr : bc2_sqrt > 0.0,
+              "ctr_adam_embedding: bc2_sqrt must be > 0 (or step_table given with step_ptr)");
+  const AdamHP h = make_hp(step_ptr ? 1.0 : step_size, step_ptr ? 1.0 : bc2_sqrt, beta1, beta2,
+                           eps, weight_decay);
   hipStream_t st = as_stream(stream);
   const bool al =
       ((uintptr_t)emb | (uintptr_t)m_emb | (uintptr_t)v_emb | (uintptr_t)grad_rows) % 16 == 0;
@@ -442,7 +465,8 @@ extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float*
   hipLaunchKernelGGL((adam_embedding_vec<K4_>), grid, 256, 0, st,                             \
                      reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
                      reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, rowmap,          \
-                     reinterpret_cast<const float4*>(grad_rows), grad_lin, h)
+                     reinterpret_cast<const float4*>(grad_rows), grad_lin, h, step_table,      \
+                     step_ptr)
     switch (K4) {
       case 1: CTR_ADAM_VEC(1); break;
       case 2: CTR_ADAM_VEC(2); break;
@@ -458,7 +482,7 @@ extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float*
   }
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
   hipLaunchKernelGGL(adam_embedding_scalar, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin, v_lin,
-                     V, K, rowmap, grad_rows, grad_lin, h);
+                     V, K, rowmap, grad_rows, grad_lin, h, step_table, step_ptr);
   CTR_LAUNCH_CHECK("adam_embedding_scalar");
   return CTR_OK;
 }
@@ -471,12 +495,12 @@ static bool deferred_vec_ok(int K, const void* a, const void* b, const void* c, 
 extern "C" int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, float* lin,
                                       float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
                                       const ctr_sparse_plan* plan, const float* grad_rows,
-                                      const float* grad_lin, int64_t step, const float* step_table,
-                                      double beta1, double beta2, double eps, double weight_decay,
-                                      ctr_stream_t stream) {
+                                      const float* grad_lin, int64_t step, const int32_t* step_ptr,
+                                      const float* step_table, double beta1, double beta2,
+                                      double eps, double weight_decay, ctr_stream_t stream) {
   CTR_REQUIRE(emb && m_emb && v_emb && last && step_table, "ctr_adam_deferred_rows: null pointer");
   CTR_REQUIRE(plan && plan->unique_rows && plan->num_unique, "ctr_adam_deferred_rows: bad plan");
-  CTR_REQUIRE(V > 0 && K > 0 && step >= 1 && step < (int64_t(1) << 31),
+  CTR_REQUIRE(V > 0 && K > 0 && (step_ptr || (step >= 1 && step < (int64_t(1) << 31))),
               "ctr_adam_deferred_rows: bad sizes");
   CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
               "ctr_adam_deferred_rows: linear table pointers must be all set or all NULL");
@@ -496,13 +520,13 @@ extern "C" int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, fl
                        reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
                        plan->unique_rows, plan->num_unique,                                      \
                        reinterpret_cast<const float4*>(grad_rows), grad_lin, (int)step,          \
-                       step_table, h);                                                           \
+                       step_ptr, step_table, h);                                                 \
   else                                                                                           \
     hipLaunchKernelGGL((deferred_rows_vec<K4_, false>), grid, 256, 0, st,                        \
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \
                        reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
                        plan->unique_rows, plan->num_unique, nullptr, nullptr, (int)step,         \
-                       step_table, h)
+                       step_ptr, step_table, h)
     switch (K4) {
       case 1: CTR_DEF_ROWS(1); break;
       case 2: CTR_DEF_ROWS(2); break;
@@ -520,11 +544,11 @@ extern "C" int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, fl
   if (apply)
     hipLaunchKernelGGL(deferred_scalar<true>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
                        v_lin, n, K, last, plan->unique_rows, plan->num_unique, grad_rows, grad_lin,
-                       (int)step, step_table, h);
+                       (int)step, step_ptr, step_table, h);
   else
     hipLaunchKernelGGL(deferred_scalar<false>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
                        v_lin, n, K, last, plan->unique_rows, plan->num_unique, nullptr, nullptr,
-                       (int)step, step_table, h);
+                       (int)step, step_ptr, step_table, h);
   CTR_LAUNCH_CHECK("deferred_scalar");
   return CTR_OK;
 }
@@ -577,8 +601,8 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
   }
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
   hipLaunchKernelGGL(deferred_scalar<false>, grid, 256, 0, st, emb, m_emb, v_emb, lin, m_lin,
-                     v_lin, V, K, last, nullptr, nullptr, nullptr, nullptr, (int)step, step_table,
-                     h);
+                     v_lin, V, K, last, nullptr, nullptr, nullptr, nullptr, (int)step, nullptr,
+                     step_table, h);
   CTR_LAUNCH_CHECK("deferred_flush_scalar");
   return CTR_OK;
 }

@@ -39,6 +39,7 @@ struct GemmArgs {
   uint32_t drop_thr;  // keep iff hash >= drop_thr
   float drop_scale;   // 1/(1-p)
   uint64_t seed, offset;
+  const int32_t* step_ptr;  // dropout stream of step *step_ptr: offset += step << 32
   int64_t k_per_split;
   int64_t slab_stride;  // elements between split-K slabs (0: no split)
   bool vec_a, vec_b;
@@ -487,6 +488,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
   // per-element epilogue over all TM*TN*16 values put the accumulators in scratch).
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
   const int epi = a.slab_stride ? (int)CTR_EPI_NONE : a.epi;
+  if (epi == CTR_EPI_BIAS_RELU_DROP && a.step_ptr) a.offset += (uint64_t)(*a.step_ptr) << 32;
   float* et = smem + wmn * (32 * 36);
   const int er = lane >> 3, ec = 4 * (lane & 7);
 #pragma unroll
@@ -526,6 +528,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
 // Split-K slabs [splits][M][N] -> C with the epilogue, summed in slab order.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, const float* __restrict__ slabs,
                                                             int splits) {
+  if (a.epi == CTR_EPI_BIAS_RELU_DROP && a.step_ptr) a.offset += (uint64_t)(*a.step_ptr) << 32;
   const int64_t total = a.M * a.N;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -651,7 +654,8 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
                             const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
                             int64_t ldc, int epi, const float* bias, const float* aux,
                             int64_t ldaux, float scale, float drop_p, uint64_t seed,
-                            uint64_t offset, void* ws, int64_t ws_bytes, ctr_stream_t stream) {
+                            uint64_t offset, const int32_t* step_ptr, void* ws, int64_t ws_bytes,
+                            ctr_stream_t stream) {
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "ctr_gemm_f32: negative size");
   CTR_REQUIRE(epi >= CTR_EPI_NONE && epi <= CTR_EPI_GRAD_MASK, "ctr_gemm_f32: bad epilogue %d",
               epi);
@@ -675,7 +679,7 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
   const double thr = (double)drop_p * 4294967296.0;
   a.drop_thr = (uint32_t)std::min(thr, 4294967295.0);
   a.drop_scale = (float)(1.0 / (1.0 - (double)drop_p));
-  a.seed = seed; a.offset = offset;
+  a.seed = seed; a.offset = offset; a.step_ptr = step_ptr;
   // float4 path: 16-B aligned rows whose contiguous extent is a multiple of 4 (then a
   // float4 is entirely inside or entirely outside the matrix; split-K bounds are
   // multiples of 32)

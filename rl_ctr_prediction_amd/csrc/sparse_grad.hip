@@ -13,17 +13,22 @@
 
 namespace ctr {
 
-constexpr int kChunk = 16;  // sorted positions per lane group (SEG_L)
+// Sorted positions per lane group: 16 when a row is >= 16 lane columns (K >= 64), else 4
+// (small K: more, shorter chunks keep enough waves in flight to hide the gather latency).
+constexpr int kMinChunk = 4;
+template <int LPR>
+constexpr int seg_chunk() { return LPR >= 16 ? 16 : 4; }
 
 // ------------------------------------------------------- segmented row sums ----------
 // Vector width VT (float4 when K % 4 == 0, else float), KV = K / width columns, LPR lanes
-// per row (power of two >= KV), one lane group per chunk of kChunk sorted positions.
+// per row (power of two >= KV), one lane group per chunk of CHUNK sorted positions.
 template <typename VT>
 struct VOps;
 template <>
 struct VOps<float> {
   __device__ static float zero() { return 0.f; }
   __device__ static void add(float& a, float b) { a += b; }
+  __device__ static float shfl_xor(float v, int o) { return __shfl_xor(v, o, kWave); }
   // (g*s - g*e) + d, each product rounded (the reference's two autograd terms)
   __device__ static float fm(float g, float s, float e, float d) {
 #pragma clang fp contract(off)
@@ -33,6 +38,10 @@ struct VOps<float> {
 template <>
 struct VOps<float4> {
   __device__ static float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ static float4 shfl_xor(float4 v, int o) {
+    return make_float4(__shfl_xor(v.x, o, kWave), __shfl_xor(v.y, o, kWave),
+                       __shfl_xor(v.z, o, kWave), __shfl_xor(v.w, o, kWave));
+  }
   __device__ static void add(float4& a, float4 b) {
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
@@ -72,6 +81,7 @@ enum { MODE_FM = 0, MODE_VALS = 1 };
 
 template <typename VT, int LPR, int MODE>
 __global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
+  constexpr int kChunk = seg_chunk<LPR>();
   const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR;
   const int c = threadIdx.x % LPR;
   const int64_t start = gid * kChunk;
@@ -148,37 +158,52 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
   flush(cur, acc, accl, first_run);
 }
 
-// Rows that span chunks: head partial of the first chunk (slot [0] if the row starts the
-// chunk, else [1]), whole middle chunks ([0]), the last chunk's head partial ([0]).
+// Rows that span chunks, one wave per row: the row's P chunk partials (the first chunk's
+// open run — slot [0] if the row starts the chunk, else [1] — then slot [0] of every later
+// chunk) are dealt round-robin to the wave's 64/LPR lane groups, each sums its share in
+// chunk order, and the group sums meet in a fixed xor butterfly: a fixed summation tree for
+// a given P, so bitwise reproducible, and a hot Zipf row of thousands of slots is no longer
+// one lane group's serial walk.
 template <typename VT, int LPR>
 __global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
-  const int c = threadIdx.x % LPR;
+  constexpr int kChunk = seg_chunk<LPR>();
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, c = lane % LPR;
   const bool col = c < a.KV;
-  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / LPR);
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
   const int U = *a.num_unique;
-  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR; u < U; u += groups) {
+  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; u < U; u += waves) {
     const int32_t off0 = a.seg_offsets[u];
     const int32_t off1 = a.seg_offsets[u + 1];
     const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
-    if (fs == ls) continue;
-    const int64_t k0 = fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1);
-    VT acc = col ? static_cast<const VT*>(a.part)[k0 * a.KV + c] : VOps<VT>::zero();
-    float accl = a.part_lin[k0];
-    for (int64_t j = fs + 1; j <= ls; ++j) {
-      if (col) VOps<VT>::add(acc, static_cast<const VT*>(a.part)[(j * 2) * a.KV + c]);
-      accl += a.part_lin[j * 2];
+    if (fs == ls) continue;  // wave-uniform
+    const int64_t P = ls - fs + 1;
+    VT acc = VOps<VT>::zero();
+    float accl = 0.f;
+    for (int64_t i = g; i < P; i += G) {
+      const int64_t k = i == 0 ? fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1) : (fs + i) * 2;
+      if (col) VOps<VT>::add(acc, static_cast<const VT*>(a.part)[k * a.KV + c]);
+      accl += a.part_lin[k];
     }
-    if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
-    if (c == 0) {
-      if (a.out_lin) a.out_lin[u] = accl;
-      if (a.rowmap) a.rowmap[a.unique_rows[u]] = (int32_t)u;
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1) {
+      VOps<VT>::add(acc, VOps<VT>::shfl_xor(acc, o));
+      accl += __shfl_xor(accl, o, kWave);
+    }
+    if (g == 0) {
+      if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
+      if (c == 0) {
+        if (a.out_lin) a.out_lin[u] = accl;
+        if (a.rowmap) a.rowmap[a.unique_rows[u]] = (int32_t)u;
+      }
     }
   }
 }
 
 template <typename VT, int LPR>
 static int launch_seg_lpr(SegArgs& a, int mode, hipStream_t st) {
-  const int64_t n_chunks = ceil_div(a.S, kChunk);
+  const int64_t n_chunks = ceil_div(a.S, seg_chunk<LPR>());
   const int groups_per_block = 256 / LPR;
   const unsigned g1 = (unsigned)ceil_div(n_chunks, groups_per_block);
   if (mode == MODE_FM)
@@ -186,8 +211,8 @@ static int launch_seg_lpr(SegArgs& a, int mode, hipStream_t st) {
   else
     hipLaunchKernelGGL((seg_chunk_kernel<VT, LPR, MODE_VALS>), g1, 256, 0, st, a);
   CTR_LAUNCH_CHECK("seg_chunk_kernel");
-  const unsigned g2 = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>(ceil_div(n_chunks, groups_per_block), 1024));
+  // one wave per unique row (rows are at most S): up to 2048 blocks of 4 waves
+  const unsigned g2 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(a.S, 4), 2048));
   hipLaunchKernelGGL((seg_combine_kernel<VT, LPR>), g2, 256, 0, st, a);
   CTR_LAUNCH_CHECK("seg_combine_kernel");
   return CTR_OK;
@@ -230,7 +255,7 @@ static int launch_seg(SegArgs& a, int K, int mode, hipStream_t st, bool aligned1
 }
 
 static int64_t seg_ws_bytes(int64_t S, int K) {
-  const int64_t n_chunks = ceil_div(S, kChunk);
+  const int64_t n_chunks = ceil_div(S, kMinChunk);
   return align_up(n_chunks * 2 * (int64_t)K * 4, 256) + align_up(n_chunks * 2 * 4, 256);
 }
 
@@ -286,7 +311,7 @@ static int seg_prepare(SegArgs& a, const ctr_sparse_plan* plan, int K, void* out
               (long long)need);
     return CTR_ERR_WORKSPACE;
   }
-  const int64_t n_chunks = ceil_div(plan->S, kChunk);
+  const int64_t n_chunks = ceil_div(plan->S, kMinChunk);
   a.part = ws;
   a.part_lin = reinterpret_cast<float*>(static_cast<char*>(ws) +
                                         align_up(n_chunks * 2 * (int64_t)K * 4, 256));

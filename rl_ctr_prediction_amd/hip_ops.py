@@ -166,8 +166,10 @@ def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.
 # --------------------------------------------------------------------------- GEMM ----
 def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False, *,
          epi: int = EPI_NONE, bias=None, aux=None, scale: float = 1.0, drop_p: float = 0.0,
-         seed: int = 0, offset: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
-    """C = op(a) @ op(b) on fp32 MFMA with a fused epilogue (see include/ctr_hip.h)."""
+         seed: int = 0, offset: int = 0, step_dev: torch.Tensor | None = None,
+         out: torch.Tensor | None = None) -> torch.Tensor:
+    """C = op(a) @ op(b) on fp32 MFMA with a fused epilogue (see include/ctr_hip.h).
+    step_dev (device int32): the dropout stream of that step (offset += step << 32)."""
     _f32(a, "A")
     _f32(b, "B")
     M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
@@ -187,19 +189,19 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
     lib.ctr_gemm_f32(int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b), b.stride(0),
                      _p(out), out.stride(0), int(epi), _p(bias), _p(aux),
                      aux.stride(0) if aux is not None else 0, float(scale), float(drop_p),
-                     int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(ws),
+                     int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(step_dev), _p(ws),
                      0 if ws is None else ws.numel(), _stream())
     return out
 
 
-def linear(x, weight, bias, *, relu=False, drop_p=0.0, seed=0, offset=0, out=None):
+def linear(x, weight, bias, *, relu=False, drop_p=0.0, seed=0, offset=0, step_dev=None, out=None):
     """nn.Linear (+ReLU +Dropout) forward: x @ weight.T + bias, fused epilogue."""
     if relu:
         epi = EPI_BIAS_RELU_DROP if drop_p > 0 else EPI_BIAS_RELU
     else:
         epi = EPI_BIAS
     return gemm(x, weight, False, True, epi=epi, bias=bias, drop_p=drop_p, seed=seed,
-                offset=offset, out=out)
+                offset=offset, step_dev=step_dev, out=out)
 
 
 def tensor_sum(x: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
@@ -350,21 +352,27 @@ def adam_scalars(step: int, lr: float, betas=(0.9, 0.999)) -> tuple[float, float
 
 
 def adam_dense(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8,
-               weight_decay=0.0) -> None:
+               weight_decay=0.0, step_dev=None, table=None) -> None:
+    """One Adam step; with step_dev/table the step index is read on the device (graphs)."""
     for t, n in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
         _f32(t, n)
-    ss, bc2s = adam_scalars(step, lr, betas)
-    lib.ctr_adam_dense(_p(p), _p(g), _p(m), _p(v), p.numel(), ss, bc2s, float(betas[0]),
-                       float(betas[1]), float(eps), float(weight_decay), _stream())
+    ss, bc2s = adam_scalars(max(step, 1), lr, betas)
+    tab = table.ensure(step) if table is not None else None
+    lib.ctr_adam_dense(_p(p), _p(g), _p(m), _p(v), p.numel(), ss, bc2s, _p(tab), _p(step_dev),
+                       float(betas[0]), float(betas[1]), float(eps), float(weight_decay),
+                       _stream())
 
 
 def adam_embedding(emb, m_emb, v_emb, lin, m_lin, v_lin, rowmap, grad_rows, grad_lin, step: int,
-                   lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> None:
+                   lr: float, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, step_dev=None,
+                   table=None) -> None:
     V, K = emb.shape
-    ss, bc2s = adam_scalars(step, lr, betas)
+    ss, bc2s = adam_scalars(max(step, 1), lr, betas)
+    tab = table.ensure(step) if table is not None else None
     lib.ctr_adam_embedding(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
-                           _p(rowmap), _p(grad_rows), _p(grad_lin), ss, bc2s, float(betas[0]),
-                           float(betas[1]), float(eps), float(weight_decay), _stream())
+                           _p(rowmap), _p(grad_rows), _p(grad_lin), ss, bc2s, _p(tab),
+                           _p(step_dev), float(betas[0]), float(betas[1]), float(eps),
+                           float(weight_decay), _stream())
 
 
 class AdamStepTable:
@@ -372,9 +380,10 @@ class AdamStepTable:
     tab[2t] = -lr/(1-beta1^t), tab[2t+1] = 1/sqrt(1-beta2^t), computed in python doubles
     exactly like adam_scalars() (so dense and deferred paths see identical fp32 values)."""
 
-    def __init__(self, lr: float, betas, device, capacity: int = 1024):
+    def __init__(self, lr: float, betas, device, capacity: int = 4096):
         self.lr, self.betas, self.device = float(lr), tuple(betas), device
         self.capacity = 0
+        self.version = 0  # bumped when the table moves (captured HIP graphs hold its address)
         self.tab = torch.zeros(2, dtype=torch.float32, device=device)
         self.ensure(capacity)
 
@@ -388,19 +397,22 @@ class AdamStepTable:
                 host[2 * t + 1] = 1.0 / bc2s
             self.tab = host.to(torch.float32).to(self.device)
             self.capacity = cap
+            self.version += 1
         return self.tab
 
 
 def adam_deferred_rows(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "SparsePlanBuffers",
                        step: int, table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8,
-                       weight_decay=0.0, grad_rows=None, grad_lin=None) -> None:
-    """grad_rows None: bring the plan's rows to `step`; else to step-1 and apply `step`."""
+                       weight_decay=0.0, grad_rows=None, grad_lin=None, step_dev=None) -> None:
+    """grad_rows None: bring the plan's rows to `step`; else to step-1 and apply `step`.
+    step_dev (device int32): read the step there instead (graphs); `step` then only sizes
+    the table."""
     V, K = emb.shape
-    tab = table.ensure(step)
+    tab = table.ensure(max(step, 1))
     lib.ctr_adam_deferred_rows(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V, K,
-                               _p(last), plan.struct(), _p(grad_rows), _p(grad_lin), int(step),
-                               _p(tab), float(betas[0]), float(betas[1]), float(eps),
-                               float(weight_decay), _stream())
+                               _p(last), plan.struct(), _p(grad_rows), _p(grad_lin),
+                               max(int(step), 1), _p(step_dev), _p(tab), float(betas[0]),
+                               float(betas[1]), float(eps), float(weight_decay), _stream())
 
 
 def adam_deferred_catchup_ids(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx: torch.Tensor,

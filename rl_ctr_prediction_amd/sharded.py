@@ -141,11 +141,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
                                    self.v_w, self.last, b.gplan, self.step_count,
                                    self.step_table, self.betas, self.eps, self.weight_decay,
-                                   grad_rows=b.g_rows, grad_lin=b.g_lin)
+                                   grad_rows=b.g_rows, grad_lin=b.g_lin, step_dev=self.step_dev)
         self._span("adam", t)
         self._dirty = True
         hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
-                           self.lr, self.betas, self.eps, self.weight_decay)
+                           self.lr, self.betas, self.eps, self.weight_decay,
+                           step_dev=self.step_dev, table=self.step_table)
         return b.loss
 
     def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor]:

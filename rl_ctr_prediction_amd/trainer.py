@@ -140,7 +140,12 @@ class FusedCTRTrainer:
         self.step_count = 0
         self._bufs: _Bufs | None = None
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
-        self._drop_counter = 0
+        # HIP-graph replay of the single-process step (see step())
+        self.use_graphs = True
+        self.max_graphs = 8
+        self._graphs: dict = {}
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        self._graph_tab_version = self.step_table.version
         # bench hook: {"adam": [], "gather": [], ...} -> [(start, end, work)] HIP events
         # recorded on the launch stream around those kernels; only the keys present in the
         # dict are instrumented (each event is a queue packet: keep the timed region lean)
@@ -253,10 +258,61 @@ class FusedCTRTrainer:
     # ------------------------------------------------------------------------ step ----
     def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
-        batch's mean BCE as a 1-element device tensor (no host sync)."""
+        batch's mean BCE as a 1-element device tensor (no host sync).
+
+        Single process: the step's ~40 launches are captured once per (x, y) buffer pair
+        into a HIP graph and replayed (every per-step scalar — the Adam step, the dropout
+        stream — is read from the device step counter), so the host no longer paces small
+        batches; the first call with new buffers runs eagerly and captures."""
         B, F = x.shape
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
+        if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
+                and y.dtype == torch.float32 and y.is_contiguous()):
+            return self._graph_step(x, y, mean_div)
+        self.step_table.ensure(self.step_count + 1)
+        loss = self._launch(x, y, mean_div)
+        self._after_step()
+        return loss
+
+    def _after_step(self) -> None:
+        """Host mirrors of what a step did on the device."""
+        self.step_count += 1
+        if self.deferred:
+            self._dirty = True
+
+    def _graph_key(self, x, y, mean_div):
+        mlp = getattr(self.model, "mlp", None)
+        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
+        return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
+                tuple(y.shape), mean_div, self.model.training, drops)
+
+    def _graph_step(self, x, y, mean_div):
+        if self.step_table.capacity < self.step_count + 2:
+            self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
+        if self._graph_tab_version != self.step_table.version:
+            self._graphs.clear()  # they hold the old table's address
+            self._graph_tab_version = self.step_table.version
+        key = self._graph_key(x, y, mean_div)
+        g = self._graphs.get(key)
+        if g is None:
+            loss = self._launch(x, y, mean_div)  # the real step; also sizes every buffer
+            self._after_step()
+            if len(self._graphs) < self.max_graphs:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    self._launch(x, y, mean_div)  # captured, not executed
+                self._graphs[key] = g
+            return loss
+        g.replay()
+        self._after_step()
+        return self._bufs.loss
+
+    def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float) -> torch.Tensor:
+        """Enqueue one step. Changes no host state: step-dependent values come from
+        self.step_dev (advanced on the device), so the launch sequence can be captured."""
+        B, F = x.shape
+        rank, ws = world()
         b = self._buffers(B, F)
         y = y.reshape(-1)
         if y.dtype != torch.float32:
@@ -265,32 +321,33 @@ class FusedCTRTrainer:
         m = self.model
         E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
         gv = self.grad_views
+        step_hint = self.step_count + 1
         if self._side is not None:
             # the sparse plan is only needed from the scatter on: build it on a side stream
             # while the catch-up (plan-free, from the ids) and the forward run here
             main = torch.cuda.current_stream()
             self._side.wait_stream(main)  # x ready; previous step's plan users done
-            x.record_stream(self._side)
+            if not torch.cuda.is_current_stream_capturing():
+                x.record_stream(self._side)
             with torch.cuda.stream(self._side):
                 t_plan = self._mark("plan")
                 b.plan.build(x, self.V)
                 self._span("plan", t_plan)
-            if self.step_count > 0:
-                t = self._mark("adam")
-                hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                                                  self.last, x, self.rowmap, self.step_dev,
-                                                  self.step_table, self.step_count, self.betas,
-                                                  self.eps, self.weight_decay)
-                self._span("adam", t)
+            t = self._mark("adam")
+            hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                                              self.last, x, self.rowmap, self.step_dev,
+                                              self.step_table, step_hint, self.betas,
+                                              self.eps, self.weight_decay)
+            self._span("adam", t)
         else:
             t_plan = self._mark("plan")
             b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
             self._span("plan", t_plan)
-            if self.deferred and self.step_count > 0:
+            if self.deferred:
                 t = self._mark("adam")
                 hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
-                                           b.plan, self.step_count, self.step_table, self.betas,
-                                           self.eps, self.weight_decay)
+                                           b.plan, step_hint, self.step_table, self.betas,
+                                           self.eps, self.weight_decay, step_dev=self.step_dev)
                 self._span("adam", t)
         if self.kind == "FM":
             t = self._mark("gather")
@@ -314,23 +371,23 @@ class FusedCTRTrainer:
             self._join_wgrad()  # the exchange all-reduces the dense gradient
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
-        self.step_count += 1
-        hip_ops.step_advance(self.step_dev)
+        hip_ops.step_advance(self.step_dev)  # the device now holds this step's index
         t = self._mark("adam")
         if self.deferred:
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
-                                       plan, self.step_count, self.step_table, self.betas,
+                                       plan, step_hint, self.step_table, self.betas,
                                        self.eps, self.weight_decay, grad_rows=grad_rows,
-                                       grad_lin=grad_lin)
-            self._dirty = True
+                                       grad_lin=grad_lin, step_dev=self.step_dev)
         else:
             hip_ops.adam_embedding(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.rowmap,
-                                   grad_rows, grad_lin, self.step_count, self.lr, self.betas,
-                                   self.eps, self.weight_decay)
+                                   grad_rows, grad_lin, step_hint, self.lr, self.betas,
+                                   self.eps, self.weight_decay, step_dev=self.step_dev,
+                                   table=self.step_table)
         self._span("adam", t)
         self._join_wgrad()
-        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
-                           self.lr, self.betas, self.eps, self.weight_decay)
+        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, step_hint,
+                           self.lr, self.betas, self.eps, self.weight_decay,
+                           step_dev=self.step_dev, table=self.step_table)
         return b.loss
 
     def _deepfm_forward_backward(self, x, y, b: _Bufs, E, w, bias, mean_div):
@@ -340,17 +397,17 @@ class FusedCTRTrainer:
         p1 = float(mlp[5].p) if training else 0.0
         B = x.shape[0]
         H1, H2 = b.h1.shape[1], b.h2.shape[1]
-        off = self._drop_counter
-        self._drop_counter += B * (H1 + H2)
+        # dropout stream of this step: (completed steps) << 32 is added on the device
+        off = 0
         t = self._mark("gather")
         fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
                                 err_flag=self.err, out=b.fm)
         self._span("gather", t)
         X = fm.emb_out
         self._linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
-                     seed=self.seed, offset=off, out=b.h1)
+                     seed=self.seed, offset=off, step_dev=self.step_dev, out=b.h1)
         self._linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
-                     seed=self.seed, offset=off + B * H1, out=b.h2)
+                     seed=self.seed, offset=off + B * H1, step_dev=self.step_dev, out=b.h2)
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]

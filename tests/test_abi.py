@@ -49,7 +49,7 @@ def test_python_binding_matches_header(built_lib):
     from rl_ctr_prediction_amd._lib import exported_symbols, lib
     assert set(exported_symbols()) == _header_functions()
     dll = lib.load()  # loads on a GPU-less host; resolves every symbol with argtypes
-    assert dll.ctr_abi_version() == 1
+    assert dll.ctr_abi_version() == 2
     assert dll.ctr_device_count() >= 0
 
 
@@ -61,7 +61,7 @@ def test_host_validation_errors_without_gpu(built_lib):
                            None, None, None, None, None)
     with pytest.raises(CtrHipError, match="epilogue"):
         lib.ctr_gemm_f32(0, 0, 4, 4, 4, 16, 4, 16, 4, 16, 4, 9, None, None, 0, 1.0, 0.0, 0, 0, None,
-                         0, None)
+                         None, 0, None)
     assert lib.load().ctr_gemm_f32_workspace_bytes(1, 0, 300, 1664, 8192) > 0  # split-K path
 
 
