@@ -139,6 +139,7 @@ class FusedCTRTrainer:
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.step_count = 0
         self._bufs: _Bufs | None = None
+        self._bufsets: dict = {}
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
         # HIP-graph replay of the single-process step (see step())
         self.use_graphs = True
@@ -232,8 +233,11 @@ class FusedCTRTrainer:
 
     # --------------------------------------------------------------------- buffers ---
     def _buffers(self, B: int, F: int) -> _Bufs:
-        b = self._bufs
-        if b is not None and b.B == B and b.plan.capacity == B * F:
+        # one buffer set per batch shape, never freed: captured HIP graphs hold their
+        # addresses (a ragged last batch must not invalidate the full-batch graphs)
+        b = self._bufsets.get((B, F))
+        if b is not None:
+            self._bufs = b
             return b
         dev, K = self.device, self.K
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
@@ -252,6 +256,7 @@ class FusedCTRTrainer:
         if ws > 1:
             b.gplan = hip_ops.SparsePlanBuffers(S * ws, dev)
             b.g_rows, b.g_lin = e(S * ws, K), e(S * ws)
+        self._bufsets[(B, F)] = b
         self._bufs = b
         return b
 
@@ -294,16 +299,17 @@ class FusedCTRTrainer:
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
         key = self._graph_key(x, y, mean_div)
-        g = self._graphs.get(key)
-        if g is None:
+        hit = self._graphs.get(key)
+        if hit is None:
             loss = self._launch(x, y, mean_div)  # the real step; also sizes every buffer
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self._graph_pool):
                     self._launch(x, y, mean_div)  # captured, not executed
-                self._graphs[key] = g
+                self._graphs[key] = (g, self._bufs)
             return loss
+        g, self._bufs = hit  # the buffer set the graph was captured with
         g.replay()
         self._after_step()
         return self._bufs.loss
