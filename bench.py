@@ -133,6 +133,8 @@ def main():
     ap.add_argument("--sharding", default="auto", choices=["auto", "rows", "replicated"],
                     help="N>1: row-sharded tables with all-to-all (auto) or replicated tables "
                          "with a sparse all-gather")
+    ap.add_argument("--sweep-slices", type=int, default=0,
+                    help="deferred mode: background sweep of 1/N of the rows per step (0 = off)")
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
@@ -179,6 +181,7 @@ def main():
     else:
         trainer = FusedCTRTrainer(model, lr=1e-3, weight_decay=1e-5, seed=1234,
                                   optimizer_mode=args.optimizer)
+    trainer.sweep_slices = args.sweep_slices
     log(f"rank {rank}/{world}: {cfg['kind']} V={V} K={K} B={B} ready in {time.perf_counter() - t0:.1f}s")
 
     for i in range(args.warmup):
@@ -192,7 +195,7 @@ def main():
 
     # breakdown pass (NOT timed): every kernel group bracketed by HIP events, to find the
     # dominant kernel and report the per-kernel table
-    keys = ("adam", "gather", "plan", "scatter", "flush", "gemm", "exchange")
+    keys = ("adam", "gather", "plan", "scatter", "flush", "gemm", "exchange", "sweep")
     n_bd = max(1, min(args.steps, args.breakdown_steps))
     trainer.flush()
     trainer.timing = {k: [] for k in keys}
@@ -256,6 +259,7 @@ def main():
         "sparse plan (radix sort + scan)": {"ms_per_step": per_step["plan"]},
         "scatter (fm_embedding_grad segmented sums)": {"ms_per_step": per_step["scatter"]},
         "exchange (RCCL collectives + row gathers, N>1)": {"ms_per_step": per_step["exchange"]},
+        "sweep (deferred_sweep_vec, background stream)": {"ms_per_step": per_step["sweep"]},
     }
     spans = timing[dominant]
     launch_ms = avg_ms(spans)

@@ -243,15 +243,28 @@ int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, float* lin, 
  * S feature ids, no sparse plan needed (the plan can then be built concurrently on another
  * stream): duplicates are resolved through `owner`, a caller-owned int32[V] scratch (no
  * initialisation needed); the target step is read from device memory (*step_ptr), so the
- * call can be captured in a HIP graph. Needs K % 4 == 0 and (K/4) | 64.
- * ctr_step_advance: *step_ptr += 1 on the stream (the device-side step counter). */
+ * call can be captured in a HIP graph. Needs K % 4 == 0 and (K/4) | 64. */
 int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float* lin,
                                   float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
                                   const void* idx, int idx_type, int64_t S, int32_t* owner,
                                   const int32_t* step_ptr, const float* step_table, double beta1,
                                   double beta2, double eps, double weight_decay,
                                   ctr_stream_t stream);
-int ctr_step_advance(int32_t* step_ptr, ctr_stream_t stream);
+/* Device step counters (int32[2]): ctr[0] = completed steps, ctr[1] = the step in flight.
+ * ctr_step_begin: ctr[1] = ctr[0] + 1;  ctr_step_end: ctr[0] = ctr[1]. Between the two,
+ * both values are constant, so kernels on several streams can read them: the catch-up,
+ * the sweep and the dropout stream read ctr[0], the Adam apply reads ctr[1].
+ * ctr_adam_deferred_sweep: bring rows [s*ceil(V/n), (s+1)*ceil(V/n)), s = ctr[0] % n_slices,
+ *   up to step ctr[0] — a background share of the flush, run concurrently with a step
+ *   after its catch-up (it skips the batch's rows, which are current to ctr[0]) and
+ *   finished before ctr_step_end. table_steps = entries of step_table (its capacity). */
+int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream);
+int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream);
+int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                            float* v_lin, int64_t V, int K, int32_t* last,
+                            const int32_t* step_ctr, int n_slices, const float* step_table,
+                            int64_t table_steps, double beta1, double beta2, double eps,
+                            double weight_decay, ctr_stream_t stream);
 
 /* ------------------------------------------------ A7: Feature_Embedding -------------
  * out[b] = [ <E[x_bi],E[x_bj]> for i<j in row-major pair order ] ++ flat(E[x_b]),

@@ -286,7 +286,67 @@ __global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
   }
 }
 
-__global__ void step_advance_kernel(int32_t* step_ptr) { *step_ptr += 1; }
+// Device step counters of a trainer: ctr[0] = completed steps, ctr[1] = the step in flight.
+// Within a step, ctr[0] stays at t-1 (catch-up, sweep and dropout read it) and ctr[1] = t
+// (the Adam apply reads it), so work on several streams never sees the counter move.
+__global__ void step_begin_kernel(int32_t* ctr) { ctr[1] = ctr[0] + 1; }
+__global__ void step_end_kernel(int32_t* ctr) { ctr[0] = ctr[1]; }
+
+// Background sweep (deferred Adam): bring one slice of the rows — slice ctr[0] % n_slices —
+// up to the completed step ctr[0], while a training step runs on other streams. Rows of the
+// step's own batch are current to ctr[0] after its catch-up (from >= target: skipped), so
+// the sweep never touches a row the step reads or updates. Lane 0 of a row's lane group
+// also owns the row's linear weight. The per-step scalars are staged in LDS (lds_steps
+// entries; larger targets read them from global memory).
+template <int K4>
+__global__ __launch_bounds__(256) void deferred_sweep_vec(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    int32_t* __restrict__ last, const int32_t* __restrict__ ctr, int n_slices, int lds_steps,
+    const float* __restrict__ tab, AdamHP h) {
+  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
+  const int target = ctr[0];
+  const bool use_lds = target < lds_steps;
+  if (use_lds) {
+    for (int i = threadIdx.x; i <= target; i += blockDim.x)
+      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
+    __syncthreads();
+  }
+  if (target <= 0) return;
+  const int64_t per = (V + n_slices - 1) / n_slices;
+  const int64_t lo = (int64_t)(target % n_slices) * per;
+  const int64_t hi = min(V, lo + per);
+  const int c = threadIdx.x % K4;
+  const bool own_lin = w && c == 0;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t r = lo + (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; r < hi; r += groups) {
+    const int from = last[r];
+    if (from >= target) continue;
+    const int64_t e = r * K4 + c;
+    float4 pp = E[e], mm = mE[e], vv = vE[e];
+    float pw = 0.f, mws = 0.f, vws = 0.f;
+    if (own_lin) {
+      pw = w[r]; mws = mw[r]; vws = vw[r];
+    }
+    for (int s = from + 1; s <= target; ++s) {
+      if (use_lds) {
+        const float2 t = s_tab[s];
+        h.neg_step_size = t.x;
+        h.inv_bc2_sqrt = t.y;
+      } else {
+        load_step(h, tab, s);
+      }
+      adam_vec(pp, z4, mm, vv, h);
+      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
+    }
+    E[e] = pp; mE[e] = mm; vE[e] = vv;
+    if (own_lin) {
+      w[r] = pw; mw[r] = mws; vw[r] = vws;
+    }
+    if (c == 0) last[r] = target;
+  }
+}
 
 // Every row to `step` (epoch end / checkpoint / eval). Rows already current cost 4 B.
 // The per-step scalars of steps 1..step are staged once per block in LDS (one ds_read_b64
@@ -662,9 +722,56 @@ extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_
   return CTR_OK;
 }
 
-extern "C" int ctr_step_advance(int32_t* step_ptr, ctr_stream_t stream) {
-  CTR_REQUIRE(step_ptr, "ctr_step_advance: null pointer");
-  hipLaunchKernelGGL(step_advance_kernel, 1, 1, 0, as_stream(stream), step_ptr);
-  CTR_LAUNCH_CHECK("step_advance_kernel");
+extern "C" int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream) {
+  CTR_REQUIRE(step_ctr, "ctr_step_begin: null pointer");
+  hipLaunchKernelGGL(step_begin_kernel, 1, 1, 0, as_stream(stream), step_ctr);
+  CTR_LAUNCH_CHECK("step_begin_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream) {
+  CTR_REQUIRE(step_ctr, "ctr_step_end: null pointer");
+  hipLaunchKernelGGL(step_end_kernel, 1, 1, 0, as_stream(stream), step_ctr);
+  CTR_LAUNCH_CHECK("step_end_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin,
+                                       float* m_lin, float* v_lin, int64_t V, int K,
+                                       int32_t* last, const int32_t* step_ctr, int n_slices,
+                                       const float* step_table, int64_t table_steps,
+                                       double beta1, double beta2, double eps,
+                                       double weight_decay, ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && step_ctr && step_table,
+              "ctr_adam_deferred_sweep: null pointer");
+  CTR_REQUIRE(V > 0 && K > 0 && n_slices > 0 && table_steps > 0,
+              "ctr_adam_deferred_sweep: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_sweep: linear table pointers must be all set or all NULL");
+  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, nullptr),
+              "ctr_adam_deferred_sweep: needs K %% 4 == 0, (K/4) | 64 and 16-B rows");
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipStream_t st = as_stream(stream);
+  const int lds_steps = (int)std::min<int64_t>(table_steps + 1, kMaxLdsSteps);
+  const size_t lds_bytes = (size_t)lds_steps * sizeof(float2);
+  const int K4 = K / 4;
+  const int64_t rows = ceil_div(V, n_slices);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows * K4, 256), 4096));
+#define CTR_SWEEP(K4_)                                                                          \
+  hipLaunchKernelGGL((deferred_sweep_vec<K4_>), grid, 256, lds_bytes, st,                       \
+                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
+                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, step_ctr,    \
+                     n_slices, lds_steps, step_table, h)
+  switch (K4) {
+    case 1: CTR_SWEEP(1); break;
+    case 2: CTR_SWEEP(2); break;
+    case 4: CTR_SWEEP(4); break;
+    case 8: CTR_SWEEP(8); break;
+    case 16: CTR_SWEEP(16); break;
+    case 32: CTR_SWEEP(32); break;
+    case 64: CTR_SWEEP(64); break;
+  }
+#undef CTR_SWEEP
+  CTR_LAUNCH_CHECK("deferred_sweep_vec");
   return CTR_OK;
 }

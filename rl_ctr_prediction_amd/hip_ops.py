@@ -18,7 +18,7 @@ __all__ = [
     "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
-    "step_advance", "ids_add_",
+    "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -431,8 +431,25 @@ def adam_deferred_catchup_ids(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx: t
                                       float(eps), float(weight_decay), _stream())
 
 
-def step_advance(step_dev: torch.Tensor) -> None:
-    lib.ctr_step_advance(_p(step_dev), _stream())
+def step_begin(step_ctr: torch.Tensor) -> None:
+    """ctr[1] = ctr[0] + 1 on the device (int32[2]: completed steps, step in flight)."""
+    lib.ctr_step_begin(_p(step_ctr), _stream())
+
+
+def step_end(step_ctr: torch.Tensor) -> None:
+    """ctr[0] = ctr[1] on the device."""
+    lib.ctr_step_end(_p(step_ctr), _stream())
+
+
+def adam_deferred_sweep(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step_ctr: torch.Tensor,
+                        n_slices: int, table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8,
+                        weight_decay=0.0) -> None:
+    """Bring slice ctr[0] % n_slices of the rows up to the completed step ctr[0]."""
+    V, K = emb.shape
+    lib.ctr_adam_deferred_sweep(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V,
+                                K, _p(last), _p(step_ctr), int(n_slices), _p(table.tab),
+                                int(table.capacity), float(betas[0]), float(betas[1]),
+                                float(eps), float(weight_decay), _stream())
 
 
 def adam_deferred_flush(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step: int,

@@ -81,6 +81,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         y = y.contiguous()
         bias, gv = self.views["bias"], self.grad_views
 
+        hip_ops.step_begin(self.step_ctr)
         # 1. plan of the local batch, per-owner counts of its unique rows
         t = self._mark("plan")
         b.plan.build(x, self.V, err_flag=self.err)
@@ -95,10 +96,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 3. owners: catch the rows up, send them back
         t = self._mark("adam")
         hip_ops.adam_deferred_catchup_ids(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
-                                          self.v_w, self.last, req, self.rowmap, self.step_dev,
+                                          self.v_w, self.last, req, self.rowmap, self.step_done,
                                           self.step_table, self.step_count + 1, self.betas,
                                           self.eps, self.weight_decay)
         self._span("adam", t)
+        self._fork_sweep()
         t = self._mark("exchange")
         rows = hip_ops.embedding_gather(self.E_tab, req)
         lin = hip_ops.embedding_gather(self.w_tab, req)
@@ -136,17 +138,18 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.segment_sum_rows(b.gplan, G, G_lin, rowmap=None, out=b.g_rows, out_lin=b.g_lin)
         self._span("scatter", t)
         self.step_count += 1
-        hip_ops.step_advance(self.step_dev)
         t = self._mark("adam")
         hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
                                    self.v_w, self.last, b.gplan, self.step_count,
                                    self.step_table, self.betas, self.eps, self.weight_decay,
-                                   grad_rows=b.g_rows, grad_lin=b.g_lin, step_dev=self.step_dev)
+                                   grad_rows=b.g_rows, grad_lin=b.g_lin, step_dev=self.step_cur)
         self._span("adam", t)
         self._dirty = True
         hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
                            self.lr, self.betas, self.eps, self.weight_decay,
-                           step_dev=self.step_dev, table=self.step_table)
+                           step_dev=self.step_cur, table=self.step_table)
+        self._join_sweep()
+        hip_ops.step_end(self.step_ctr)
         return b.loss
 
     def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor]:

@@ -127,10 +127,17 @@ class FusedCTRTrainer:
         # the plan-free catch-up (csrc/adam.hip deferred_mark_kernel)
         self.rowmap = torch.full((self.V_tab,), -1, dtype=torch.int32, device=self.device)
         self.last = torch.zeros(self.V_tab, dtype=torch.int32, device=self.device)
-        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.device)  # completed steps
+        # device step counters: [0] completed steps, [1] the step in flight (ctr_step_begin/end)
+        self.step_ctr = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self.step_done, self.step_cur = self.step_ctr[0:1], self.step_ctr[1:2]
+        # optional background sweep: each step brings 1/sweep_slices of the rows up to date on
+        # its own stream. Off by default: measured on MI355X (C3) it slows the concurrent
+        # GEMMs by more than it saves at flush() (8.6 vs 9.9 M ex/s at K=30)
+        self.sweep_slices = 0
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self._wgrad_stream = torch.cuda.Stream(device=self.device) if self.kind == "DeepFM" else None
+        self._sweep_stream = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -206,7 +213,7 @@ class FusedCTRTrainer:
         for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
             t.zero_()
         self.last.zero_()
-        self.step_dev.zero_()
+        self.step_ctr.zero_()
         self.step_count = 0
 
     def optimizer_state_dict(self) -> dict:
@@ -316,10 +323,11 @@ class FusedCTRTrainer:
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float) -> torch.Tensor:
         """Enqueue one step. Changes no host state: step-dependent values come from
-        self.step_dev (advanced on the device), so the launch sequence can be captured."""
+        self.step_ctr (advanced on the device), so the launch sequence can be captured."""
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
+        hip_ops.step_begin(self.step_ctr)
         y = y.reshape(-1)
         if y.dtype != torch.float32:
             y = y.float()
@@ -341,10 +349,11 @@ class FusedCTRTrainer:
                 self._span("plan", t_plan)
             t = self._mark("adam")
             hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                                              self.last, x, self.rowmap, self.step_dev,
+                                              self.last, x, self.rowmap, self.step_done,
                                               self.step_table, step_hint, self.betas,
                                               self.eps, self.weight_decay)
             self._span("adam", t)
+            self._fork_sweep()
         else:
             t_plan = self._mark("plan")
             b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
@@ -353,7 +362,7 @@ class FusedCTRTrainer:
                 t = self._mark("adam")
                 hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                            b.plan, step_hint, self.step_table, self.betas,
-                                           self.eps, self.weight_decay, step_dev=self.step_dev)
+                                           self.eps, self.weight_decay, step_dev=self.step_done)
                 self._span("adam", t)
         if self.kind == "FM":
             t = self._mark("gather")
@@ -377,24 +386,42 @@ class FusedCTRTrainer:
             self._join_wgrad()  # the exchange all-reduces the dense gradient
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
-        hip_ops.step_advance(self.step_dev)  # the device now holds this step's index
         t = self._mark("adam")
         if self.deferred:
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                        plan, step_hint, self.step_table, self.betas,
                                        self.eps, self.weight_decay, grad_rows=grad_rows,
-                                       grad_lin=grad_lin, step_dev=self.step_dev)
+                                       grad_lin=grad_lin, step_dev=self.step_cur)
         else:
             hip_ops.adam_embedding(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.rowmap,
                                    grad_rows, grad_lin, step_hint, self.lr, self.betas,
-                                   self.eps, self.weight_decay, step_dev=self.step_dev,
+                                   self.eps, self.weight_decay, step_dev=self.step_cur,
                                    table=self.step_table)
         self._span("adam", t)
         self._join_wgrad()
         hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, step_hint,
                            self.lr, self.betas, self.eps, self.weight_decay,
-                           step_dev=self.step_dev, table=self.step_table)
+                           step_dev=self.step_cur, table=self.step_table)
+        self._join_sweep()
+        hip_ops.step_end(self.step_ctr)
         return b.loss
+
+    def _fork_sweep(self) -> None:
+        """Start this step's background sweep (after the catch-up: the batch's rows are
+        current, so the sweep and the step touch disjoint rows)."""
+        if self._sweep_stream is None or not self.sweep_slices:
+            return
+        self._sweep_stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._sweep_stream):
+            t = self._mark("sweep")
+            hip_ops.adam_deferred_sweep(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                        self.v_w, self.last, self.step_ctr, self.sweep_slices,
+                                        self.step_table, self.betas, self.eps, self.weight_decay)
+            self._span("sweep", t)
+
+    def _join_sweep(self) -> None:
+        if self._sweep_stream is not None and self.sweep_slices:
+            torch.cuda.current_stream().wait_stream(self._sweep_stream)
 
     def _deepfm_forward_backward(self, x, y, b: _Bufs, E, w, bias, mean_div):
         mlp, gv, vw = self.model.mlp, self.grad_views, self.views
@@ -411,9 +438,9 @@ class FusedCTRTrainer:
         self._span("gather", t)
         X = fm.emb_out
         self._linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
-                     seed=self.seed, offset=off, step_dev=self.step_dev, out=b.h1)
+                     seed=self.seed, offset=off, step_dev=self.step_done, out=b.h1)
         self._linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
-                     seed=self.seed, offset=off + B * H1, step_dev=self.step_dev, out=b.h2)
+                     seed=self.seed, offset=off + B * H1, step_dev=self.step_done, out=b.h2)
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]
