@@ -1,6 +1,6 @@
 """Benchmark: CTR training examples/sec of the fused HIP step (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline]
 
 N>1 is launched by the driver as `python -m torch.distributed.run --nproc-per-node N ...`:
 one process per GPU, RCCL over xGMI, data parallel with replicated tables (weak scaling:
@@ -11,6 +11,11 @@ fields, 10M-id vocabulary, embed_dim 64, batch 8192 per GPU, synthetic Criteo-sh
 (skewed field cardinalities, Zipf(1.1) within fields) and planted-FM labels, inputs
 resident in HBM, reference semantics (dense Adam, lr 1e-3, wd 1e-5, dropout 0.2).
 c2 = configs[1]: FM, 1M vocab, dim 16, batch 4096.
+c4 = configs[3]: REINFORCE (PolicyGradient.learn) over Feature_Embedding states of the C2
+table, policy MLP 741-1024-512-256-128-5, episode 4096 transitions per GPU; N>1 splits
+one episode over the ranks with the single-process result (pg_model.py).
+c5 = configs[4]: FM, Avazu-shape 22 fields, 40M vocab, dim 128, batch 8192 per GPU; N>1
+row-shards the table across the ranks (all-to-all), the configuration it is quoted on.
 
 The JSON line carries `roofline` for the dominant kernel (the dense Adam pass over the
 table, adam_embedding_vec, timed per launch with HIP events on its stream inside the
@@ -43,6 +48,12 @@ CONFIGS = {
                         "10M vocab, embed_dim 64, batch 8192/GPU"),
     "c2": dict(kind="FM", V=1_000_000, F=26, K=16, B=4096,
                workload="C2 FM, Criteo-shape 26 fields, 1M vocab, embed_dim 16, batch 4096/GPU"),
+    "c4": dict(kind="PG", V=1_000_000, F=26, K=16, B=4096, A=5,
+               workload="C4 REINFORCE PolicyGradient.learn: Feature_Embedding state (C2 table, "
+                        "325 pairs + 416) -> policy MLP 741-1024-512-256-128-5, episode "
+                        "4096 transitions/GPU"),
+    "c5": dict(kind="FM", V=40_000_000, F=22, K=128, B=8192,
+               workload="C5 FM, Avazu-shape 22 fields, 40M vocab, embed_dim 128, batch 8192/GPU"),
 }
 
 
@@ -106,6 +117,154 @@ def cpu_baseline(cfg, batches, max_seconds=25.0):
                       f"{t / n * 1e3:.0f} ms/step; param init {init_s:.1f} s untimed"}
 
 
+def cpu_baseline_pg(cfg, episodes, max_seconds=25.0):
+    """PolicyGradient.learn restated on torch-CPU (oracle.pg_learn) on this host."""
+    from oracle import ctr_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(1)
+    V, F, K, A = cfg["V"], cfg["F"], cfg["K"], cfg["A"]
+    E = torch.randn(V, K)
+    policy = O.pg_policy(F * (F - 1) // 2 + F * K, A)
+    opt = torch.optim.Adam(policy.parameters(), lr=1e-4, weight_decay=1e-5)
+    eps = [(torch.from_numpy(x), torch.from_numpy(a), r) for x, a, r in episodes]
+    O.pg_learn(policy, opt, E, *eps[0])  # warm-up
+    n, t = 0, 0.0
+    while n < 3 or (t < max_seconds and n < 10):
+        s = time.perf_counter()
+        O.pg_learn(policy, opt, E, *eps[n % len(eps)])
+        t += time.perf_counter() - s
+        n += 1
+    return {"value": n * cfg["B"] / t, "unit": "transitions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} timed learn() calls (+1 warm-up) on the same episodes, "
+                      f"oracle/ctr_oracle.py pg_learn (torch-CPU: FE state, policy MLP, "
+                      f"loss_func, Adam); {t / n * 1e3:.0f} ms per episode"}
+
+
+def bench_pg(args, cfg, world, rank, dev):
+    """C4: one step = store_transition(episode) + learn() (PG_model.py:156-179) on this
+    rank's B transitions; N>1 = one episode of N*B transitions split over the ranks."""
+    from rl_ctr_prediction_amd import PolicyGradient, hip_ops
+    from rl_ctr_prediction_amd.synthetic import CriteoSynth
+
+    V, F, K, B, A = cfg["V"], cfg["F"], cfg["K"], cfg["B"], cfg["A"]
+    torch.manual_seed(1)  # identical replicas
+    pg = PolicyGradient(V, F, K, "c4", action_nums=A, device=str(dev), fix_input_dims=True)
+    pg.policy_net.train()
+    synth = CriteoSynth(V, F, seed=1)
+    n_eps = max(1, min(args.batches, args.warmup))
+    rng = np.random.default_rng([4, rank])
+    host = []
+    for x, y in synth.batches(n_eps, B, rank=rank):
+        a = rng.integers(1, A + 1, size=(B, 1)).astype(np.int64)
+        host.append((x, a, y.reshape(-1, 1).astype(np.float32)))
+    eps = [tuple(torch.from_numpy(t).to(dev) for t in e) for e in host]
+
+    def step(i):
+        x, a, r = eps[i % len(eps)]
+        pg.store_transition(x, a, r)
+        return pg.learn()
+
+    for i in range(args.warmup):
+        step(i)
+    # roofline pass (not timed): HIP events around every policy GEMM launch
+    spans = []
+    real_gemm = hip_ops.gemm
+
+    def timed(fn, flops_of):
+        def wrap(*a, **kw):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = fn(*a, **kw)
+            e1.record()
+            spans.append((e0, e1, flops_of(out, a, kw)))
+            return out
+        return wrap
+
+    def gemm_flops(res, a, kw):  # hip_ops.gemm(a, b, trans_a, trans_b, ...)
+        trans_a = a[2] if len(a) > 2 else kw.get("trans_a", False)
+        return 2.0 * res.shape[0] * res.shape[1] * (a[0].shape[0] if trans_a else a[0].shape[1])
+
+    # hip_ops.linear calls hip_ops.gemm through the module, so wrapping gemm sees every launch
+    hip_ops.gemm = timed(real_gemm, gemm_flops)
+    fe_ev = []
+    real_fe = hip_ops.feature_embedding
+
+    def fe_wrap(*a, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = real_fe(*a, **kw)
+        e1.record()
+        fe_ev.append((e0, e1))
+        return out
+
+    hip_ops.feature_embedding = fe_wrap
+    try:
+        n_bd = max(1, min(args.steps, args.breakdown_steps))
+        for i in range(n_bd):
+            step(i)
+        torch.cuda.synchronize()
+    finally:
+        hip_ops.gemm, hip_ops.feature_embedding = real_gemm, real_fe
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    g_ms = [a.elapsed_time(b) for a, b, _ in spans]
+    flops = sum(w for _, _, w in spans) / len(spans)
+    launch_ms = sum(g_ms) / len(g_ms)
+    achieved = flops / (launch_ms * 1e-3) / 1e12
+    fe_ms = sum(a.elapsed_time(b) for a, b in fe_ev) / len(fe_ev)
+    fe_bytes = B * F * 8 + B * F * 4 * K + B * (F * (F - 1) // 2 + F * K) * 4
+    result = {
+        "metric": METRIC, "value": world * B * args.steps / elapsed, "unit": "transitions/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: Criteo-shape ids as states, uniform actions, reward = click label "
+                "(planted-FM); random-init weights",
+        "config": {"workload": cfg["workload"], "model": "PolicyGradient (Net, fix_input_dims)",
+                   "episode_transitions": B * world, "fields": F, "vocab": V, "embed_dim": K,
+                   "actions": A, "parallelism": f"dp{world}" + (
+                       " (one episode split over the ranks: reward all-gather, gradient "
+                       "all-reduce)" if world > 1 else ""),
+                   "optimizer": "Adam lr=1e-4 wd=1e-5 (PG_model.py:87)"},
+        "roofline": {"kernel": "gemm_f32_kernel (policy MLP fwd + bwd, averaged per launch)",
+                     "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
+                     "algorithmic_flops_per_launch": flops, "traffic": None,
+                     "avg_launch_ms": launch_ms, "launches_timed": len(spans),
+                     "timing": "HIP events on the launch stream around each GEMM launch over "
+                               "un-timed learn() calls before the timed region"},
+        "kernels": {"feature_embedding_kernel": {"ms_per_call": fe_ms,
+                                                 "GBps": fe_bytes / (fe_ms * 1e-3) / 1e9},
+                    "gemm_f32_kernel": {"ms_per_step": sum(g_ms) / n_bd}},
+        "last_loss": float(loss.item()),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        result["cpu_baseline"] = cpu_baseline_pg(cfg, host)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def load_traffic(config: str, kernel: str):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
     FETCH_SIZE/WRITE_SIZE passes with the gfx950 corrections, profiles/)."""
@@ -161,6 +320,8 @@ def main():
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
 
     cfg = CONFIGS[args.config]
+    if cfg["kind"] == "PG":
+        return bench_pg(args, cfg, world, rank, dev)
     V, F, K, B = cfg["V"], cfg["F"], cfg["K"], cfg["B"]
     t0 = time.perf_counter()
     torch.manual_seed(1)  # identical replicas on every rank

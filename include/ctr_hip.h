@@ -281,7 +281,12 @@ int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int 
  *   Replaces PG_model.py:139-154.
  * ctr_pg_loss_grad: loss = sum_b(-log probs[b, act_b - 1]) * mean(vt) (PG_model.py:104-107,
  *   actions 1-based) and the gradient w.r.t. the softmax LOGITS (softmax backward fused),
- *   scaled by grad_scale. loss_out is a device scalar. */
+ *   scaled by grad_scale. loss_out is a device scalar.
+ * ctr_pg_vt_mean: out[0] = mean(vt[0..n)) summed in the order ctr_pg_loss_grad uses.
+ * ctr_pg_loss_grad_global: ctr_pg_loss_grad for one rank's slice of an episode that is
+ *   split over data-parallel ranks: c = vt_mean[0] (the episode-wide mean, device scalar)
+ *   and loss_out = sum_b(-log probs[b, act_b - 1]) * vt_mean[0], this rank's share of the
+ *   episode loss (the shares sum to it). Same reference lines as ctr_pg_loss_grad. */
 int ctr_softmax_rows(const float* x, int64_t B, int A, float* out, ctr_stream_t stream);
 int64_t ctr_pg_workspace_bytes(int64_t n);
 int ctr_pg_discount_norm(const float* r, int64_t n, double gamma, double* out, float* out_f32,
@@ -289,6 +294,10 @@ int ctr_pg_discount_norm(const float* r, int64_t n, double gamma, double* out, f
 int ctr_pg_loss_grad(const float* probs, const int64_t* acts, const float* vt, int64_t B,
                      int A, float grad_scale, float* loss_out, float* dlogits, void* ws,
                      int64_t ws_bytes, ctr_stream_t stream);
+int ctr_pg_vt_mean(const float* vt, int64_t n, float* out, ctr_stream_t stream);
+int ctr_pg_loss_grad_global(const float* probs, const int64_t* acts, int64_t B, int A,
+                            const float* vt_mean, float grad_scale, float* loss_out,
+                            float* dlogits, ctr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,7 @@ A from-scratch restatement of jqsl2012/RL_CTR_Prediction's algorithms on torch-C
   train_step          all_main/pretrain_main.py:67-83 (fwd, BCE, zero_grad, backward, Adam)
   feature_embedding   Feature_embedding.py:51-59
   pg_*                PG_model.py:104-154 (loss_func, choose_action, discount_and_norm)
+  pg_policy/pg_learn  PG_model.py:24-58,156-179 (Net, learn: FE state, MLP, loss, Adam)
   sparse_plan         the grouping inside embedding_dense_backward (numpy, bit-exact ints)
   pretrain_run        all_main/pretrain_main.py:119-202 (per-epoch Adam, no shuffle, AUC)
 
@@ -210,6 +211,30 @@ def pg_choose_action(probs: torch.Tensor, action_nums: int) -> torch.Tensor:
     random_action = torch.randint(low=1, high=action_nums + 1, size=[n, 1])
     return torch.where(random_seeds >= torch.max(probs, 1)[0].view(-1, 1),
                        max_action.view(-1, 1), random_action)
+
+
+def pg_policy(input_dims: int, action_nums: int) -> torch.nn.Sequential:
+    """Net.mlp (PG_model.py:41-56): [Linear -> ReLU -> Dropout(0.2)] x 4 with widths
+    1024, 512, 256, 128, then Linear(action_nums); softmax applied by the caller."""
+    layers, width, d = [], 1024, input_dims
+    for _ in range(4):
+        layers += [torch.nn.Linear(d, width), torch.nn.ReLU(), torch.nn.Dropout(p=0.2)]
+        d, width = width, width // 2
+    layers.append(torch.nn.Linear(d, action_nums))
+    return torch.nn.Sequential(*layers)
+
+
+def pg_learn(policy: torch.nn.Sequential, opt, E: torch.Tensor, states: torch.Tensor,
+             acts: torch.Tensor, rewards: np.ndarray, gamma: float = 1.0) -> float:
+    """PolicyGradient.learn (PG_model.py:156-179): returns, FE state (detached), softmax
+    policy, loss_func, zero_grad/backward/Adam.step (Adam(lr 1e-4, wd 1e-5), line 87)."""
+    vt = torch.from_numpy(pg_discount_and_norm(rewards, gamma)).float()
+    probs = torch.softmax(policy(feature_embedding(E, states)), dim=1)
+    loss = pg_loss(probs, acts, vt)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    return loss.item()
 
 
 # --------------------------------------------------------------------- driver -------

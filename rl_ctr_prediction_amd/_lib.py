@@ -77,6 +77,8 @@ SIGNATURES = {
     "ctr_pg_workspace_bytes": (_i64, [_i64]),
     "ctr_pg_discount_norm": (_i32, [_vp, _i64, _f64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "ctr_pg_loss_grad": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp, _vp, _i64, _vp]),
+    "ctr_pg_vt_mean": (_i32, [_vp, _i64, _vp, _vp]),
+    "ctr_pg_loss_grad_global": (_i32, [_vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp]),
 }
 
 

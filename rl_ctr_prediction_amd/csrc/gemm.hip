@@ -94,6 +94,15 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc
 // zeroed in LDS before use.
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
+#ifndef CTR_GEMM_TRACE
+#define CTR_GEMM_TRACE 0
+#endif
+#if CTR_GEMM_TRACE
+// tuning builds only: per block [realtime start, memtime start, memtime after the k-loop,
+// memtime end, xcc<<8 | se<<4 | cu]
+__device__ unsigned long long g_gemm_trace[16384 * 5];
+#endif
+
 // global_load_lds_dwordx4 in inline asm: hipcc (ROCm 7.2) treats the builtin's LDS write
 // as aliasing every later ds_read and puts an s_waitcnt vmcnt(0) before the first fragment
 // read of each k-tile, draining the ring; hidden from its waitcnt model, the ring is
@@ -163,6 +172,10 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+#if CTR_GEMM_TRACE
+  const unsigned long long tr_rt = wall_clock64(), tr_t0 = clock64();
+  const int tr_b = blockIdx.x + gridDim.x * blockIdx.z;
+#endif
   const int kw = wave / (WAVES_M * WAVES_N);
   const int wmn = wave % (WAVES_M * WAVES_N);
   const int wm0 = (wmn / WAVES_N) * WM;
@@ -451,6 +464,17 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
     }
   }
   __syncthreads();  // every stage read before the buffers are reused below
+#if CTR_GEMM_TRACE
+  const unsigned long long tr_t1 = clock64();
+  if (tid == 0 && tr_b < 16384) {
+    const unsigned hw = __builtin_amdgcn_s_getreg(GETREG_IMMED(31, 0, 4));
+    const unsigned xcc = __builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20));
+    g_gemm_trace[tr_b * 5 + 0] = tr_rt;
+    g_gemm_trace[tr_b * 5 + 1] = tr_t0;
+    g_gemm_trace[tr_b * 5 + 2] = tr_t1;
+    g_gemm_trace[tr_b * 5 + 4] = ((unsigned long long)xcc << 8) | (((hw >> 13) & 3) << 4) | ((hw >> 8) & 15);
+  }
+#endif
 
   // in-block k-split: waves kw > 0 hand their partial tiles to wave kw = 0 through LDS
   if (KSPLIT > 1) {
@@ -523,6 +547,9 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
       }
       __builtin_amdgcn_wave_barrier();
     }
+#if CTR_GEMM_TRACE
+  if (tid == 0 && tr_b < 16384) g_gemm_trace[tr_b * 5 + 3] = clock64();
+#endif
 }
 
 // Split-K slabs [splits][M][N] -> C with the epilogue, summed in slab order.
@@ -649,6 +676,13 @@ extern "C" int64_t ctr_gemm_f32_workspace_bytes(int trans_a, int trans_b, int64_
   const TileCfg c = choose_tiles(M, N, K);
   return c.splits > 1 ? (int64_t)c.splits * M * N * (int64_t)sizeof(float) : 0;
 }
+
+#if CTR_GEMM_TRACE
+extern "C" int ctr_debug_gemm_trace(unsigned long long* host, int n_blocks) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_trace),
+                                  sizeof(unsigned long long) * 5 * std::min(n_blocks, 16384));
+}
+#endif
 
 extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                             const float* A, int64_t lda, const float* B, int64_t ldb, float* C,

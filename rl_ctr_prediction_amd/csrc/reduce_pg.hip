@@ -196,37 +196,49 @@ __global__ __launch_bounds__(1024) void pg_discount_norm_kernel(const float* __r
 //   nlp = sum_b -log(p[b, a_b - 1]);  loss = mean(nlp * vt) ;
 //   c = d loss / d nlp = sum_i vt_i / n;  g[b,a] = -c / p[b,a];
 //   dlogit[b,j] = p[b,j] * (g[b,j] - g[b,a] * p[b,a])     (softmax backward)
+// vt_mean != NULL (data-parallel episode split over ranks): c = vt_mean[0] * grad_scale
+// with the episode-wide mean from pg_vt_mean_kernel, and loss = nlp * vt_mean[0] — this
+// rank's share of the global loss (the shares are summed by the caller's all-reduce).
+__device__ __forceinline__ float block_sum_1024(float v, float* s_red) {
+  const int t = threadIdx.x, T = blockDim.x;
+  v = wave_sum(v);
+  if ((t & 63) == 0) s_red[t >> 6] = v;
+  __syncthreads();
+  float tot = 0.f;
+  for (int w = 0; w < T / 64; ++w) tot += s_red[w];
+  __syncthreads();
+  return tot;
+}
+
 __global__ __launch_bounds__(1024) void pg_loss_grad_kernel(const float* __restrict__ p,
                                                             const int64_t* __restrict__ acts,
                                                             const float* __restrict__ vt,
+                                                            const float* __restrict__ vt_mean,
                                                             int64_t B, int A, float grad_scale,
                                                             float* __restrict__ loss_out,
                                                             float* __restrict__ dlogits) {
   __shared__ float s_red[16];
   const int t = threadIdx.x, T = blockDim.x;
-  auto block_sum = [&](float v) -> float {
-    v = wave_sum(v);
-    if ((t & 63) == 0) s_red[t >> 6] = v;
-    __syncthreads();
-    float tot = 0.f;
-    for (int w = 0; w < T / 64; ++w) tot += s_red[w];
-    __syncthreads();
-    return tot;
-  };
   float nl = 0.f, sv = 0.f;
   for (int64_t b = t; b < B; b += T) {
     int64_t a = acts[b] - 1;
     a = a < 0 ? 0 : (a >= A ? A - 1 : a);
     nl += -logf(p[b * A + a]);
-    sv += vt[b];
+    if (!vt_mean) sv += vt[b];
   }
-  const float nlp = block_sum(nl);
-  const float svt = block_sum(sv);
-  float lv = 0.f;
-  for (int64_t b = t; b < B; b += T) lv += nlp * vt[b];
-  const float loss = block_sum(lv) / (float)B;
-  if (t == 0 && loss_out) loss_out[0] = loss;
-  const float c = (svt / (float)B) * grad_scale;
+  const float nlp = block_sum_1024(nl, s_red);
+  float c;
+  if (vt_mean) {
+    if (t == 0 && loss_out) loss_out[0] = nlp * vt_mean[0];
+    c = vt_mean[0] * grad_scale;
+  } else {
+    const float svt = block_sum_1024(sv, s_red);
+    float lv = 0.f;
+    for (int64_t b = t; b < B; b += T) lv += nlp * vt[b];
+    const float loss = block_sum_1024(lv, s_red) / (float)B;
+    if (t == 0 && loss_out) loss_out[0] = loss;
+    c = (svt / (float)B) * grad_scale;
+  }
   if (!dlogits) return;
   for (int64_t b = t; b < B; b += T) {
     int64_t a = acts[b] - 1;
@@ -239,6 +251,17 @@ __global__ __launch_bounds__(1024) void pg_loss_grad_kernel(const float* __restr
       dlogits[b * A + j] = p[b * A + j] * (gj - dot);
     }
   }
+}
+
+// mean(vt) over a whole episode in exactly the order pg_loss_grad_kernel sums it, so a
+// data-parallel step uses the bit-identical c of the single-process step.
+__global__ __launch_bounds__(1024) void pg_vt_mean_kernel(const float* __restrict__ vt, int64_t n,
+                                                          float* __restrict__ out) {
+  __shared__ float s_red[16];
+  float sv = 0.f;
+  for (int64_t b = threadIdx.x; b < n; b += blockDim.x) sv += vt[b];
+  const float svt = block_sum_1024(sv, s_red);
+  if (threadIdx.x == 0) out[0] = svt / (float)n;
 }
 
 }  // namespace ctr
@@ -320,8 +343,26 @@ extern "C" int ctr_pg_loss_grad(const float* probs, const int64_t* acts, const f
   (void)ws;
   (void)ws_bytes;
   CTR_REQUIRE(B > 0 && A > 0 && probs && acts && vt, "ctr_pg_loss_grad: bad arguments");
-  hipLaunchKernelGGL(pg_loss_grad_kernel, 1, 1024, 0, as_stream(stream), probs, acts, vt, B, A,
-                     grad_scale, loss_out, dlogits);
+  hipLaunchKernelGGL(pg_loss_grad_kernel, 1, 1024, 0, as_stream(stream), probs, acts, vt,
+                     (const float*)nullptr, B, A, grad_scale, loss_out, dlogits);
   CTR_LAUNCH_CHECK("ctr_pg_loss_grad");
+  return CTR_OK;
+}
+
+extern "C" int ctr_pg_vt_mean(const float* vt, int64_t n, float* out, ctr_stream_t stream) {
+  CTR_REQUIRE(n > 0 && vt && out, "ctr_pg_vt_mean: bad arguments");
+  hipLaunchKernelGGL(pg_vt_mean_kernel, 1, 1024, 0, as_stream(stream), vt, n, out);
+  CTR_LAUNCH_CHECK("ctr_pg_vt_mean");
+  return CTR_OK;
+}
+
+extern "C" int ctr_pg_loss_grad_global(const float* probs, const int64_t* acts, int64_t B, int A,
+                                       const float* vt_mean, float grad_scale, float* loss_out,
+                                       float* dlogits, ctr_stream_t stream) {
+  CTR_REQUIRE(B >= 0 && A > 0 && vt_mean && (B == 0 || (probs && acts)),
+              "ctr_pg_loss_grad_global: bad arguments");
+  hipLaunchKernelGGL(pg_loss_grad_kernel, 1, 1024, 0, as_stream(stream), probs, acts,
+                     (const float*)nullptr, vt_mean, B, A, grad_scale, loss_out, dlogits);
+  CTR_LAUNCH_CHECK("ctr_pg_loss_grad_global");
   return CTR_OK;
 }

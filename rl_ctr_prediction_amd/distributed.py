@@ -66,6 +66,29 @@ def allgather_sparse_rows(rows: torch.Tensor, vals: torch.Tensor, lin: torch.Ten
     return rows_all, vals_all, lin_all
 
 
+def allgather_varlen(t: torch.Tensor, group=None) -> tuple[torch.Tensor, list[int]]:
+    """Concatenation, in rank order, of every rank's 1-D tensor `t` (lengths may differ)
+    -> (the concatenation, per-rank lengths). Padded to the longest for the collective."""
+    rank, ws = world()
+    n = t.numel()
+    if ws == 1:
+        return t.reshape(-1), [n]
+    stage = t.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if stage else t.device
+    cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(ws)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    cap = max(max(counts), 1)
+    send = torch.zeros(cap, dtype=t.dtype, device=dev)
+    send[:n] = t.reshape(-1).to(dev)
+    recv = torch.empty(ws * cap, dtype=t.dtype, device=dev)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    recv = recv.view(ws, cap)
+    out = torch.cat([recv[r, :counts[r]] for r in range(ws)]).to(t.device)
+    return out, counts
+
+
 def alltoallv(send: torch.Tensor, send_counts: list[int], recv_counts: list[int],
               group=None) -> torch.Tensor:
     """Variable-split all-to-all along dim 0: rank r sends send[sum(send_counts[:j]) ...]

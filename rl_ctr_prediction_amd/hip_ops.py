@@ -19,7 +19,7 @@ __all__ = [
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
     "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
-    "softmax_rows", "pg_discount_norm", "pg_loss_grad", "check_index_error", "Workspace",
+    "softmax_rows", "pg_discount_norm", "pg_loss_grad", "pg_vt_mean", "pg_loss_grad_global", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
 
@@ -505,3 +505,25 @@ def pg_loss_grad(probs: torch.Tensor, acts: torch.Tensor, vt: torch.Tensor, grad
                          _p(dlogits), None, 0, _stream())
     return loss, dlogits
 
+
+def pg_vt_mean(vt: torch.Tensor) -> torch.Tensor:
+    """Device scalar mean(vt), summed in pg_loss_grad's order."""
+    vt = _f32(vt.reshape(-1).contiguous(), "vt")
+    out = torch.empty(1, dtype=torch.float32, device=vt.device)
+    lib.ctr_pg_vt_mean(_p(vt), vt.numel(), _p(out), _stream())
+    return out
+
+
+def pg_loss_grad_global(probs: torch.Tensor, acts: torch.Tensor, vt_mean: torch.Tensor,
+                        grad_scale=1.0):
+    """pg_loss_grad for one rank's slice of a data-parallel episode (vt_mean = the
+    episode-wide pg_vt_mean); the returned loss is this rank's share of the episode loss."""
+    _f32(probs, "probs")
+    _f32(vt_mean, "vt_mean")
+    acts = _dev(acts, "acts").reshape(-1).to(torch.int64).contiguous()
+    B, A = probs.shape
+    loss = torch.empty(1, dtype=torch.float32, device=probs.device)
+    dlogits = torch.empty_like(probs)
+    lib.ctr_pg_loss_grad_global(_p(probs), _p(acts), B, A, _p(vt_mean), float(grad_scale),
+                                _p(loss), _p(dlogits), _stream())
+    return loss, dlogits

@@ -13,9 +13,16 @@ C4 REINFORCE configuration; documented in DESIGN.md).
 
 ``learn`` is one fused native pass: Feature_Embedding -> 5 fused GEMMs -> softmax ->
 loss + softmax-backward kernel -> 5 weight-gradient GEMMs with Dropout/ReLU mask
-epilogues -> dense Adam over one flat parameter buffer (+ one all-reduce when data
-parallel). The embedding is not updated: its output is detached (Feature_embedding.py:59),
-so torch's Adam never sees a gradient for it.
+epilogues -> dense Adam over one flat parameter buffer. The embedding is not updated: its
+output is detached (Feature_embedding.py:59), so torch's Adam never sees a gradient for it.
+
+Data parallel: the ranks' transitions are slices of ONE episode, in
+rank order. Every rank all-gathers the episode's rewards (4 B per transition) and runs the
+same discount + normalisation over the whole episode, so the returns, their mean (the
+loss_func's mean(vt)) and hence every per-sample logit gradient are bit-identical to one
+process learning the whole episode; the weight gradients are summed by one all-reduce
+(no division: loss_func is a sum over the episode), the loss shares likewise. Dropout
+masks are indexed by the transition's position in the episode, so they match too.
 """
 from __future__ import annotations
 
@@ -24,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import hip_ops
-from .distributed import allreduce_sum_, world
+from .distributed import allgather_varlen, allreduce_sum_, world
 from .feature_embedding import Feature_Embedding
 from .p_model import _dropout_seed, mlp_forward
 
@@ -184,33 +191,53 @@ class PolicyGradient:
         return d64.cpu().numpy().reshape(-1, 1)
 
     def learn(self):
-        _, vt = self._discount_norm_device()
         states = self.ep_states.to(self.device)
         acts = self.ep_as.to(self.device)
-        loss = self._fused_learn(states, acts, vt)
+        rank, ws = world()
+        if ws == 1:
+            _, vt = self._discount_norm_device()
+            loss = self._fused_learn(states, acts, vt)
+        else:
+            r = self.ep_rs.to(self.device).float().reshape(-1)
+            if r.numel() == 0:
+                raise ValueError("data-parallel learn: this rank holds no transitions")
+            r_all, counts = allgather_varlen(r, self.group)
+            _, vt_all, stats = hip_ops.pg_discount_norm(r_all, float(self.gamma))
+            if float(stats[1].item()) == 0.0:
+                raise FloatingPointError("divide by zero encountered in divide")
+            loss = self._fused_learn(states, acts, None, vt_mean=hip_ops.pg_vt_mean(vt_all),
+                                     row0=sum(counts[:rank]), n_episode=sum(counts))
         self._ep_states, self._ep_as, self._ep_rs = [], [], []
         return loss
 
     # ------------------------------------------------------------------ fused pass ----
-    def _fused_learn(self, states, acts, vt) -> torch.Tensor:
+    def _fused_learn(self, states, acts, vt, vt_mean=None, row0: int = 0,
+                     n_episode: int | None = None) -> torch.Tensor:
+        """vt: this episode's normalised returns (single process); or vt_mean: the
+        episode-wide mean(vt) when this rank holds rows [row0, row0 + B) of an episode of
+        n_episode transitions split over the data-parallel ranks."""
         net = self.policy_net
         training = net.training
         x0 = net._state(states)
         n = x0.shape[0]
+        n_ep = n if n_episode is None else n_episode
         acts_l = []
         h = x0
         mods = list(net.mlp)
         drops = [float(mods[3 * i + 2].p) if training else 0.0 for i in range(4)]
         for i, lin in enumerate(self._layers):
             last = i == len(self._layers) - 1
-            off = self._drop_offset
-            self._drop_offset += n * lin.out_features
+            off = self._drop_offset + row0 * lin.out_features
+            self._drop_offset += n_ep * lin.out_features
             h_in = h
             h = hip_ops.linear(h_in, lin.weight, lin.bias, relu=not last,
                                drop_p=0.0 if last else drops[i], seed=self._seed, offset=off)
             acts_l.append(h_in)
         probs = hip_ops.softmax_rows(h)
-        loss, g = hip_ops.pg_loss_grad(probs, acts, vt)
+        if vt_mean is None:
+            loss, g = hip_ops.pg_loss_grad(probs, acts, vt)
+        else:
+            loss, g = hip_ops.pg_loss_grad_global(probs, acts, vt_mean)
         for i in range(len(self._layers) - 1, -1, -1):
             lin = self._layers[i]
             inp = acts_l[i]
@@ -219,9 +246,9 @@ class PolicyGradient:
             if i > 0:
                 g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
                                  scale=1.0 / (1.0 - drops[i - 1]))
-        if world()[1] > 1:
+        if vt_mean is not None:  # the episode's gradient and loss: sums of the ranks' shares
             allreduce_sum_(self._grad, self.group)
-            self._grad.div_(world()[1])
+            allreduce_sum_(loss, self.group)
         self._step += 1
         hip_ops.adam_dense(self._flat, self._grad, self._m, self._v, self._step, self.lr,
                            self.betas, self.eps, self.weight_decay)
