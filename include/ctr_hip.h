@@ -107,12 +107,33 @@ int ctr_deepfm_head(const float* h, int64_t B, int H, const float* w_out, const 
  * Replaces: nn.Linear / ReLU / Dropout of DeepFM.mlp (p_model.py:276-293) and of
  * PG_model.Net.mlp (PG_model.py:41-51), forward and autograd backward (dX and dW). */
 int64_t ctr_gemm_f32_workspace_bytes(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K);
+/* ctr_gemm_f32 = ctr_gemm_f32_ex(CTR_GEMM_AUTO, ...). */
 int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                  const float* A, int64_t lda, const float* B, int64_t ldb,
                  float* C, int64_t ldc, int epi, const float* bias,
                  const float* aux, int64_t ldaux, float scale,
                  float drop_p, uint64_t seed, uint64_t offset, const int32_t* step_ptr,
                  void* ws, int64_t ws_bytes, ctr_stream_t stream);
+
+/* GEMM algorithms (same contract, same fp32 operands and outputs):
+ *  CTR_GEMM_EXACT_F32  v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation.
+ *  CTR_GEMM_SPLIT_BF16 each fp32 operand split exactly into three bf16 planes
+ *                      (x = x0 + x1 + x2, RNE); the six partial products with
+ *                      i + j <= 2 on v_mfma_f32_32x32x16_bf16, fp32 accumulation. The
+ *                      dropped terms are <= 2^-23 |a*b| per product (one fp32 multiply's
+ *                      rounding); 2.7x the fp32 matrix rate.
+ *  CTR_GEMM_AUTO       SPLIT_BF16 unless the environment sets CTR_GEMM_ALGO=exact. */
+enum ctr_gemm_algo { CTR_GEMM_AUTO = 0, CTR_GEMM_EXACT_F32 = 1, CTR_GEMM_SPLIT_BF16 = 2 };
+int64_t ctr_gemm_f32_ex_workspace_bytes(int algo, int trans_a, int trans_b, int64_t M, int64_t N,
+                                        int64_t K);
+int ctr_gemm_f32_ex(int algo, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                    const float* A, int64_t lda, const float* B, int64_t ldb,
+                    float* C, int64_t ldc, int epi, const float* bias,
+                    const float* aux, int64_t ldaux, float scale,
+                    float drop_p, uint64_t seed, uint64_t offset, const int32_t* step_ptr,
+                    void* ws, int64_t ws_bytes, ctr_stream_t stream);
+/* The algorithm CTR_GEMM_AUTO (or any value) resolves to in this process. */
+int ctr_gemm_resolved_algo(int algo);
 
 /* Deterministic reductions (fixed order; identical bits run to run).
  * ctr_sum_f32:    out[0] = scale * sum_i x[i]

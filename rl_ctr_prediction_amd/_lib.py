@@ -43,6 +43,11 @@ SIGNATURES = {
     "ctr_gemm_f32_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
     "ctr_gemm_f32": (_i32, [_i32, _i32, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i32,
                             _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp, _i64, _vp]),
+    "ctr_gemm_f32_ex_workspace_bytes": (_i64, [_i32, _i32, _i32, _i64, _i64, _i64]),
+    "ctr_gemm_f32_ex": (_i32, [_i32, _i32, _i32, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
+                               _i64, _i32, _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp,
+                               _i64, _vp]),
+    "ctr_gemm_resolved_algo": (_i32, [_i32]),
     "ctr_reduce_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sum_f32": (_i32, [_vp, _i64, _f32, _vp, _vp, _i64, _vp]),
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),

@@ -17,56 +17,9 @@
 // slabs and summed in slab order by a second kernel: deterministic, no atomics.
 #include <stdlib.h>
 
-#include "ctr_common.h"
+#include "gemm_common.h"
 
 namespace ctr {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct GemmArgs {
-  int64_t M, N, K;
-  const float* A;
-  int64_t lda;
-  const float* B;
-  int64_t ldb;
-  float* C;
-  int64_t ldc;
-  int epi;
-  const float* bias;
-  const float* aux;
-  int64_t ldaux;
-  float scale;        // GRAD_MASK multiplier
-  uint32_t drop_thr;  // keep iff hash >= drop_thr
-  float drop_scale;   // 1/(1-p)
-  uint64_t seed, offset;
-  const int32_t* step_ptr;  // dropout stream of step *step_ptr: offset += step << 32
-  int64_t k_per_split;
-  int64_t slab_stride;  // elements between split-K slabs (0: no split)
-  bool vec_a, vec_b;
-  bool vec_c;  // C rows 16-B aligned (float4 epilogue stores)
-};
-
-__device__ __forceinline__ float apply_epi(const GemmArgs& a, int epi, float acc, int64_t m,
-                                           int64_t n) {
-  switch (epi) {
-    case CTR_EPI_BIAS:
-      return acc + a.bias[n];
-    case CTR_EPI_BIAS_RELU: {
-      const float v = acc + a.bias[n];
-      return v > 0.f ? v : 0.f;
-    }
-    case CTR_EPI_BIAS_RELU_DROP: {
-      float v = acc + a.bias[n];
-      v = v > 0.f ? v : 0.f;
-      const uint32_t hsh = hash_u32(a.seed, a.offset + (uint64_t)(m * a.N + n));
-      return hsh >= a.drop_thr ? v * a.drop_scale : 0.f;
-    }
-    case CTR_EPI_GRAD_MASK:
-      return a.aux[m * a.ldaux + n] > 0.f ? acc * a.scale : 0.f;
-    default:
-      return acc;
-  }
-}
 
 // ------------------------------------------------------------------- the kernel ------
 // Block = WAVES_M x WAVES_N x KSPLIT waves (4: one per SIMD), tile BM x BN x BK=32; a wave
@@ -185,9 +138,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
   // tile of this block: tiles sharing A rows are consecutive, and consecutive tiles are
   // kept on one XCD (blocks b, b+8, b+16... share an XCD under round-robin dispatch)
   const int64_t gn = (a.N + BN - 1) / BN;
-  const int64_t T = gridDim.x;
-  int64_t tix = blockIdx.x;
-  if (T % 8 == 0) tix = (tix % 8) * (T / 8) + tix / 8;
+  const int64_t tix = xcd_tile_index();
   const int64_t m0 = (tix / gn) * BM;
   const int64_t n0 = (tix % gn) * BN;
   const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
@@ -506,47 +457,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N* KSPLIT * 64) void gemm_f32_kernel
   }
   if (kw > 0) return;
 
-  // Epilogue through a wave-private 32x33 LDS tile per accumulator: the MFMA's C/D map
-  // (col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)) is written out, then read back
-  // in row order for the epilogue and the stores. Keeps the accumulator indexing static (a
-  // per-element epilogue over all TM*TN*16 values put the accumulators in scratch).
-  float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
-  const int epi = a.slab_stride ? (int)CTR_EPI_NONE : a.epi;
-  if (epi == CTR_EPI_BIAS_RELU_DROP && a.step_ptr) a.offset += (uint64_t)(*a.step_ptr) << 32;
-  float* et = smem + wmn * (32 * 36);
-  const int er = lane >> 3, ec = 4 * (lane & 7);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) et[((r & 3) + 8 * (r >> 2) + 4 * h) * 36 + il] = acc[i][tn][r];
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private tile, no barrier
-      __builtin_amdgcn_wave_barrier();
-      // lane -> row er + 8j, columns ec..ec+3: each store instruction covers 8 rows x 128 B
-      const int64_t n = n0 + wn0 + tn * 32 + ec;
-      for (int j = 0; j < 4; ++j) {
-        const int row = er + 8 * j;
-        const int64_t m = m0 + wm0 + i * 32 + row;
-        if (m >= a.M) continue;
-        const float4 v = *reinterpret_cast<const float4*>(et + row * 36 + ec);
-        float* crow = C + m * a.ldc;
-        if (a.vec_c && n + 3 < a.N) {
-          float4 o;
-          o.x = apply_epi(a, epi, v.x, m, n + 0);
-          o.y = apply_epi(a, epi, v.y, m, n + 1);
-          o.z = apply_epi(a, epi, v.z, m, n + 2);
-          o.w = apply_epi(a, epi, v.w, m, n + 3);
-          *reinterpret_cast<float4*>(crow + n) = o;
-        } else {
-          if (n + 0 < a.N) crow[n + 0] = apply_epi(a, epi, v.x, m, n + 0);
-          if (n + 1 < a.N) crow[n + 1] = apply_epi(a, epi, v.y, m, n + 1);
-          if (n + 2 < a.N) crow[n + 2] = apply_epi(a, epi, v.z, m, n + 2);
-          if (n + 3 < a.N) crow[n + 3] = apply_epi(a, epi, v.w, m, n + 3);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
+  gemm_store_tiles<TM, TN>(a, acc, smem + wmn * (32 * 36), m0 + wm0, n0 + wn0, lane);
 #if CTR_GEMM_TRACE
   if (tid == 0 && tr_b < 16384) g_gemm_trace[tr_b * 5 + 3] = clock64();
 #endif
@@ -668,14 +579,103 @@ static void launch_tile(int ti, const GemmArgs& a, bool ta, bool tb, dim3 grid, 
 
 using namespace ctr;
 
+// CTR_GEMM_AUTO resolves to CTR_GEMM_SPLIT_BF16 unless CTR_GEMM_ALGO=exact is set in the
+// environment (read once per process).
+static int resolve_algo(int algo) {
+  if (algo != CTR_GEMM_AUTO) return algo;
+  static const int dflt = [] {
+    const char* e = getenv("CTR_GEMM_ALGO");
+    return (e && (strcmp(e, "exact") == 0 || strcmp(e, "f32") == 0)) ? (int)CTR_GEMM_EXACT_F32
+                                                                       : (int)CTR_GEMM_SPLIT_BF16;
+  }();
+  return dflt;
+}
+
+// Measured winners (MI355X, tools/gemm_bench.py sweeps of both kernels over every tiling x
+// split-K; profiles/r01_gemm_tuning_sb16.txt) for the shapes of the hot path: the DeepFM
+// MLP at B=8192 (C3) and the PG policy MLP at B=4096 (C4). Other shapes use the model.
+struct KnownGemm {
+  int64_t M, N, K;
+  int ta, tb, algo, tile, splits;
+};
+static const KnownGemm kKnown[] = {
+    {8192, 300, 1664, 0, 1, CTR_GEMM_SPLIT_BF16, 4, 2},   // DeepFM fwd0  X.W0^T
+    {8192, 200, 300, 0, 1, CTR_GEMM_SPLIT_BF16, 0, 1},    // fwd1  H1.W1^T
+    {8192, 300, 200, 0, 0, CTR_GEMM_SPLIT_BF16, 0, 1},    // dH1 = dH2.W1
+    {8192, 1664, 300, 0, 0, CTR_GEMM_SPLIT_BF16, 1, 1},   // dX  = dH1.W0
+    {200, 300, 8192, 1, 0, CTR_GEMM_EXACT_F32, 0, 16},    // dW1 = dH2^T.H1
+    {300, 1664, 8192, 1, 0, CTR_GEMM_SPLIT_BF16, 1, 16},  // dW0 = dH1^T.X
+    {4096, 1024, 741, 0, 1, CTR_GEMM_SPLIT_BF16, 2, 1},   // PG policy fwd0
+    {1024, 741, 4096, 1, 0, CTR_GEMM_SPLIT_BF16, 3, 4},   // dW0
+    {4096, 512, 1024, 0, 1, CTR_GEMM_SPLIT_BF16, 0, 1},   // fwd1
+    {4096, 1024, 512, 0, 0, CTR_GEMM_SPLIT_BF16, 3, 1},   // dX1
+    {512, 1024, 4096, 1, 0, CTR_GEMM_SPLIT_BF16, 3, 8},   // dW1
+};
+
+struct GemmPlan {
+  int algo;
+  int tile;  // exact kernel's tiling (algo == EXACT)
+  Sb16Cfg sc;  // split kernel's config (algo == SPLIT)
+  int splits;
+  int64_t kps;
+  int bm, bn;
+};
+
+static GemmPlan plan_gemm(int algo, int ta, int tb, int64_t M, int64_t N, int64_t K) {
+  GemmPlan p{};
+  auto k_split = [&](int sp, int& splits, int64_t& kps) {
+    splits = 1;
+    kps = std::max<int64_t>(K, 1);
+    if (sp > 1 && K >= 64) {
+      kps = align_up(ceil_div(K, sp), 32);
+      splits = (int)ceil_div(K, kps);
+    }
+  };
+  const bool forced_cfg = getenv("CTR_GEMM_CFG") != nullptr;
+  if (algo == CTR_GEMM_AUTO && !forced_cfg) {
+    for (const KnownGemm& k : kKnown) {
+      if (k.M != M || k.N != N || k.K != K || k.ta != (ta != 0) || k.tb != (tb != 0)) continue;
+      if (k.algo == CTR_GEMM_SPLIT_BF16 && resolve_algo(CTR_GEMM_AUTO) != CTR_GEMM_SPLIT_BF16)
+        break;  // the environment asked for the exact kernel everywhere
+      p.algo = k.algo;
+      k_split(k.splits, p.splits, p.kps);
+      if (p.algo == CTR_GEMM_SPLIT_BF16) {
+        p.sc = Sb16Cfg{k.tile, p.splits, p.kps, 0, 0};
+        sb16_tile_dims(k.tile, p.sc.bm, p.sc.bn);
+        p.bm = p.sc.bm, p.bn = p.sc.bn;
+      } else {
+        p.tile = k.tile;
+        p.bm = kTiles[k.tile].bm, p.bn = kTiles[k.tile].bn;
+      }
+      return p;
+    }
+  }
+  p.algo = resolve_algo(algo);
+  if (p.algo == CTR_GEMM_SPLIT_BF16) {
+    p.sc = sb16_choose(M, N, K);
+    p.splits = p.sc.splits, p.kps = p.sc.kps, p.bm = p.sc.bm, p.bn = p.sc.bn;
+  } else {
+    const TileCfg c = choose_tiles(M, N, K);
+    p.tile = c.tile, p.splits = c.splits, p.kps = c.kps;
+    p.bm = kTiles[c.tile].bm, p.bn = kTiles[c.tile].bn;
+  }
+  return p;
+}
+
+extern "C" int64_t ctr_gemm_f32_ex_workspace_bytes(int algo, int trans_a, int trans_b, int64_t M,
+                                                   int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return -1;
+  if (algo < CTR_GEMM_AUTO || algo > CTR_GEMM_SPLIT_BF16) return -1;
+  const int64_t s = plan_gemm(algo, trans_a, trans_b, M, N, K).splits;
+  return s > 1 ? s * M * N * (int64_t)sizeof(float) : 0;
+}
+
 extern "C" int64_t ctr_gemm_f32_workspace_bytes(int trans_a, int trans_b, int64_t M, int64_t N,
                                                 int64_t K) {
-  (void)trans_a;
-  (void)trans_b;
-  if (M < 0 || N < 0 || K < 0) return -1;
-  const TileCfg c = choose_tiles(M, N, K);
-  return c.splits > 1 ? (int64_t)c.splits * M * N * (int64_t)sizeof(float) : 0;
+  return ctr_gemm_f32_ex_workspace_bytes(CTR_GEMM_AUTO, trans_a, trans_b, M, N, K);
 }
+
+extern "C" int ctr_gemm_resolved_algo(int algo) { return resolve_algo(algo); }
 
 #if CTR_GEMM_TRACE
 extern "C" int ctr_debug_gemm_trace(unsigned long long* host, int n_blocks) {
@@ -684,12 +684,14 @@ extern "C" int ctr_debug_gemm_trace(unsigned long long* host, int n_blocks) {
 }
 #endif
 
-extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
-                            const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
-                            int64_t ldc, int epi, const float* bias, const float* aux,
-                            int64_t ldaux, float scale, float drop_p, uint64_t seed,
-                            uint64_t offset, const int32_t* step_ptr, void* ws, int64_t ws_bytes,
-                            ctr_stream_t stream) {
+extern "C" int ctr_gemm_f32_ex(int algo, int trans_a, int trans_b, int64_t M, int64_t N,
+                               int64_t K, const float* A, int64_t lda, const float* B,
+                               int64_t ldb, float* C, int64_t ldc, int epi, const float* bias,
+                               const float* aux, int64_t ldaux, float scale, float drop_p,
+                               uint64_t seed, uint64_t offset, const int32_t* step_ptr, void* ws,
+                               int64_t ws_bytes, ctr_stream_t stream) {
+  CTR_REQUIRE(algo >= CTR_GEMM_AUTO && algo <= CTR_GEMM_SPLIT_BF16, "ctr_gemm_f32: bad algo %d",
+              algo);
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "ctr_gemm_f32: negative size");
   CTR_REQUIRE(epi >= CTR_EPI_NONE && epi <= CTR_EPI_GRAD_MASK, "ctr_gemm_f32: bad epilogue %d",
               epi);
@@ -723,11 +725,13 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
             ((trans_b ? K : N) % 4 == 0);
   a.vec_c = (reinterpret_cast<uintptr_t>(C) % 16 == 0) && (ldc % 4 == 0);
 
-  const TileCfg c = choose_tiles(M, N, K);
-  a.k_per_split = c.splits > 1 ? c.kps : std::max<int64_t>(K, 1);
+  const GemmPlan pl = plan_gemm(algo, trans_a, trans_b, M, N, K);
+  const int splits = pl.splits;
+  const int64_t kps = pl.kps;
+  a.k_per_split = splits > 1 ? kps : std::max<int64_t>(K, 1);
   a.slab_stride = 0;
-  if (c.splits > 1) {
-    const int64_t need = (int64_t)c.splits * M * N * (int64_t)sizeof(float);
+  if (splits > 1) {
+    const int64_t need = (int64_t)splits * M * N * (int64_t)sizeof(float);
     if (!ws || ws_bytes < need) {
       set_error("ctr_gemm_f32: split-K workspace %lld < %lld bytes", (long long)ws_bytes,
                 (long long)need);
@@ -738,18 +742,33 @@ extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
     a.slab_stride = M * N;
     a.vec_c = (reinterpret_cast<uintptr_t>(ws) % 16 == 0) && (N % 4 == 0) && ((M * N) % 4 == 0);
   }
-  const TileDef& d = kTiles[c.tile];
-  const dim3 grid((unsigned)(ceil_div(N, d.bn) * ceil_div(M, d.bm)), 1, (unsigned)c.splits);
-  launch_tile(c.tile, a, trans_a != 0, trans_b != 0, grid, st);
-  CTR_LAUNCH_CHECK("gemm_f32_kernel");
-  if (c.splits > 1) {
+  const dim3 grid((unsigned)(ceil_div(N, pl.bn) * ceil_div(M, pl.bm)), 1, (unsigned)splits);
+  if (pl.algo == CTR_GEMM_SPLIT_BF16) {
+    sb16_launch(pl.sc, a, trans_a != 0, trans_b != 0, grid, st);
+    CTR_LAUNCH_CHECK("gemm_sb16_kernel");
+  } else {
+    launch_tile(pl.tile, a, trans_a != 0, trans_b != 0, grid, st);
+    CTR_LAUNCH_CHECK("gemm_f32_kernel");
+  }
+  if (splits > 1) {
     GemmArgs r = a;
     r.C = C;
     r.ldc = ldc;
     const unsigned g2 = (unsigned)std::min<int64_t>(ceil_div(M * N, 256), 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, g2, 256, 0, st, r, static_cast<const float*>(ws),
-                       c.splits);
+                       splits);
     CTR_LAUNCH_CHECK("splitk_reduce_kernel");
   }
   return CTR_OK;
+}
+
+extern "C" int ctr_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                            const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                            int64_t ldc, int epi, const float* bias, const float* aux,
+                            int64_t ldaux, float scale, float drop_p, uint64_t seed,
+                            uint64_t offset, const int32_t* step_ptr, void* ws, int64_t ws_bytes,
+                            ctr_stream_t stream) {
+  return ctr_gemm_f32_ex(CTR_GEMM_AUTO, trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, epi,
+                         bias, aux, ldaux, scale, drop_p, seed, offset, step_ptr, ws, ws_bytes,
+                         stream);
 }

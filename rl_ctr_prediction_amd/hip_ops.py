@@ -164,12 +164,17 @@ def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.
 
 
 # --------------------------------------------------------------------------- GEMM ----
+GEMM_AUTO, GEMM_EXACT_F32, GEMM_SPLIT_BF16 = 0, 1, 2  # enum ctr_gemm_algo
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False, *,
          epi: int = EPI_NONE, bias=None, aux=None, scale: float = 1.0, drop_p: float = 0.0,
          seed: int = 0, offset: int = 0, step_dev: torch.Tensor | None = None,
-         out: torch.Tensor | None = None) -> torch.Tensor:
-    """C = op(a) @ op(b) on fp32 MFMA with a fused epilogue (see include/ctr_hip.h).
-    step_dev (device int32): the dropout stream of that step (offset += step << 32)."""
+         out: torch.Tensor | None = None, algo: int = GEMM_AUTO) -> torch.Tensor:
+    """C = op(a) @ op(b) on the MFMA units with a fused epilogue (see include/ctr_hip.h):
+    algo GEMM_EXACT_F32 (fp32 MFMA) or GEMM_SPLIT_BF16 (three-plane bf16 split, fp32
+    accurate); GEMM_AUTO = the library default. step_dev (device int32): the dropout stream
+    of that step (offset += step << 32)."""
     _f32(a, "A")
     _f32(b, "B")
     M, K = (a.shape[1], a.shape[0]) if trans_a else a.shape
@@ -184,13 +189,13 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
             raise ValueError("gemm: bad out shape")
     if aux is not None:
         _f32(aux, "aux")
-    nbytes = lib.ctr_gemm_f32_workspace_bytes(int(trans_a), int(trans_b), M, N, K)
+    nbytes = lib.ctr_gemm_f32_ex_workspace_bytes(int(algo), int(trans_a), int(trans_b), M, N, K)
     ws = Workspace.get(nbytes, a.device)
-    lib.ctr_gemm_f32(int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b), b.stride(0),
-                     _p(out), out.stride(0), int(epi), _p(bias), _p(aux),
-                     aux.stride(0) if aux is not None else 0, float(scale), float(drop_p),
-                     int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(step_dev), _p(ws),
-                     0 if ws is None else ws.numel(), _stream())
+    lib.ctr_gemm_f32_ex(int(algo), int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b),
+                        b.stride(0), _p(out), out.stride(0), int(epi), _p(bias), _p(aux),
+                        aux.stride(0) if aux is not None else 0, float(scale), float(drop_p),
+                        int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(step_dev), _p(ws),
+                        0 if ws is None else ws.numel(), _stream())
     return out
 
 

@@ -147,28 +147,58 @@ def test_out_of_range_ids_flag_not_fault(cuda):
 
 
 # ------------------------------------------------------------------------- GEMM -----
+_ALGO = {"exact": 1, "split": 2}  # enum ctr_gemm_algo (hip_ops.GEMM_EXACT_F32 / _SPLIT_BF16)
+
+
+def test_gemm_split_bf16_accuracy(cuda):
+    """The split-bf16 GEMM is as accurate as the exact-fp32 one: on the DeepFM shapes its
+    error against fp64, relative to the L1 bound, is within 2x of the fp32 kernel's
+    (both are fp32-accumulation errors), and both are far under the 1e-5 bar."""
+    H = _hip()
+    g = torch.Generator().manual_seed(5)
+    for (M, N, K, ta, tb) in ((8192, 300, 1664, False, True), (300, 1664, 8192, True, False),
+                              (8192, 1664, 300, False, False)):
+        A = torch.randn(M, K, generator=g) * 0.1
+        Bm = torch.randn(K, N, generator=g)
+        a = (A.t() if ta else A).contiguous().to(cuda)
+        b = (Bm.t() if tb else Bm).contiguous().to(cuda)
+        ref = A.double() @ Bm.double()
+        bound = A.double().abs() @ Bm.double().abs()
+        err = {}
+        for name, algo in _ALGO.items():
+            C = H.gemm(a, b, ta, tb, algo=algo).cpu().double()
+            err[name] = ((C - ref).abs() / bound).max().item()
+        assert err["split"] < 1e-6, err
+        assert err["split"] <= 2.0 * err["exact"] + 1e-8, (M, N, K, err)
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 5, 3), (64, 64, 32), (130, 70, 33),
                                    (300, 1664, 8192), (8192, 300, 1664), (8192, 1664, 300),
                                    (512, 200, 300), (4, 1024, 741)])
-def test_gemm_vs_fp64(cuda, ta, tb, M, N, K):
+@pytest.mark.parametrize("algo", ["exact", "split"])
+def test_gemm_vs_fp64(cuda, ta, tb, M, N, K, algo):
     H = _hip()
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
     A = torch.randn(M, K, generator=g)
     Bm = torch.randn(K, N, generator=g)
     a = (A.t() if ta else A).contiguous().to(cuda)
     b = (Bm.t() if tb else Bm).contiguous().to(cuda)
-    C = H.gemm(a, b, ta, tb).cpu().double()
+    C = H.gemm(a, b, ta, tb, algo=_ALGO[algo]).cpu().double()
     ref = A.double() @ Bm.double()
     bound = (A.double().abs() @ Bm.double().abs())
-    # fp32 accumulation (exact-fp32 MFMA = a k-ordered fmaf chain): error grows ~sqrt(K)
+    # fp32 accumulation (exact-fp32 MFMA = a k-ordered fmaf chain; split-bf16: products to
+    # 2^-23 relative, fp32 accumulation): error grows ~sqrt(K)
     tol = 1e-6 * max(1.0, (K / 1024) ** 0.5)
     assert ((C - ref).abs() <= tol * bound + 1e-30).all()
 
 
-@pytest.mark.parametrize("tile", range(10))  # every compiled tiling of csrc/gemm.hip (kTiles)
-def test_gemm_every_tiling(cuda, tile, monkeypatch):
+def _gemm_tilings(n_tiles, algo_name):
+    return [(algo_name, t) for t in range(n_tiles)]
+
+
+# every compiled tiling of csrc/gemm.hip (kTiles) and csrc/gemm_sb16.hip (kSb16)
+@pytest.mark.parametrize("algo,tile", _gemm_tilings(10, "exact") + _gemm_tilings(7, "split"))
+def test_gemm_every_tiling(cuda, algo, tile, monkeypatch):
     """Force each tiling (and split-K) on shapes with M/N edges and K tails, both the float4
     path (extents % 4 == 0) and the scalar path, every transpose: fp32 parity vs fp64."""
     H = _hip()
@@ -184,13 +214,14 @@ def test_gemm_every_tiling(cuda, tile, monkeypatch):
                 for tb in (False, True):
                     a = (A.t() if ta else A).contiguous().to(cuda)
                     b = (Bm.t() if tb else Bm).contiguous().to(cuda)
-                    C = H.gemm(a, b, ta, tb).cpu().double()
+                    C = H.gemm(a, b, ta, tb, algo=_ALGO[algo]).cpu().double()
                     bad = (C - ref).abs() > 2e-6 * bound + 1e-30
                     assert not bad.any(), (tile, splits, M, N, K, ta, tb, int(bad.sum()))
         bias = torch.randn(452, generator=g)
         A = torch.randn(333, 1060, generator=g)
         W = torch.randn(452, 1060, generator=g)
-        y = H.linear(A.to(cuda), W.to(cuda), bias.to(cuda), relu=True).cpu().double()
+        y = H.gemm(A.to(cuda), W.to(cuda), False, True, epi=H.EPI_BIAS_RELU, bias=bias.to(cuda),
+                   algo=_ALGO[algo]).cpu().double()
         r = (A.double() @ W.double().t() + bias.double()).clamp(min=0)
         np.testing.assert_allclose(y.numpy(), r.numpy(), rtol=1e-5, atol=1e-4)
 

@@ -33,17 +33,32 @@ SHAPES = {  # name: (M, N, K, trans_a, trans_b)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--configs", default="auto," + ",".join(
-        f"{t}x{s}" for t in range(10) for s in (1, 2, 4, 8, 9, 16)))
+    ap.add_argument("--algo", default="split", choices=["exact", "split"])
+    ap.add_argument("--c4", action="store_true", help="the C4 policy-MLP shapes instead")
+    ap.add_argument("--configs", default=None)
     ap.add_argument("--square", type=int, default=0,
                     help="time only an NxNxN NN product (kernel's intrinsic rate)")
     args = ap.parse_args()
+    algo = {"exact": H.GEMM_EXACT_F32, "split": H.GEMM_SPLIT_BF16}[args.algo]
+    if args.c4:
+        SHAPES.clear()
+        b = 4096
+        dims = [741, 1024, 512, 256, 128, 5]
+        for i in range(5):
+            k, n = dims[i], dims[i + 1]
+            SHAPES[f"fwd{i} {k}->{n}"] = (b, n, k, False, True)
+            if i > 0:
+                SHAPES[f"dX{i} {n}->{k}"] = (b, k, n, False, False)
+            SHAPES[f"dW{i} {k}x{n}"] = (n, k, b, True, False)
     if args.square:
         n = args.square
         SHAPES.clear()
         SHAPES[f"square {n}"] = (n, n, n, False, False)
         SHAPES[f"square {n} NT"] = (n, n, n, False, True)
         SHAPES[f"square {n} TN"] = (n, n, n, True, False)
+    if args.configs is None:
+        nt = 10 if args.algo == "exact" else 7
+        args.configs = "auto," + ",".join(f"{t}x{s}" for t in range(nt) for s in (1, 2, 4, 8, 16))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     total_best = 0.0
@@ -61,12 +76,12 @@ def main():
                     continue
                 os.environ["CTR_GEMM_CFG"] = f"{tile},{sp}"
             for _ in range(3):
-                H.gemm(a, b, ta, tb, out=out)
+                H.gemm(a, b, ta, tb, out=out, algo=algo)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.reps):
-                H.gemm(a, b, ta, tb, out=out)
+                H.gemm(a, b, ta, tb, out=out, algo=algo)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / args.reps * 1e3
@@ -84,7 +99,7 @@ def main():
     a = torch.randn(513, 300, device=dev)
     w = torch.randn(200, 300, device=dev)
     ref = (a.double() @ w.double().t()).float()
-    got = H.gemm(a, w, False, True)
+    got = H.gemm(a, w, False, True, algo=algo)
     print(json.dumps({"check_max_abs_err": float((got - ref).abs().max())}))
 
 

@@ -18,7 +18,7 @@ import csv, glob, collections
 agg = collections.defaultdict(list)
 for f in glob.glob("gpurun_out/pmc_gemm/p*/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "gemm_f32_kernel" in r["Kernel_Name"]:
+        if "gemm_" in r["Kernel_Name"] and "reduce" not in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg.items()):
     print(f"{k:28s} {sum(v)/len(v):16.1f}")
