@@ -151,9 +151,10 @@ _ALGO = {"exact": 1, "split": 2}  # enum ctr_gemm_algo (hip_ops.GEMM_EXACT_F32 /
 
 
 def test_gemm_split_bf16_accuracy(cuda):
-    """The split-bf16 GEMM is as accurate as the exact-fp32 one: on the DeepFM shapes its
-    error against fp64, relative to the L1 bound, is within 2x of the fp32 kernel's
-    (both are fp32-accumulation errors), and both are far under the 1e-5 bar."""
+    """The split-bf16 GEMM is at least as accurate as the exact-fp32 one: on the DeepFM
+    shapes its worst error against fp64, relative to the L1 bound, is no larger than the
+    fp32 kernel's (its main accumulator rounds once per 16 k, the fp32 MFMA chain 8 times;
+    measured ~0.3-0.45x), and both are far under the 1e-5 bar."""
     H = _hip()
     g = torch.Generator().manual_seed(5)
     for (M, N, K, ta, tb) in ((8192, 300, 1664, False, True), (300, 1664, 8192, True, False),
@@ -169,7 +170,7 @@ def test_gemm_split_bf16_accuracy(cuda):
             C = H.gemm(a, b, ta, tb, algo=algo).cpu().double()
             err[name] = ((C - ref).abs() / bound).max().item()
         assert err["split"] < 1e-6, err
-        assert err["split"] <= 2.0 * err["exact"] + 1e-8, (M, N, K, err)
+        assert err["split"] <= err["exact"], (M, N, K, err)
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 5, 3), (64, 64, 32), (130, 70, 33),
