@@ -54,7 +54,12 @@ CONFIGS = {
                         "4096 transitions/GPU"),
     "c5": dict(kind="FM", V=40_000_000, F=22, K=128, B=8192,
                workload="C5 FM, Avazu-shape 22 fields, 40M vocab, embed_dim 128, batch 8192/GPU"),
+    # SURVEY.md §8f rank 1 (not a BASELINE config): InnerPNN at the C3 shape
+    "ipnn": dict(kind="IPNN", V=10_000_000, F=26, K=64, B=8192,
+                 workload="IPNN (flat ++ 325 pair dots -> MLP 1989-300-200-1), Criteo-shape 26 "
+                          "fields, 10M vocab, embed_dim 64, batch 8192/GPU"),
 }
+MLP_KINDS = ("DeepFM", "IPNN")
 
 
 def log(*a):
@@ -316,7 +321,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from rl_ctr_prediction_amd import DeepFM, FM, FusedCTRTrainer, ShardedCTRTrainer
+    from rl_ctr_prediction_amd import DeepFM, FM, FusedCTRTrainer, InnerPNN, ShardedCTRTrainer
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
 
     cfg = CONFIGS[args.config]
@@ -326,7 +331,8 @@ def main():
     t0 = time.perf_counter()
     torch.manual_seed(1)  # identical replicas on every rank
     with torch.device(dev):
-        model = FM(V, K) if cfg["kind"] == "FM" else DeepFM(V, F, K)
+        model = {"FM": lambda: FM(V, K), "DeepFM": lambda: DeepFM(V, F, K),
+                 "IPNN": lambda: InnerPNN(V, F, K)}[cfg["kind"]]()
     model.train()
     synth = CriteoSynth(V, F, seed=1)
     # every distinct batch is seen during the warm-up, so its HIP graph is captured there
@@ -403,7 +409,7 @@ def main():
 
     U = trainer._bufs.plan.num_unique_host()
     S = B * F
-    deep = cfg["kind"] == "DeepFM"
+    deep = cfg["kind"] in MLP_KINDS
     gemm_flops_bd = sum(w for _, _, w in bd["gemm"])
     kernels = {
         "_note": f"breakdown pass of {n_bd} un-timed steps (+flush), every group bracketed "
@@ -427,12 +433,15 @@ def main():
     if dominant == "gemm":
         flops = sum(w for _, _, w in spans) / len(spans)
         achieved = flops / (launch_ms * 1e-3) / 1e12
-        roofline = {"kernel": "gemm_f32_kernel (fp32 MFMA 32x32x2; the 6 MLP GEMMs of a step, "
-                              "averaged per launch)",
+        roofline = {"kernel": "MLP GEMMs (gemm_sb16_kernel: fp32-accurate split-bf16 MFMA; "
+                              "gemm_f32_kernel: fp32 MFMA), the 6 of a step averaged per launch",
                     "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
+                    "peak_note": "fp32 matrix peak (the path's dtype); the split-bf16 "
+                                 "algorithm's own ceiling is 2.5 PF bf16 / 6 products = "
+                                 "417 TF",
                     "algorithmic_flops_per_launch": flops}
-        traffic, src = load_traffic(args.config, "gemm_f32_kernel")
+        traffic, src = load_traffic(args.config, "gemm")
     else:
         if dominant == "adam":
             if args.optimizer == "dense":

@@ -294,6 +294,21 @@ int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int 
                                   int64_t V, const float* emb, float* out, int32_t* err_flag,
                                   ctr_stream_t stream);
 
+/* ------------------------------------------------ §8f: IPNN (InnerPNN) --------------
+ * ctr_ipnn_forward: cat[b] = flat(E[x_b]) (F*K) ++ [ <E[x_bi],E[x_bj]> for i<j, row-major ]
+ *   (P = F(F-1)/2), cat is [B, >= F*K + P] with row stride ldc: the MLP input of
+ *   p_model.InnerPNN.forward (p_model.py:187-195).
+ * ctr_ipnn_backward: dslot[b*F+f, :] (slot order, [B*F, K]) = dcat[b, f*K:(f+1)*K]
+ *   + sum_{j != f} dcat[b, F*K + pair(f,j)] * E[x_bj, :] — the gradient of every slot's
+ *   embedding through the view and the two pair index ops; per-row sums then go through
+ *   ctr_segment_sum_rows (embedding_dense_backward of p_model.py:187). */
+int ctr_ipnn_forward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                     const float* emb, float* cat, int64_t ldc, int32_t* err_flag,
+                     ctr_stream_t stream);
+int ctr_ipnn_backward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                      const float* emb, const float* dcat, int64_t ldd, float* dslot,
+                      ctr_stream_t stream);
+
 /* ------------------------------------------------------ A8: REINFORCE (PG) -----------
  * ctr_softmax_rows: out[b,:] = softmax(x[b,:]) (PG_model.py:56).
  * ctr_pg_discount_norm: discounted return of an episode, reverse recurrence

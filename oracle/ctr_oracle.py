@@ -9,6 +9,7 @@ A from-scratch restatement of jqsl2012/RL_CTR_Prediction's algorithms on torch-C
 
   fm_forward          p_model.py:40-57       (FM.forward)
   deepfm_forward      p_model.py:296-324     (DeepFM.to_fm + forward, MLP 276-293)
+  ipnn_forward        p_model.py:146-200     (InnerPNN: flat ++ pairwise inner products, MLP)
   bce                 all_main/pretrain_main.py:74,139 (nn.BCELoss, mean)
   train_step          all_main/pretrain_main.py:67-83 (fwd, BCE, zero_grad, backward, Adam)
   feature_embedding   Feature_embedding.py:51-59
@@ -33,12 +34,30 @@ DEEPFM_KEYS = FM_KEYS + ("mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bi
                          "mlp.6.weight", "mlp.6.bias")
 
 
+IPNN_KEYS = ("feature_embedding.weight", "mlp.0.weight", "mlp.0.bias", "mlp.3.weight",
+             "mlp.3.bias", "mlp.6.weight", "mlp.6.bias")
+
+
+def ipnn_pairs(F: int):
+    """The reference's self.row / self.col (p_model.py:179-182): row-major i < j."""
+    row, col = np.triu_indices(F, k=1)
+    return torch.as_tensor(row), torch.as_tensor(col)
+
+
 def init_params(kind: str, V: int, F: int, K: int, seed: int | None = None) -> dict:
     """Parameters with the reference modules' default initialisers, created in the
     reference's order: N(0,1) embeddings (nn.Embedding), zero bias, nn.Linear's
     kaiming-uniform weights / uniform biases."""
     if seed is not None:
         torch.manual_seed(seed)
+    if kind == "IPNN":  # p_model.py:153-177: embedding, then Linear(F*K + P, 300), ...
+        p = {"feature_embedding.weight": torch.nn.Embedding(V, K).weight.data}
+        dims = [F * K + F * (F - 1) // 2, 300, 200, 1]
+        for i, name in zip(range(3), ("mlp.0", "mlp.3", "mlp.6")):
+            lin = torch.nn.Linear(dims[i], dims[i + 1])
+            p[f"{name}.weight"] = lin.weight.data
+            p[f"{name}.bias"] = lin.bias.data
+        return {k: v.clone().requires_grad_(True) for k, v in p.items()}
     p = {"linear.weight": torch.nn.Embedding(V, 1).weight.data,
          "bias": torch.zeros(1),
          "feature_embedding.weight": torch.nn.Embedding(V, K).weight.data}
@@ -81,8 +100,27 @@ def deepfm_forward(params: dict, x: torch.Tensor, drop_p: float = 0.2,
     return torch.sigmoid(fm_logit(params, x) + deep)
 
 
+def ipnn_cat(E: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """MLP input of InnerPNN.forward (p_model.py:187-195): flat(e) ++ <e_i, e_j>, i < j."""
+    B, F = x.shape
+    e = Fn.embedding(x, E)
+    row, col = ipnn_pairs(F)
+    inner = torch.sum(torch.mul(e[:, row], e[:, col]), dim=2)
+    return torch.cat([e.reshape(B, -1), inner], dim=1)
+
+
+def ipnn_forward(params: dict, x: torch.Tensor, drop_p: float = 0.2,
+                 training: bool = True) -> torch.Tensor:
+    return torch.sigmoid(mlp(params, ipnn_cat(params["feature_embedding.weight"], x), drop_p,
+                             training))
+
+
 def forward(kind: str, params: dict, x, drop_p=0.2, training=True):
-    return fm_forward(params, x) if kind == "FM" else deepfm_forward(params, x, drop_p, training)
+    if kind == "FM":
+        return fm_forward(params, x)
+    if kind == "IPNN":
+        return ipnn_forward(params, x, drop_p, training)
+    return deepfm_forward(params, x, drop_p, training)
 
 
 def bce(p: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -132,8 +170,10 @@ def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) ->
     Dropout off."""
     B, F = x.shape
     E = params["feature_embedding.weight"].detach()
-    w = params["linear.weight"].detach()
     V, K = E.shape
+    if kind == "IPNN":
+        return _ipnn_condition(params, x, y)
+    w = params["linear.weight"].detach()
     e = Fn.embedding(x, E)
     lw = Fn.embedding(x, w).detach()
     s = e.sum(dim=1)
@@ -156,6 +196,36 @@ def grad_condition(kind: str, params: dict, x: torch.Tensor, y: torch.Tensor) ->
     A_E = torch.zeros(V, K).index_add_(0, flat, terms.reshape(-1, K))
     A_w = torch.zeros(V, 1).index_add_(0, flat, g.reshape(B, 1).abs().expand(B, F).reshape(-1, 1))
     return {"feature_embedding.weight": A_E, "linear.weight": A_w}
+
+
+def _ipnn_condition(params: dict, x: torch.Tensor, y: torch.Tensor) -> dict:
+    """grad_condition for InnerPNN: dz = dL/dz per example; the condition of dcat is
+    |dz| |W2| |W1| |W0| through the ReLU masks; a slot's gradient sums its flat part and
+    sum_j dP_fj e_j, whose condition is (cond(dP_fj) + |dP_fj|) |e_j|."""
+    B, F = x.shape
+    det = {k: v.detach() for k, v in params.items()}
+    E = det["feature_embedding.weight"]
+    V, K = E.shape
+    cat = ipnn_cat(E, x)
+    h1 = Fn.relu(Fn.linear(cat, det["mlp.0.weight"], det["mlp.0.bias"]))
+    h2 = Fn.relu(Fn.linear(h1, det["mlp.3.weight"], det["mlp.3.bias"]))
+    z = Fn.linear(h2, det["mlp.6.weight"], det["mlp.6.bias"]).requires_grad_(True)
+    bce(torch.sigmoid(z), y.reshape(-1, 1).float()).backward()
+    g = z.grad.reshape(B, 1)
+    dh2 = (g * det["mlp.6.weight"]).abs() * (h2 > 0)
+    c1 = (dh2 @ det["mlp.3.weight"].abs()) * (h1 > 0)
+    ccat = c1 @ det["mlp.0.weight"].abs()                                  # [B, F*K + P]
+    d1 = (g * det["mlp.6.weight"]) * (h2 > 0)
+    dcat = (((d1 @ det["mlp.3.weight"]) * (h1 > 0)) @ det["mlp.0.weight"]).abs()
+    e = Fn.embedding(x, E).abs()                                           # [B, F, K]
+    terms = ccat[:, :F * K].reshape(B, F, K).clone()
+    row, col = ipnn_pairs(F)
+    wp = ccat[:, F * K:] + dcat[:, F * K:]                                 # [B, P]
+    for p_, (i, j) in enumerate(zip(row.tolist(), col.tolist())):
+        terms[:, i] += wp[:, p_:p_ + 1] * e[:, j]
+        terms[:, j] += wp[:, p_:p_ + 1] * e[:, i]
+    A_E = torch.zeros(V, K).index_add_(0, x.reshape(-1), terms.reshape(-1, K))
+    return {"feature_embedding.weight": A_E}
 
 
 # ------------------------------------------------------------ scatter grouping -------

@@ -50,33 +50,16 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = __builtin_fmaf(h.neg_step_size * m, __builtin_amdgcn_rcpf(denom), p);  // addcdiv_
 }
 
-// Two elements with the same operations on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 /
-// v_pk_add_f32: two IEEE results per lane per issue, each rounded exactly as adam_elem's
-// scalar op): bitwise adam_elem, at ~2/3 of its issue cycles (the square root and the
-// reciprocal have no packed form). The replay loops (flush, catch-up) are VALU-bound on this.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void adam_pair(f32x2& p, f32x2 g, f32x2& m, f32x2& v,
-                                          const AdamHP& h) {
-#pragma clang fp contract(off)
-  const f32x2 wd = h.wd, w1 = h.w1, w2 = h.w2, b2 = h.beta2, ibc = h.inv_bc2_sqrt, eps = h.eps;
-  g = __builtin_elementwise_fma(wd, p, g);
-  m = __builtin_elementwise_fma(w1, g - m, m);
-  v = __builtin_elementwise_fma(w2 * g, g, v * b2);
-  const f32x2 sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
-  const f32x2 den = __builtin_elementwise_fma(sq, ibc, eps);
-  const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-  p = __builtin_elementwise_fma(h.neg_step_size * m, rc, p);
-}
-
+// Four elements (a float4 column). Scalar ops on purpose: a packed-fp32 form
+// (v_pk_fma_f32 / v_pk_mul_f32, bitwise the same results) measured slower on MI355X — the
+// apply pass 2-4x (deferred_rows_vec<APPLY>: 7.3 -> 32.6 us at C2, 33.5 -> 59.7 us at C3)
+// and no faster on the flush (3.54 vs 3.56 ms), which is not VALU-bound.
 __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4& v,
                                          const AdamHP& h) {
-  f32x2 p0 = {p.x, p.y}, p1 = {p.z, p.w}, m0 = {m.x, m.y}, m1 = {m.z, m.w};
-  f32x2 v0 = {v.x, v.y}, v1 = {v.z, v.w};
-  adam_pair(p0, (f32x2){g.x, g.y}, m0, v0, h);
-  adam_pair(p1, (f32x2){g.z, g.w}, m1, v1, h);
-  p = make_float4(p0.x, p0.y, p1.x, p1.y);
-  m = make_float4(m0.x, m0.y, m1.x, m1.y);
-  v = make_float4(v0.x, v0.y, v1.x, v1.y);
+  adam_elem(p.x, g.x, m.x, v.x, h);
+  adam_elem(p.y, g.y, m.y, v.y, h);
+  adam_elem(p.z, g.z, m.z, v.z, h);
+  adam_elem(p.w, g.w, m.w, v.w, h);
 }
 
 // ------------------------------------------------------------------ dense -----------

@@ -479,6 +479,41 @@ def feature_embedding(idx: torch.Tensor, emb: torch.Tensor, err_flag=None) -> to
     return out
 
 
+def ipnn_forward(idx: torch.Tensor, emb: torch.Tensor, out: torch.Tensor | None = None,
+                 err_flag=None) -> torch.Tensor:
+    """InnerPNN MLP input [B, F*K + F(F-1)/2]: flat embeddings, then the pairwise inner
+    products in row-major pair order (p_model.py:187-195)."""
+    idx, it = _idx(idx)
+    _f32(emb, "feature_embedding.weight")
+    B, F = idx.shape
+    V, K = emb.shape
+    W = F * K + F * (F - 1) // 2
+    if out is None:
+        out = torch.empty(B, W, dtype=torch.float32, device=emb.device)
+    elif out.dtype != torch.float32 or out.shape[0] < B or out.shape[1] < W or out.stride(1) != 1:
+        raise ValueError(f"ipnn_forward: out must be float32 [>= {B}, >= {W}], unit column stride")
+    lib.ctr_ipnn_forward(_p(idx), it, B, F, K, V, _p(emb), _p(out), out.stride(0), _p(err_flag),
+                         _stream())
+    return out
+
+
+def ipnn_backward(idx: torch.Tensor, emb: torch.Tensor, dcat: torch.Tensor,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-slot embedding gradients [B*F, K] (slot order) from dL/dcat."""
+    idx, it = _idx(idx)
+    _f32(emb, "feature_embedding.weight")
+    _f32(dcat, "dcat")
+    B, F = idx.shape
+    V, K = emb.shape
+    if dcat.shape[0] < B or dcat.shape[1] < F * K + F * (F - 1) // 2 or dcat.stride(1) != 1:
+        raise ValueError("ipnn_backward: dcat must be [B, F*K + F(F-1)/2]")
+    if out is None:
+        out = torch.empty(B * F, K, dtype=torch.float32, device=emb.device)
+    lib.ctr_ipnn_backward(_p(idx), it, B, F, K, V, _p(emb), _p(dcat), dcat.stride(0), _p(out),
+                          _stream())
+    return out
+
+
 # ----------------------------------------------------------------------- REINFORCE ----
 def softmax_rows(x: torch.Tensor) -> torch.Tensor:
     _f32(x, "x")

@@ -1,6 +1,6 @@
-"""FM and DeepFM with the reference's construction API, on the HIP kernels.
+"""FM, DeepFM and InnerPNN with the reference's construction API, on the HIP kernels.
 
-Drop-in for ``src/models/p_model.py`` (FM 28-57, DeepFM 256-324): identical constructor
+Drop-in for ``src/models/p_model.py`` (FM 28-57, InnerPNN 146-200, DeepFM 256-324): identical constructor
 signatures, submodules created in the same order (so ``torch.manual_seed(s)`` gives the
 same initial weights as the reference) and identical state_dict keys, so the RL drivers'
 ``torch.load('...FMbest.pth')`` / ``load_state_dict`` and ``Feature_Embedding.load_embedding``
@@ -84,6 +84,28 @@ class _LinearAct(torch.autograd.Function):
         dw = hip_ops.gemm(g, x.contiguous(), trans_a=True) if ctx.needs_input_grad[1] else None
         db = hip_ops.colsum(g) if ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None
+
+
+class _IPNNPart(torch.autograd.Function):
+    """cat = flat(E[x]) ++ pairwise inner products (p_model.py:187-195). Backward: the
+    per-slot gradients (ctr_ipnn_backward), summed per row in slot order (deterministic),
+    returned dense like embedding_dense_backward."""
+
+    @staticmethod
+    def forward(ctx, x, emb):
+        ctx.save_for_backward(x, emb)
+        return hip_ops.ipnn_forward(x, emb)
+
+    @staticmethod
+    def backward(ctx, gcat):
+        x, emb = ctx.saved_tensors
+        B, F = x.shape
+        V, K = emb.shape
+        dslot = hip_ops.ipnn_backward(x, emb, gcat.contiguous())
+        plan = hip_ops.SparsePlanBuffers(B * F, emb.device).build(x, V)
+        grad_rows, _ = hip_ops.segment_sum_rows(plan, dslot)
+        g_emb, _ = hip_ops.rows_to_dense(plan, V, grad_rows)
+        return None, g_emb
 
 
 def _fm_part(x, emb, lin, bias, want_emb):
@@ -171,4 +193,49 @@ class DeepFM(nn.Module):
             h = hip_ops.linear(h, m[3].weight, m[3].bias, relu=True, drop_p=p1,
                                seed=_dropout_seed())
             head = hip_ops.deepfm_head(h, m[6].weight, m[6].bias, r.z)
+            return head["p"].view(-1, 1)
+
+
+class InnerPNN(nn.Module):
+    """p_model.py:146-200: MLP [F*K + F(F-1)/2 -> 300 -> 200 -> 1] (ReLU, Dropout 0.2) over
+    the flat embeddings and their pairwise inner products; no linear term, no bias."""
+
+    def __init__(self, feature_nums, field_nums, latent_dims, output_dim=1):
+        super().__init__()
+        latent_dims = int(latent_dims)
+        self.feature_nums = feature_nums
+        self.field_nums = field_nums
+        self.latent_dims = latent_dims
+        self.feature_embedding = nn.Embedding(self.feature_nums, self.latent_dims)
+        deep_input_dims = self.field_nums * self.latent_dims + self.field_nums * (self.field_nums - 1) // 2
+        layers = []
+        for neuron_num in (300, 200):
+            layers.append(nn.Linear(deep_input_dims, neuron_num))
+            layers.append(nn.ReLU())
+            layers.append(nn.Dropout(p=0.2))
+            deep_input_dims = neuron_num
+        layers.append(nn.Linear(deep_input_dims, 1))
+        self.mlp = nn.Sequential(*layers)
+        # the reference's pair lists (p_model.py:179-182), kept for API parity
+        self.row, self.col = [], []
+        for i in range(self.field_nums - 1):
+            for j in range(i + 1, self.field_nums):
+                self.row.append(i), self.col.append(j)
+
+    def forward(self, x):
+        E = self.feature_embedding.weight
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            cat = _IPNNPart.apply(x, E)
+            return torch.sigmoid(mlp_forward(self.mlp, cat, self.training))
+        with torch.no_grad():
+            h = hip_ops.ipnn_forward(x, E.detach())
+            m = self.mlp
+            p0 = m[2].p if self.training else 0.0
+            p1 = m[5].p if self.training else 0.0
+            h = hip_ops.linear(h, m[0].weight, m[0].bias, relu=True, drop_p=p0,
+                               seed=_dropout_seed())
+            h = hip_ops.linear(h, m[3].weight, m[3].bias, relu=True, drop_p=p1,
+                               seed=_dropout_seed())
+            zero = torch.zeros(h.shape[0], dtype=torch.float32, device=h.device)
+            head = hip_ops.deepfm_head(h, m[6].weight, m[6].bias, zero)
             return head["p"].view(-1, 1)

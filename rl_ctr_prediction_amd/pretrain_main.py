@@ -8,8 +8,8 @@ out), same semantics: batches in file order (no shuffle), Adam re-created every 
 AUC over the concatenated test predictions, loss-/AUC-based early stopping with reload
 of the checkpoint four epochs back.
 
-Differences, all deliberate: the training step is the fused HIP step (FM and DeepFM;
-the other eight model families are out of scope); the batches are
+Differences, all deliberate: the training step is the fused HIP step (FM, DeepFM and
+IPNN; the other seven model families are out of scope); the batches are
 sliced from one device-resident copy of the data instead of 8 DataLoader worker
 processes; the rotating-checkpoint cleanup skips files that were never written (the
 reference crashes there when epoch < 5, all_main/pretrain_main.py:201-202).
@@ -45,9 +45,11 @@ def get_model(model_name, feature_nums, field_nums, latent_dims):
         return Model.FM(feature_nums, latent_dims)
     if model_name == "DeepFM":
         return Model.DeepFM(feature_nums, field_nums, latent_dims)
+    if model_name == "IPNN":
+        return Model.InnerPNN(feature_nums, field_nums, latent_dims)
     raise NotImplementedError(
-        f"{model_name}: only FM and DeepFM (the north-star hot path) are built on HIP; "
-        "LR/FFM/W&D/FNN/IPNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
+        f"{model_name}: FM, DeepFM and IPNN are built on HIP; "
+        "LR/FFM/W&D/FNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
 
 
 def get_dataset(datapath, dataset_name, campaign_id):
@@ -200,7 +202,7 @@ def _parser():
     parser.add_argument("--data_path", default="../../data/")
     parser.add_argument("--dataset_name", default="avazu/", help="ipinyou, cretio, yoyi, avazu")
     parser.add_argument("--campaign_id", default="avazu/", help="1458, 3358, 3386, 3427, 3476, avazu")
-    parser.add_argument("--model_name", default="FM", help="FM, DeepFM")
+    parser.add_argument("--model_name", default="FM", help="FM, DeepFM, IPNN")
     parser.add_argument("--latent_dims", type=int, default=10)
     parser.add_argument("--epoch", type=int, default=20)
     parser.add_argument("--learning_rate", type=float, default=1e-3)

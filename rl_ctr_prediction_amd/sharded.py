@@ -42,6 +42,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None):
+        if not hasattr(model, "linear"):
+            raise NotImplementedError("row sharding drives FM / DeepFM; train InnerPNN with "
+                                      "FusedCTRTrainer (replicated tables)")
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:

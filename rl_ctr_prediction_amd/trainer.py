@@ -33,7 +33,7 @@ import torch.nn as nn
 
 from . import hip_ops
 from .distributed import allgather_sparse_rows, allreduce_sum_, world
-from .p_model import FM, DeepFM
+from .p_model import FM, DeepFM, InnerPNN
 
 
 class _nullctx:
@@ -46,6 +46,8 @@ class _nullctx:
 DEEPFM_DENSE = ("bias", "mlp.0.weight", "mlp.0.bias", "mlp.3.weight", "mlp.3.bias",
                 "mlp.6.weight", "mlp.6.bias")
 FM_DENSE = ("bias",)
+IPNN_DENSE = DEEPFM_DENSE[1:]  # InnerPNN: the MLP only (no linear term, no bias)
+_MLP_KINDS = ("DeepFM", "IPNN")
 
 
 @dataclass
@@ -64,6 +66,8 @@ class _Bufs:
     gplan: hip_ops.SparsePlanBuffers | None = None
     g_rows: torch.Tensor | None = None
     g_lin: torch.Tensor | None = None
+    dslot: torch.Tensor | None = None  # IPNN: per-slot embedding gradients [S, K]
+    zero: torch.Tensor | None = None   # IPNN: the (absent) FM logit, zeros [B]
 
 
 class FusedCTRTrainer:
@@ -78,10 +82,11 @@ class FusedCTRTrainer:
     def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 0.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, process_group=None, seed: int | None = None,
                  optimizer_mode: str = "deferred"):
-        if not isinstance(model, (FM, DeepFM)):
-            raise TypeError("FusedCTRTrainer drives FM or DeepFM")
+        if not isinstance(model, (FM, DeepFM, InnerPNN)):
+            raise TypeError("FusedCTRTrainer drives FM, DeepFM or InnerPNN")
         self.model = model
-        self.kind = "DeepFM" if isinstance(model, DeepFM) else "FM"
+        self.kind = ("DeepFM" if isinstance(model, DeepFM) else
+                     "IPNN" if isinstance(model, InnerPNN) else "FM")
         self.lr, self.weight_decay, self.betas, self.eps = float(lr), float(weight_decay), betas, eps
         self.group = process_group
         E = model.feature_embedding.weight
@@ -90,7 +95,7 @@ class FusedCTRTrainer:
             raise RuntimeError("FusedCTRTrainer needs the model on a ROCm device")
         self.V, self.K = E.shape
         named = dict(model.named_parameters())
-        self.dense_names = DEEPFM_DENSE if self.kind == "DeepFM" else FM_DENSE
+        self.dense_names = {"DeepFM": DEEPFM_DENSE, "FM": FM_DENSE, "IPNN": IPNN_DENSE}[self.kind]
         # 16-B aligned views (offsets multiples of 4 floats): the GEMMs read the weights
         # through the float4 / LDS-DMA path only when a row start is 16-B aligned
         self.offsets, total = {}, 0
@@ -115,11 +120,14 @@ class FusedCTRTrainer:
         self.row_lo, self.row_hi = self._table_rows()
         self.V_tab = self.row_hi - self.row_lo
         self.E_tab = E.data[self.row_lo:self.row_hi]
-        self.w_tab = model.linear.weight.data[self.row_lo:self.row_hi]
         self.m_E = torch.zeros_like(self.E_tab)
         self.v_E = torch.zeros_like(self.E_tab)
-        self.m_w = torch.zeros(self.V_tab, dtype=torch.float32, device=self.device)
-        self.v_w = torch.zeros_like(self.m_w)
+        if self.kind == "IPNN":  # no linear table: every lin pointer of the ABI is NULL
+            self.w_tab = self.m_w = self.v_w = None
+        else:
+            self.w_tab = model.linear.weight.data[self.row_lo:self.row_hi]
+            self.m_w = torch.zeros(self.V_tab, dtype=torch.float32, device=self.device)
+            self.v_w = torch.zeros_like(self.m_w)
         if optimizer_mode not in ("deferred", "dense"):
             raise ValueError(f"optimizer_mode must be 'deferred' or 'dense', not {optimizer_mode!r}")
         self.deferred = optimizer_mode == "deferred"
@@ -136,7 +144,8 @@ class FusedCTRTrainer:
         self.sweep_slices = 0
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
-        self._wgrad_stream = torch.cuda.Stream(device=self.device) if self.kind == "DeepFM" else None
+        self._wgrad_stream = (torch.cuda.Stream(device=self.device) if self.kind in _MLP_KINDS
+                              else None)
         self._sweep_stream = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
@@ -211,7 +220,8 @@ class FusedCTRTrainer:
         (all_main/pretrain_main.py:153): fresh moments, step 0."""
         self.flush()
         for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
-            t.zero_()
+            if t is not None:
+                t.zero_()
         self.last.zero_()
         self.step_ctr.zero_()
         self.step_count = 0
@@ -223,7 +233,8 @@ class FusedCTRTrainer:
         m = {n: v for n, v in zip(self.dense_names, self._split(self.m_flat))}
         v = {n: v for n, v in zip(self.dense_names, self._split(self.v_flat))}
         m["feature_embedding.weight"], v["feature_embedding.weight"] = self.m_E, self.v_E
-        m["linear.weight"], v["linear.weight"] = self.m_w.view(-1, 1), self.v_w.view(-1, 1)
+        if self.m_w is not None:
+            m["linear.weight"], v["linear.weight"] = self.m_w.view(-1, 1), self.v_w.view(-1, 1)
         state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": m[n].clone(),
                      "exp_avg_sq": v[n].clone()} for i, (n, _) in enumerate(named)}
         return {"state": state if self.step_count else {},
@@ -248,8 +259,9 @@ class FusedCTRTrainer:
             return b
         dev, K = self.device, self.K
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
-        deep = self.kind == "DeepFM"
-        fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, F * K) if deep else None,
+        deep = self.kind in _MLP_KINDS
+        W = F * K + (F * (F - 1) // 2 if self.kind == "IPNN" else 0)  # MLP input width
+        fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, W) if deep else None,
                                p=None, loss_elem=e(B), gz=e(B))
         S = B * F
         b = _Bufs(B=B, fm=fm, plan=hip_ops.SparsePlanBuffers(S, dev), grad_rows=e(S, K),
@@ -257,7 +269,10 @@ class FusedCTRTrainer:
         if deep:
             mlp = self.model.mlp
             H1, H2 = mlp[0].out_features, mlp[3].out_features
-            b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, F * K)
+            b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, W)
+            if self.kind == "IPNN":
+                b.dslot = e(S, K)
+                b.zero = torch.zeros(B, dtype=torch.float32, device=dev)
             b.head = dict(z=e(B), p=e(B), loss_elem=fm.loss_elem, gz=fm.gz, dh_pre=e(B, H2))
         rank, ws = world()
         if ws > 1:
@@ -333,7 +348,8 @@ class FusedCTRTrainer:
             y = y.float()
         y = y.contiguous()
         m = self.model
-        E, w, bias = m.feature_embedding.weight.data, m.linear.weight.data, self.views["bias"]
+        E, bias = m.feature_embedding.weight.data, self.views.get("bias")
+        w = m.linear.weight.data if self.kind != "IPNN" else None
         gv = self.grad_views
         step_hint = self.step_count + 1
         if self._side is not None:
@@ -372,16 +388,20 @@ class FusedCTRTrainer:
             gz = b.fm.gz
         else:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
-        hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        if bias is not None:
+            hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         if self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)  # the plan
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
-        hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
-                                  grad_rows=b.grad_rows, grad_lin=b.grad_lin)
+        if self.kind == "IPNN":
+            hip_ops.segment_sum_rows(b.plan, b.dslot, rowmap=sparse_rowmap, out=b.grad_rows)
+        else:
+            hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
+                                      grad_rows=b.grad_rows, grad_lin=b.grad_lin)
         self._span("scatter", t)
         hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
-        grad_rows, grad_lin, plan = b.grad_rows, b.grad_lin, b.plan
+        grad_rows, grad_lin, plan = b.grad_rows, (b.grad_lin if w is not None else None), b.plan
         if ws > 1:
             self._join_wgrad()  # the exchange all-reduces the dense gradient
             grad_rows, grad_lin = self._exchange(b)
@@ -433,15 +453,19 @@ class FusedCTRTrainer:
         # dropout stream of this step: (completed steps) << 32 is added on the device
         off = 0
         t = self._mark("gather")
-        fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
-                                err_flag=self.err, out=b.fm)
+        if self.kind == "IPNN":  # cat = flat(E[x]) ++ pairwise inner products
+            X = hip_ops.ipnn_forward(x, E, out=b.fm.emb_out, err_flag=self.err)
+            z_fm = b.zero
+        else:
+            fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
+                                    err_flag=self.err, out=b.fm)
+            X, z_fm = fm.emb_out, fm.z
         self._span("gather", t)
-        X = fm.emb_out
         self._linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
                      seed=self.seed, offset=off, step_dev=self.step_done, out=b.h1)
         self._linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
                      seed=self.seed, offset=off + B * H1, step_dev=self.step_done, out=b.h2)
-        head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], fm.z, y,
+        head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], z_fm, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
@@ -449,6 +473,8 @@ class FusedCTRTrainer:
                    scale=1.0 / (1.0 - p0), out=b.dh1)
         # Linear(F*K,300): dX = dH1 @ W0, the MLP-input gradient the scatter needs
         self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
+        if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
+            hip_ops.ipnn_backward(x, E, b.dx, out=b.dslot)
         # the weight / bias gradients are needed only by the dense Adam at the end of the
         # step: on the side stream they run under the scatter and the embedding Adam
         side = self._wgrad_stream
@@ -468,7 +494,7 @@ class FusedCTRTrainer:
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""
-        if self._wgrad_stream is not None and self.kind == "DeepFM":
+        if self._wgrad_stream is not None:
             torch.cuda.current_stream().wait_stream(self._wgrad_stream)
 
     def _exchange(self, b: _Bufs):

@@ -5,11 +5,14 @@ runs it on CPU to produce small input/output fixtures in this directory. The fix
 data: inputs, initial parameters and the reference's outputs. The GPU box never sees the
 reference; tests there compare against these files.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [fixture ...]
+
+(no argument: every fixture; else only the named ones, e.g. `ipnn`)
 
 Fixtures:
   g_fm.npz       FM fwd/bwd + 2 Adam steps (std 0.1 init) and an N(0,1) saturated case
   g_deepfm.npz   DeepFM fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
+  g_ipnn.npz     InnerPNN fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
   g_bce.npz      sigmoid + BCELoss values and d/dz incl. saturated logits
   g_fe.npz       Feature_Embedding forward
   g_pg.npz       PolicyGradient: discount_and_norm_rewards, loss_func (+ grads), choose_action
@@ -142,6 +145,49 @@ def gen_deepfm(P):
         for k in DEEPFM_KEYS:
             out[f"step{s + 1}/{k}"] = _np(sd[k])
     np.savez(HERE / "g_deepfm.npz", **out)
+
+
+IPNN_KEYS = ["feature_embedding.weight", "mlp.0.weight", "mlp.0.bias", "mlp.3.weight",
+             "mlp.3.bias", "mlp.6.weight", "mlp.6.bias"]
+
+
+def gen_ipnn(P):
+    """InnerPNN (p_model.py:146-200): same protocol as gen_deepfm; std 0.1 embeddings."""
+    out = {}
+    V, F, K, B = 500, 8, 16, 64
+    torch.manual_seed(0)
+    m = P.InnerPNN(V, F, K)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    with torch.no_grad():
+        m.feature_embedding.weight.normal_(0, 0.1)
+    sd = m.state_dict()
+    for k in IPNN_KEYS:
+        out[f"init/{k}"] = _np(sd[k])
+    g = torch.Generator().manual_seed(3)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    crit = torch.nn.BCELoss()
+    m.train()
+    for s in range(2):
+        x = _hot_ids(g, B, F, V)
+        y = (torch.rand(B, 1, generator=g) < 0.3).float()
+        p = m(x)
+        loss = crit(p, y)
+        m.zero_grad()
+        loss.backward()
+        out[f"x{s}"] = _np(x)
+        out[f"y{s}"] = _np(y)
+        out[f"p{s}"] = _np(p)
+        out[f"loss{s}"] = np.float32(loss.item())
+        named = dict(m.named_parameters())
+        for k in IPNN_KEYS:
+            out[f"grad{s}/{k}"] = _np(named[k].grad)
+        opt.step()
+        sd = m.state_dict()
+        for k in IPNN_KEYS:
+            out[f"step{s + 1}/{k}"] = _np(sd[k])
+    np.savez(HERE / "g_ipnn.npz", **out)
 
 
 def gen_bce():
@@ -289,12 +335,11 @@ def gen_toy(P, PM):
 def main():
     P, FE, PG, PM = _import_reference()
     torch.set_num_threads(4)
-    gen_fm(P)
-    gen_deepfm(P)
-    gen_bce()
-    gen_fe(FE)
-    gen_pg(PG)
-    gen_toy(P, PM)
+    gens = {"fm": lambda: gen_fm(P), "deepfm": lambda: gen_deepfm(P), "ipnn": lambda: gen_ipnn(P),
+            "bce": gen_bce, "fe": lambda: gen_fe(FE), "pg": lambda: gen_pg(PG),
+            "toy": lambda: gen_toy(P, PM)}
+    for name in (sys.argv[1:] or list(gens)):
+        gens[name]()
     (HERE / "manifest.json").write_text(json.dumps({
         "generator": "tests/golden/make_golden.py",
         "reference": "jqsl2012/RL_CTR_Prediction @ /root/reference (imported, CPU)",

@@ -349,6 +349,39 @@ def test_feature_embedding_vs_oracle(cuda, F, K):
     np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5 * K)
 
 
+# ------------------------------------------------------------------- IPNN (§8f) ------
+@pytest.mark.parametrize("F,K,B", [(2, 1, 3), (8, 16, 64), (26, 64, 300), (22, 128, 50),
+                                   (5, 3, 7), (39, 10, 100)])
+def test_ipnn_forward_and_backward_vs_oracle(cuda, F, K, B):
+    """cat = flat(E[x]) ++ pair dots (p_model.py:187-195) and the per-slot gradient
+    through it, against the oracle's torch-CPU ops (autograd for the backward). Flat part
+    bit-exact; dots and gradients within 1e-5 of their L1 scale (sum of |terms|)."""
+    H = _hip()
+    g = torch.Generator().manual_seed(F * K + B)
+    V = 300
+    E = torch.randn(V, K, generator=g)
+    x = torch.randint(0, V, (B, F), generator=g)
+    x[:, 0] = x[:, 1 % F]  # a repeated id inside an example
+    cat = H.ipnn_forward(x.to(cuda), E.to(cuda)).cpu()
+    ref = O.ipnn_cat(E.double(), x)
+    np.testing.assert_array_equal(cat[:, :F * K].numpy(), ref[:, :F * K].float().numpy())
+    scale = O.ipnn_cat(E.double().abs(), x)
+    assert ((cat.double() - ref).abs() <= 1e-5 * scale + 1e-30).all()
+    dcat = torch.randn(B, F * K + F * (F - 1) // 2, generator=g)
+    e = torch.nn.functional.embedding(x, E.double()).requires_grad_(True)
+    row, col = O.ipnn_pairs(F)
+    out = torch.cat([e.reshape(B, -1), (e[:, row] * e[:, col]).sum(2)], 1)
+    out.backward(dcat.double())
+    ds = H.ipnn_backward(x.to(cuda), E.to(cuda), dcat.to(cuda)).cpu().double().view(B, F, K)
+    ea = e.detach().abs()
+    pa = dcat.double().abs()[:, F * K:]
+    bound = dcat.double().abs()[:, :F * K].reshape(B, F, K).clone()
+    for p_, (i, j) in enumerate(zip(row.tolist(), col.tolist())):
+        bound[:, i] += pa[:, p_:p_ + 1] * ea[:, j]
+        bound[:, j] += pa[:, p_:p_ + 1] * ea[:, i]
+    assert ((ds - e.grad).abs() <= 1e-5 * bound + 1e-30).all()
+
+
 # ------------------------------------------------------------------------ REINFORCE ---
 def test_pg_discount_norm_vs_golden(cuda, golden):
     H = _hip()

@@ -30,11 +30,14 @@ def _fused_grads(tr):
     U = b.plan.num_unique_host()
     rows = b.plan.unique_rows[:U].long()
     gE = torch.zeros(tr.V, tr.K, device=tr.device)
-    gw = torch.zeros(tr.V, 1, device=tr.device)
     gE[rows] = b.grad_rows[:U]
-    gw[rows, 0] = b.grad_lin[:U]
+    gw = None
+    if tr.w_tab is not None:
+        gw = torch.zeros(tr.V, 1, device=tr.device)
+        gw[rows, 0] = b.grad_lin[:U]
+        gw = gw.cpu().numpy()
     dense = {n: v.detach().cpu().numpy() for n, v in tr.grad_views.items()}
-    return gE.cpu().numpy(), gw.cpu().numpy(), dense
+    return gE.cpu().numpy(), gw, dense
 
 
 def _fm_from_golden(g, tag, dev):
@@ -297,6 +300,58 @@ def test_pg_learn_matches_autograd(cuda):
     assert pg.ep_states.numel() == 0
 
 
+def _ipnn_from_golden(g, dev):
+    P = _pkg()
+    V, K = g["init/feature_embedding.weight"].shape
+    W = g["init/mlp.0.weight"].shape[1]
+    F = next(f for f in range(2, 200) if f * K + f * (f - 1) // 2 == W)
+    m = P.InnerPNN(V, F, K).to(dev)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    m.load_state_dict({k: torch.tensor(g[f"init/{k}"]) for k in O.IPNN_KEYS})
+    return m
+
+
+def test_fused_ipnn_two_steps_vs_reference(cuda, golden):
+    """InnerPNN (§8f rank 1) through the fused step: loss, every gradient, two Adam steps."""
+    P = _pkg()
+    g = golden("g_ipnn.npz")
+    m = _ipnn_from_golden(g, cuda)
+    tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
+    for s in range(2):
+        loss = tr.step(torch.tensor(g[f"x{s}"], device=cuda), torch.tensor(g[f"y{s}"], device=cuda))
+        assert loss.item() == pytest.approx(float(g[f"loss{s}"]), rel=1e-5)
+        gE, gw, dense = _fused_grads(tr)
+        assert gw is None
+        assert_grad_close(gE, g[f"grad{s}/feature_embedding.weight"], err_msg="grad E")
+        for k, v in dense.items():
+            assert_grad_close(v, g[f"grad{s}/{k}"], err_msg=f"grad {k}")
+        sd = m.state_dict()
+        for k in O.IPNN_KEYS:
+            assert_adam_close(sd[k].cpu().numpy(), g[f"step{s + 1}/{k}"], 1e-3, err_msg=k)
+
+
+def test_autograd_ipnn_grads_vs_reference(cuda, golden):
+    g = golden("g_ipnn.npz")
+    m = _ipnn_from_golden(g, cuda)
+    m.train()
+    x, y = torch.tensor(g["x0"], device=cuda), torch.tensor(g["y0"], device=cuda)
+    p = m(x)
+    np.testing.assert_allclose(p.detach().cpu().numpy(), g["p0"], rtol=1e-5, atol=1e-7)
+    loss = torch.nn.BCELoss()(p, y)
+    m.zero_grad()
+    loss.backward()
+    named = dict(m.named_parameters())
+    for k in O.IPNN_KEYS:
+        ref = g[f"grad0/{k}"]
+        np.testing.assert_allclose(named[k].grad.cpu().numpy(), ref, rtol=1e-5,
+                                   atol=1e-6 * max(np.abs(ref).max(), 1e-12), err_msg=k)
+    with torch.no_grad():  # eval path (no autograd) = the same forward
+        m.eval()
+        np.testing.assert_allclose(m(x).cpu().numpy(), g["p0"], rtol=1e-5, atol=1e-7)
+
+
 def test_fused_step_is_deterministic(cuda):
     """Two trainers from the same state on the same batches end bitwise identical (no
     float atomics anywhere: what keeps data-parallel replicas in lockstep)."""
@@ -319,7 +374,8 @@ def test_fused_step_is_deterministic(cuda):
 
 # ------------------------------------------------------------ full BASELINE sizes ----
 @pytest.mark.parametrize("kind,V,K,B", [("FM", 1_000_000, 16, 4096),
-                                        ("DeepFM", 10_000_000, 64, 8192)])
+                                        ("DeepFM", 10_000_000, 64, 8192),
+                                        ("IPNN", 1_000_000, 16, 4096)])
 def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     """C2 / C3 at full size: one fused step against the CPU oracle on the same synthetic
     batch (dropout off), compared on the loss, the touched rows and a sample of the
@@ -329,14 +385,16 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     F = 26
     torch.manual_seed(5)
     with torch.device(cuda):
-        m = P.FM(V, K) if kind == "FM" else P.DeepFM(V, F, K)
-    if kind == "DeepFM":
+        m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
+             "IPNN": lambda: P.InnerPNN(V, F, K)}[kind]()
+    if kind != "FM":
         for mod in m.modules():
             if isinstance(mod, torch.nn.Dropout):
                 mod.p = 0.0
     with torch.no_grad():
         m.feature_embedding.weight.mul_(0.05)
-        m.linear.weight.mul_(0.05)
+        if kind != "IPNN":
+            m.linear.weight.mul_(0.05)
     params_cpu = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
     x, y = next(CriteoSynth(V, F, seed=9).batches(1, B))
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -352,8 +410,9 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     assert_grad_close(gE, params_cpu["feature_embedding.weight"].grad.numpy(),
                       cond=cond["feature_embedding.weight"].numpy(), n_terms=n_terms,
                       err_msg="grad E")
-    assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(),
-                      cond=cond["linear.weight"].numpy(), n_terms=n_terms, err_msg="grad w")
+    if gw is not None:
+        assert_grad_close(gw, params_cpu["linear.weight"].grad.numpy(),
+                          cond=cond["linear.weight"].numpy(), n_terms=n_terms, err_msg="grad w")
     for k, v in dense.items():
         assert_grad_close(v, params_cpu[k].grad.numpy(), err_msg=f"grad {k}")
     E = m.feature_embedding.weight.detach()
@@ -363,9 +422,10 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B):
     sample = np.unique(np.concatenate([rows, rng.integers(0, V, 20000), [0, V - 1]]))
     idx = torch.tensor(sample)
     assert_adam_close(E[idx.to(cuda)].cpu().numpy(), Er[idx].numpy(), 1e-3, err_msg="E")
-    w, wr = m.linear.weight.detach(), params_cpu["linear.weight"].detach()
-    assert_adam_close(w[idx.to(cuda)].cpu().numpy(), wr[idx].numpy(), 1e-3, err_msg="w")
-    if kind == "DeepFM":
+    if kind != "IPNN":
+        w, wr = m.linear.weight.detach(), params_cpu["linear.weight"].detach()
+        assert_adam_close(w[idx.to(cuda)].cpu().numpy(), wr[idx].numpy(), 1e-3, err_msg="w")
+    if kind != "FM":
         sd = m.state_dict()
         for k in ("mlp.0.weight", "mlp.3.weight", "mlp.6.weight", "mlp.0.bias"):
             assert_adam_close(sd[k].cpu().numpy(), params_cpu[k].detach().numpy(), 1e-3, err_msg=k)

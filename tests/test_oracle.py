@@ -55,6 +55,35 @@ def test_deepfm_matches_reference(golden):
                                        rtol=1e-6, atol=1e-8, err_msg=k)
 
 
+def test_ipnn_matches_reference(golden):
+    """InnerPNN (p_model.py:146-200): forward, every gradient and two Adam steps."""
+    g = golden("g_ipnn.npz")
+    params = {k: torch.tensor(g[f"init/{k}"]).clone().requires_grad_(True) for k in O.IPNN_KEYS}
+    opt = O.make_optimizer(params, 1e-3, 1e-5)
+    for s in range(2):
+        x, y = torch.tensor(g[f"x{s}"]), torch.tensor(g[f"y{s}"])
+        loss, p, gr = O.grads("IPNN", params, x, y, drop_p=0.0)
+        np.testing.assert_allclose(p.numpy(), g[f"p{s}"], rtol=1e-6, atol=0)
+        assert loss == pytest.approx(float(g[f"loss{s}"]), rel=1e-6)
+        for k in O.IPNN_KEYS:
+            np.testing.assert_allclose(gr[k].numpy(), g[f"grad{s}/{k}"], rtol=1e-5, atol=1e-9,
+                                       err_msg=k)
+        opt.step()
+        for k in O.IPNN_KEYS:
+            np.testing.assert_allclose(params[k].detach().numpy(), g[f"step{s + 1}/{k}"],
+                                       rtol=1e-6, atol=1e-8, err_msg=k)
+
+
+def test_ipnn_condition_bounds_the_reference_gradient(golden):
+    """The parity scale of the IPNN embedding gradient dominates the gradient itself."""
+    g = golden("g_ipnn.npz")
+    params = {k: torch.tensor(g[f"init/{k}"]).clone().requires_grad_(True) for k in O.IPNN_KEYS}
+    x, y = torch.tensor(g["x0"]), torch.tensor(g["y0"])
+    c = O.grad_condition("IPNN", params, x, y)["feature_embedding.weight"].numpy()
+    gE = g["grad0/feature_embedding.weight"]
+    assert (np.abs(gE) <= c * (1 + 1e-5) + 1e-30).all()
+
+
 def test_bce_formula_matches_reference(golden):
     """The unfused BCE∘sigmoid gradient the kernels implement, in ATen's op order."""
     g = golden("g_bce.npz")
