@@ -294,6 +294,18 @@ int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int 
                                   int64_t V, const float* emb, float* out, int32_t* err_flag,
                                   ctr_stream_t stream);
 
+/* ------------------------------------------ §8f: binary on-disk batches (host) -----
+ * ctr_csv_to_bin: the reference's encoded CSV (`label,idx_1..idx_F` per line,
+ *   src/encode/data_.py:85; parsed by pd.read_csv at all_main/pretrain_main.py:50-53) ->
+ *   a "CTRBIN01" file: 64-byte header (rows, cols = 1+F, max feature id) + int32
+ *   [rows][cols] (label, ids), memory-mappable. Streams in constant memory; ragged rows
+ *   or non-integer fields fail with the line number. Host code, no GPU needed.
+ * ctr_bin_info: header fields of such a file (validates magic and size). */
+int ctr_csv_to_bin(const char* csv_path, const char* bin_path, int64_t* rows, int32_t* cols,
+                   int64_t* max_id);
+int ctr_bin_info(const char* bin_path, int64_t* rows, int32_t* cols, int64_t* max_id,
+                 int64_t* data_offset);
+
 /* ------------------------------------------------ §8f: IPNN (InnerPNN) --------------
  * ctr_ipnn_forward: cat[b] = flat(E[x_b]) (F*K) ++ [ <E[x_bi],E[x_bj]> for i<j, row-major ]
  *   (P = F(F-1)/2), cat is [B, >= F*K + P] with row stride ldc: the MLP input of

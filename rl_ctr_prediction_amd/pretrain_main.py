@@ -28,6 +28,7 @@ import torch.nn as nn
 from sklearn.metrics import roc_auc_score
 
 from . import creat_data as Data
+from .binfmt import load_encoded
 from . import p_model as Model
 from .trainer import FusedCTRTrainer
 
@@ -52,10 +53,17 @@ def get_model(model_name, feature_nums, field_nums, latent_dims):
         "LR/FFM/W&D/FNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
 
 
-def get_dataset(datapath, dataset_name, campaign_id):
+def get_dataset(datapath, dataset_name, campaign_id, binary=True):
+    """binary: read train_/test_ through their CTRBIN01 sidecars (rl_ctr_prediction_amd.binfmt:
+    converted once by the native parser, memory-mapped afterwards) instead of pd.read_csv —
+    the same integer matrix."""
     data_path = datapath + dataset_name + campaign_id
-    train_fm = pd.read_csv(data_path + "train_.txt", header=None).values.astype(int)
-    test_fm = pd.read_csv(data_path + "test_.txt", header=None).values.astype(int)
+    if binary:
+        train_fm = load_encoded(data_path + "train_.txt")
+        test_fm = load_encoded(data_path + "test_.txt")
+    else:
+        train_fm = pd.read_csv(data_path + "train_.txt", header=None).values.astype(int)
+        test_fm = pd.read_csv(data_path + "test_.txt", header=None).values.astype(int)
     field_nums = len(train_fm[0, 1:])
     feature_index = pd.read_csv(data_path + "featindex.txt", header=None).values
     feature_nums = int(feature_index[-1, 0].split("\t")[1]) + 1
