@@ -306,6 +306,19 @@ int ctr_csv_to_bin(const char* csv_path, const char* bin_path, int64_t* rows, in
 int ctr_bin_info(const char* bin_path, int64_t* rows, int32_t* cols, int64_t* max_id,
                  int64_t* data_offset);
 
+/* ------------------------------------- §8f: ensemble prediction + sign reward -------
+ * generate_preds of the RL drivers (hybrid_td3_main_per_v10.py:54-164): preds [B, M] (row
+ * stride ld_preds; the M pretrained models' pCTRs), actions [B] (ensemble size, 1-based),
+ * prob_weights / c_actions [B, M], labels [B] (0/1) -> y_preds [B], rewards [B],
+ * return_c_actions [B, M]; M <= 32. Keeps the reference's indexing of the sorted
+ * c_actions by the example's ordinal within its action group (line 127). rank_ws:
+ * int32[B] scratch. action_type / label_type: CTR_IDX_I32 or CTR_IDX_I64. */
+int ctr_ensemble_preds(const float* preds, int64_t B, int M, int64_t ld_preds,
+                       const void* actions, int action_type, const float* prob_weights,
+                       const float* c_actions, const void* labels, int label_type,
+                       float* y_preds, float* rewards, float* return_c_actions, int32_t* rank_ws,
+                       ctr_stream_t stream);
+
 /* ------------------------------------------------ §8f: IPNN (InnerPNN) --------------
  * ctr_ipnn_forward: cat[b] = flat(E[x_b]) (F*K) ++ [ <E[x_bi],E[x_bj]> for i<j, row-major ]
  *   (P = F(F-1)/2), cat is [B, >= F*K + P] with row stride ldc: the MLP input of

@@ -15,6 +15,7 @@ A from-scratch restatement of jqsl2012/RL_CTR_Prediction's algorithms on torch-C
   feature_embedding   Feature_embedding.py:51-59
   pg_*                PG_model.py:104-154 (loss_func, choose_action, discount_and_norm)
   pg_policy/pg_learn  PG_model.py:24-58,156-179 (Net, learn: FE state, MLP, loss, Adam)
+  ensemble_preds      all_main/hybrid_td3_main_per_v10.py:54-164 (generate_preds, per example)
   sparse_plan         the grouping inside embedding_dense_backward (numpy, bit-exact ints)
   pretrain_run        all_main/pretrain_main.py:119-202 (per-epoch Adam, no shuffle, AUC)
 
@@ -226,6 +227,58 @@ def _ipnn_condition(params: dict, x: torch.Tensor, y: torch.Tensor) -> dict:
         terms[:, j] += wp[:, p_:p_ + 1] * e[:, i]
     A_E = torch.zeros(V, K).index_add_(0, x.reshape(-1), terms.reshape(-1, K))
     return {"feature_embedding.weight": A_E}
+
+
+# ------------------------------------------------------- RL ensemble (generate_preds) --
+def ensemble_preds(preds, actions, prob_weights, c_actions, labels):
+    """generate_preds (hybrid_td3_main_per_v10.py:54-164) restated per example, fp32 like the
+    reference's tensors: preds/prob_weights/c_actions [B,M], actions [B] (1-based ensemble
+    size), labels [B]. Returns (y [B], rewards [B], return_c_actions [B,M]) as float32.
+
+    a == M: y = sum_m pw*pred, ret_c = c. a < M: the a models with the largest pw (stable
+    order), softmax of the a largest c values of the example, y = sum w*pred; ret_c[model_m]
+    = m-th largest c value of batch row j, j = the example's ordinal among same-action
+    examples (the reference indexes the full-batch sorted c_actions with group-local
+    positions, line 127). Reward: label 1 -> y > mean(preds), label 0 -> y < mean."""
+    preds = np.asarray(preds, np.float32)
+    pw = np.asarray(prob_weights, np.float32)
+    ca = np.asarray(c_actions, np.float32)
+    act = np.asarray(actions).reshape(-1)
+    lab = np.asarray(labels).reshape(-1)
+    B, M = preds.shape
+    y = np.ones(B, np.float32)
+    r = np.ones(B, np.float32)
+    rc = np.zeros((B, M), np.float32)
+    seen = {}
+    for b in range(B):
+        a = int(act[b])
+        if not 1 <= a <= M:
+            continue
+        j = seen.get(a, 0)
+        seen[a] = j + 1
+        mean = np.float32(preds[b].sum(dtype=np.float32) / np.float32(M))
+        if a == M:
+            acc = np.float32(0)
+            for m in range(M):
+                acc = np.float32(acc + np.float32(pw[b, m] * preds[b, m]))
+            y[b] = acc
+            rc[b] = ca[b]
+        else:
+            models = np.argsort(-pw[b], kind="stable")[:a]
+            top_c = np.sort(ca[b])[::-1][:a]
+            row_j = np.sort(ca[j])[::-1]
+            e = np.exp((top_c - top_c[0]).astype(np.float64)).astype(np.float32)
+            w = (e / e.sum(dtype=np.float32)).astype(np.float32)
+            acc = np.float32(0)
+            for m in range(a):
+                acc = np.float32(acc + np.float32(w[m] * preds[b, models[m]]))
+                rc[b, models[m]] = row_j[m]
+            y[b] = acc
+        if lab[b] == 1:
+            r[b] = 1.0 if y[b] > mean else 0.0
+        elif lab[b] == 0:
+            r[b] = 1.0 if y[b] < mean else 0.0
+    return y, r, rc
 
 
 # ------------------------------------------------------------ scatter grouping -------

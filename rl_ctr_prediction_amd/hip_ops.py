@@ -514,6 +514,28 @@ def ipnn_backward(idx: torch.Tensor, emb: torch.Tensor, dcat: torch.Tensor,
     return out
 
 
+def ensemble_preds(preds: torch.Tensor, actions: torch.Tensor, prob_weights: torch.Tensor,
+                   c_actions: torch.Tensor, labels: torch.Tensor):
+    """generate_preds' arithmetic (hybrid_td3_main_per_v10.py:54-164) on [B, M] model pCTRs:
+    returns (y_preds [B,1], rewards [B,1], return_c_actions [B,M])."""
+    _f32(preds, "preds")
+    B, M = preds.shape
+    if preds.stride(1) != 1:
+        preds = preds.contiguous()
+    pw = _f32(prob_weights.reshape(B, M).contiguous(), "prob_weights")
+    ca = _f32(c_actions.reshape(B, M).contiguous(), "c_actions")
+    act, at = _idx(actions.reshape(B).contiguous(), "actions")
+    lab, lt = _idx(labels.reshape(B).contiguous(), "labels")
+    dev = preds.device
+    y = torch.empty(B, 1, dtype=torch.float32, device=dev)
+    r = torch.empty(B, 1, dtype=torch.float32, device=dev)
+    rc = torch.empty(B, M, dtype=torch.float32, device=dev)
+    rank = torch.empty(max(B, 1), dtype=torch.int32, device=dev)
+    lib.ctr_ensemble_preds(_p(preds), B, M, preds.stride(0), _p(act), at, _p(pw), _p(ca),
+                           _p(lab), lt, _p(y), _p(r), _p(rc), _p(rank), _stream())
+    return y, r, rc
+
+
 # ----------------------------------------------------------------------- REINFORCE ----
 def softmax_rows(x: torch.Tensor) -> torch.Tensor:
     _f32(x, "x")

@@ -75,8 +75,9 @@ class DeviceBatches:
     (features int64 [N,F] like the reference's collated LongTensor, labels float)."""
 
     def __init__(self, dataset: Data.libsvm_dataset, batch_size: int, device):
-        self.x = torch.as_tensor(np.asarray(dataset.Data), dtype=torch.int64).to(device)
-        self.y = torch.as_tensor(np.asarray(dataset.label), dtype=torch.float32).to(device)
+        # np.array copies: the data may be a read-only memory map (binfmt.open_bin)
+        self.x = torch.from_numpy(np.array(dataset.Data, dtype=np.int64)).to(device)
+        self.y = torch.from_numpy(np.array(dataset.label, dtype=np.float32)).to(device)
         self.batch_size = int(batch_size)
 
     def __len__(self):

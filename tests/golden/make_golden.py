@@ -13,6 +13,8 @@ Fixtures:
   g_fm.npz       FM fwd/bwd + 2 Adam steps (std 0.1 init) and an N(0,1) saturated case
   g_deepfm.npz   DeepFM fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
   g_ipnn.npz     InnerPNN fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
+  g_ensemble.npz generate_preds of the RL drivers (hybrid_td3_main_per_v10.py:54-164) on
+                 fixed pretrained-model pCTRs (stand-in models returning them)
   g_bce.npz      sigmoid + BCELoss values and d/dz incl. saturated logits
   g_fe.npz       Feature_Embedding forward
   g_pg.npz       PolicyGradient: discount_and_norm_rewards, loss_func (+ grads), choose_action
@@ -190,6 +192,27 @@ def gen_ipnn(P):
     np.savez(HERE / "g_ipnn.npz", **out)
 
 
+def gen_ensemble():
+    """The reference's generate_preds with M stand-in models that return fixed pCTR columns
+    (the function only calls model_dict[i](features).detach())."""
+    import src.all_main.hybrid_td3_main_per_v10 as H  # noqa: E402
+    out = {}
+    g = torch.Generator().manual_seed(7)
+    for case, (B, M) in enumerate([(257, 5), (64, 3), (1500, 8), (40, 1)]):
+        preds = torch.rand(B, M, generator=g)
+        model_dict = {i: (lambda x, i=i: preds[:, i:i + 1]) for i in range(M)}
+        feats = torch.zeros(B, 2, dtype=torch.long)
+        actions = torch.randint(1, M + 1, (B, 1), generator=g)
+        pw = torch.softmax(torch.randn(B, M, generator=g), dim=1)
+        ca = torch.rand(B, M, generator=g) * 2 - 1
+        labels = torch.randint(0, 2, (B, 1), generator=g)
+        y, r, rc = H.generate_preds(model_dict, feats, actions, pw, ca, labels, "cpu", "train")
+        for k, v in dict(preds=preds, actions=actions, pw=pw, ca=ca, labels=labels, y=y, r=r,
+                         rc=rc).items():
+            out[f"c{case}_{k}"] = _np(v)
+    np.savez(HERE / "g_ensemble.npz", **out)
+
+
 def gen_bce():
     z = torch.tensor([0.0, 0.3, -0.3, 2.0, -2.0, 8.0, -8.0, 15.0, -15.0, 16.5, -16.5, 17.0, -17.0,
                       30.0, -30.0, 50.0, -50.0, 88.0, -88.0, 90.0, -90.0, 104.0, -104.0, 1e-4,
@@ -336,6 +359,7 @@ def main():
     P, FE, PG, PM = _import_reference()
     torch.set_num_threads(4)
     gens = {"fm": lambda: gen_fm(P), "deepfm": lambda: gen_deepfm(P), "ipnn": lambda: gen_ipnn(P),
+            "ensemble": gen_ensemble,
             "bce": gen_bce, "fe": lambda: gen_fe(FE), "pg": lambda: gen_pg(PG),
             "toy": lambda: gen_toy(P, PM)}
     for name in (sys.argv[1:] or list(gens)):

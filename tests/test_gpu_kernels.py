@@ -408,3 +408,65 @@ def test_softmax_rows(cuda):
     x = torch.randn(1000, 5) * 3
     np.testing.assert_allclose(H.softmax_rows(x.to(cuda)).cpu().numpy(),
                                torch.softmax(x, 1).numpy(), rtol=1e-5, atol=1e-7)
+
+
+# ------------------------------------------------------ RL ensemble (§8f rank 3) -----
+@pytest.mark.parametrize("case", range(4))
+def test_ensemble_preds_vs_golden(cuda, golden, case):
+    """The kernel against the reference's own generate_preds outputs: rewards and
+    return_c_actions bit-exact, y within 1e-6 relative (softmax / sum roundings)."""
+    H = _hip()
+    g = golden("g_ensemble.npz")
+    k = lambda n: torch.tensor(g[f"c{case}_{n}"], device=cuda)  # noqa: E731
+    y, r, rc = H.ensemble_preds(k("preds"), k("actions"), k("pw"), k("ca"), k("labels"))
+    np.testing.assert_allclose(y.cpu().numpy(), g[f"c{case}_y"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(r.cpu().numpy(), g[f"c{case}_r"])
+    np.testing.assert_array_equal(rc.cpu().numpy(), g[f"c{case}_rc"])
+
+
+@pytest.mark.parametrize("B,M,dt", [(100_000, 5, torch.int64), (3000, 32, torch.int32),
+                                    (1, 2, torch.int64), (2049, 7, torch.int32)])
+def test_ensemble_preds_vs_oracle(cuda, B, M, dt):
+    """Large and edge batches (more than one 1024-example rank chunk, M = 32, actions out of
+    range, labels other than 0/1) against the oracle's per-example restatement."""
+    H = _hip()
+    g = torch.Generator().manual_seed(B + M)
+    preds = torch.rand(B, M, generator=g)
+    actions = torch.randint(0, M + 2, (B, 1), generator=g).to(dt)  # 0 and M+1: out of range
+    pw = torch.softmax(torch.randn(B, M, generator=g), dim=1)
+    ca = torch.rand(B, M, generator=g) * 2 - 1
+    labels = torch.randint(0, 3, (B, 1), generator=g).to(dt)      # 2: neither branch
+    y, r, rc = H.ensemble_preds(preds.to(cuda), actions.to(cuda), pw.to(cuda), ca.to(cuda),
+                                labels.to(cuda))
+    yo, ro, rco = O.ensemble_preds(preds.numpy(), actions.numpy(), pw.numpy(), ca.numpy(),
+                                   labels.numpy())
+    np.testing.assert_allclose(y.cpu().numpy().ravel(), yo, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(rc.cpu().numpy(), rco)
+    rr = r.cpu().numpy().ravel()
+    # a reward may differ only where y and the models' mean tie to fp32 rounding
+    mean = preds.numpy().mean(axis=1)
+    bad = (rr != ro) & (np.abs(yo - mean) > 1e-6)
+    assert not bad.any(), int(bad.sum())
+
+
+def test_generate_preds_drop_in(cuda):
+    """rl_ctr_prediction_amd.ensemble.generate_preds with real models (FM on HIP)."""
+    from rl_ctr_prediction_amd import FM
+    from rl_ctr_prediction_amd.ensemble import generate_preds
+    torch.manual_seed(0)
+    V, F, K, B = 500, 6, 8, 300
+    models = {i: FM(V, K).to(cuda).eval() for i in range(4)}
+    x = torch.randint(0, V, (B, F), device=cuda)
+    g = torch.Generator().manual_seed(1)
+    actions = torch.randint(1, 5, (B, 1), generator=g).to(cuda)
+    pw = torch.softmax(torch.randn(B, 4, generator=g), 1).to(cuda)
+    ca = (torch.rand(B, 4, generator=g) * 2 - 1).to(cuda)
+    labels = torch.randint(0, 2, (B, 1), generator=g).to(cuda)
+    y, r, rc = generate_preds(models, x, actions, pw, ca, labels, cuda, mode="train")
+    assert y.shape == (B, 1) and r.shape == (B, 1) and rc.shape == (B, 4)
+    with torch.no_grad():
+        preds = torch.cat([models[i](x) for i in range(4)], 1).cpu().numpy()
+    yo, ro, rco = O.ensemble_preds(preds, actions.cpu().numpy(), pw.cpu().numpy(),
+                                   ca.cpu().numpy(), labels.cpu().numpy())
+    np.testing.assert_allclose(y.cpu().numpy().ravel(), yo, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(rc.cpu().numpy(), rco)

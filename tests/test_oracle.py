@@ -197,3 +197,15 @@ def test_grad_condition_bounds_the_gradient(golden):
     single = np.bincount(flat, minlength=gE.shape[0]) == 1
     want = torch.zeros_like(AE).index_add_(0, x.reshape(-1), expect.reshape(-1, E.shape[1]))
     np.testing.assert_allclose(AE.numpy()[single], want.numpy()[single], rtol=1e-4, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_ensemble_preds_matches_reference(golden, case):
+    """generate_preds (hybrid_td3_main_per_v10.py:54-164): rewards and returned continuous
+    actions bit-exact (index work + selected values), y to fp32 rounding."""
+    g = golden("g_ensemble.npz")
+    k = lambda n: g[f"c{case}_{n}"]  # noqa: E731
+    y, r, rc = O.ensemble_preds(k("preds"), k("actions"), k("pw"), k("ca"), k("labels"))
+    np.testing.assert_allclose(y, k("y").ravel(), rtol=1e-6, atol=0)
+    np.testing.assert_array_equal(r, k("r").ravel())
+    np.testing.assert_array_equal(rc, k("rc"))
