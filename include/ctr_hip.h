@@ -319,6 +319,23 @@ int ctr_ensemble_preds(const float* preds, int64_t B, int M, int64_t ld_preds,
                        float* y_preds, float* rewards, float* return_c_actions, int32_t* rank_ws,
                        ctr_stream_t stream);
 
+/* ------------------------------------------------ §8f: FFM (field-aware FM) ---------
+ * tables: a DEVICE array of F pointers, table t = field t's embedding [V, K] (K <= 64,
+ * F*V < 2^31). ctr_ffm_forward: z = bias + sum_f lin[x_f] + sum_{i<j} sum_k
+ * E_j[x_i,k] * E_i[x_j,k] (p_model.FFM.forward, p_model.py:82-100), with the fused BCE head
+ * when labels != NULL (as ctr_fm_forward). ctr_ffm_backward: the F(F-1) row gradients of
+ * every example, vals[pos, :] = gz[b] * E_f[x_bt, :] for table t's row x_bf, key[pos] =
+ * t*V + x_bf, pos = (b*F + f)*(F-1) + (t < f ? t : t-1) ([B*F*(F-1)] keys, [.., K] vals):
+ * a sparse plan over the keys (key range F*V) + ctr_segment_sum_rows give every table's
+ * row sums in slot order. */
+int ctr_ffm_forward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                    const float* const* tables, const float* lin, const float* bias, float* z,
+                    const float* labels, float mean_div, float* p, float* loss_elem, float* gz,
+                    int32_t* err_flag, ctr_stream_t stream);
+int ctr_ffm_backward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                     const float* const* tables, const float* gz, int32_t* keys, float* vals,
+                     ctr_stream_t stream);
+
 /* ------------------------------------------------ §8f: IPNN (InnerPNN) --------------
  * ctr_ipnn_forward: cat[b] = flat(E[x_b]) (F*K) ++ [ <E[x_bi],E[x_bj]> for i<j, row-major ]
  *   (P = F(F-1)/2), cat is [B, >= F*K + P] with row stride ldc: the MLP input of

@@ -10,6 +10,7 @@ A from-scratch restatement of jqsl2012/RL_CTR_Prediction's algorithms on torch-C
   fm_forward          p_model.py:40-57       (FM.forward)
   deepfm_forward      p_model.py:296-324     (DeepFM.to_fm + forward, MLP 276-293)
   ipnn_forward        p_model.py:146-200     (InnerPNN: flat ++ pairwise inner products, MLP)
+  ffm_forward         p_model.py:59-100      (FFM: one table per field, E_j[x_i] . E_i[x_j])
   bce                 all_main/pretrain_main.py:74,139 (nn.BCELoss, mean)
   train_step          all_main/pretrain_main.py:67-83 (fwd, BCE, zero_grad, backward, Adam)
   feature_embedding   Feature_embedding.py:51-59
@@ -51,6 +52,11 @@ def init_params(kind: str, V: int, F: int, K: int, seed: int | None = None) -> d
     kaiming-uniform weights / uniform biases."""
     if seed is not None:
         torch.manual_seed(seed)
+    if kind == "FFM":  # p_model.py:65-78: linear, bias, then one Embedding(V, K) per field
+        p = {"linear.weight": torch.nn.Embedding(V, 1).weight.data, "bias": torch.zeros(1)}
+        for t in range(F):
+            p[f"field_feature_embeddings.{t}.weight"] = torch.nn.Embedding(V, K).weight.data
+        return {k: v.clone().requires_grad_(True) for k, v in p.items()}
     if kind == "IPNN":  # p_model.py:153-177: embedding, then Linear(F*K + P, 300), ...
         p = {"feature_embedding.weight": torch.nn.Embedding(V, K).weight.data}
         dims = [F * K + F * (F - 1) // 2, 300, 200, 1]
@@ -116,7 +122,20 @@ def ipnn_forward(params: dict, x: torch.Tensor, drop_p: float = 0.2,
                              training))
 
 
+def ffm_logit(params: dict, x: torch.Tensor) -> torch.Tensor:
+    """bias + sum_f w[x_f] + sum_k sum_{i<j} E_j[x_i,k] * E_i[x_j,k], shape [B,1]."""
+    B, F = x.shape
+    emb = [Fn.embedding(x, params[f"field_feature_embeddings.{t}.weight"]) for t in range(F)]
+    row, col = ipnn_pairs(F)
+    second = torch.stack([emb[j][:, i] * emb[i][:, j]
+                          for i, j in zip(row.tolist(), col.tolist())], dim=1)  # [B, P, K]
+    lin = Fn.embedding(x, params["linear.weight"]).sum(dim=1)
+    return params["bias"] + lin + second.sum(dim=1).sum(dim=1, keepdim=True)
+
+
 def forward(kind: str, params: dict, x, drop_p=0.2, training=True):
+    if kind == "FFM":
+        return torch.sigmoid(ffm_logit(params, x))
     if kind == "FM":
         return fm_forward(params, x)
     if kind == "IPNN":

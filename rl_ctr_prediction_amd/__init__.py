@@ -5,10 +5,10 @@ running on hand-written gfx950 HIP kernels behind the C ABI in include/ctr_hip.h
 (libctr_hip.so). See DESIGN.md.
 """
 from .feature_embedding import Feature_Embedding
-from .p_model import FM, DeepFM, InnerPNN
+from .p_model import FFM, FM, DeepFM, InnerPNN
 from .pg_model import Net, PolicyGradient
 from .sharded import ShardedCTRTrainer
 from .trainer import FusedCTRTrainer
 
-__all__ = ["FM", "DeepFM", "InnerPNN", "Feature_Embedding", "Net", "PolicyGradient", "FusedCTRTrainer",
+__all__ = ["FM", "FFM", "DeepFM", "InnerPNN", "Feature_Embedding", "Net", "PolicyGradient", "FusedCTRTrainer",
            "ShardedCTRTrainer"]

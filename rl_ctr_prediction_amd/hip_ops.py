@@ -536,6 +536,56 @@ def ensemble_preds(preds: torch.Tensor, actions: torch.Tensor, prob_weights: tor
     return y, r, rc
 
 
+class FFMTables:
+    """Device array of the F field tables' data pointers (ctr_ffm_* take `float* const*`);
+    rebuilt when a table is re-allocated (Module.to(), load_state_dict into new storage)."""
+
+    def __init__(self):
+        self._key = None
+        self.ptrs = None
+
+    def get(self, tables) -> torch.Tensor:
+        key = tuple(t.data_ptr() for t in tables)
+        if key != self._key:
+            for t in tables:
+                _f32(t, "ffm table")
+            self.ptrs = torch.tensor(key, dtype=torch.int64, device=tables[0].device)
+            self._key = key
+        return self.ptrs
+
+
+def ffm_forward(idx, tables, ptrs, lin, bias, labels=None, mean_div=None, err_flag=None):
+    """FFM logits z [B] (and with labels: p, per-example loss, dL/dz)."""
+    idx, it = _idx(idx)
+    B, F = idx.shape
+    V, K = tables[0].shape
+    if len(tables) != F:
+        raise ValueError(f"ffm_forward: {len(tables)} tables for {F} fields")
+    dev = tables[0].device
+    e = lambda: torch.empty(B, dtype=torch.float32, device=dev)  # noqa: E731
+    z = e()
+    out = {"z": z}
+    if labels is not None:
+        out.update(p=e(), loss_elem=e(), gz=e())
+    lib.ctr_ffm_forward(_p(idx), it, B, F, K, V, _p(ptrs), _p(lin), _p(bias), _p(z),
+                        _p(labels), float(B if mean_div is None else mean_div), _p(out.get("p")),
+                        _p(out.get("loss_elem")), _p(out.get("gz")), _p(err_flag), _stream())
+    return out
+
+
+def ffm_backward(idx, tables, ptrs, gz):
+    """(keys int32 [B*F*(F-1)], vals [B*F*(F-1), K]): every example's table-row gradients."""
+    idx, it = _idx(idx)
+    B, F = idx.shape
+    V, K = tables[0].shape
+    n = B * F * (F - 1)
+    keys = torch.empty(max(n, 1), dtype=torch.int32, device=gz.device)
+    vals = torch.empty(max(n, 1), K, dtype=torch.float32, device=gz.device)
+    lib.ctr_ffm_backward(_p(idx), it, B, F, K, V, _p(ptrs), _p(_f32(gz.contiguous(), "gz")),
+                         _p(keys), _p(vals), _stream())
+    return keys[:n], vals[:n]
+
+
 # ----------------------------------------------------------------------- REINFORCE ----
 def softmax_rows(x: torch.Tensor) -> torch.Tensor:
     _f32(x, "x")

@@ -1,6 +1,6 @@
-"""FM, DeepFM and InnerPNN with the reference's construction API, on the HIP kernels.
+"""FM, FFM, DeepFM and InnerPNN with the reference's construction API, on the HIP kernels.
 
-Drop-in for ``src/models/p_model.py`` (FM 28-57, InnerPNN 146-200, DeepFM 256-324): identical constructor
+Drop-in for ``src/models/p_model.py`` (FM 28-57, FFM 59-100, InnerPNN 146-200, DeepFM 256-324): identical constructor
 signatures, submodules created in the same order (so ``torch.manual_seed(s)`` gives the
 same initial weights as the reference) and identical state_dict keys, so the RL drivers'
 ``torch.load('...FMbest.pth')`` / ``load_state_dict`` and ``Feature_Embedding.load_embedding``
@@ -106,6 +106,35 @@ class _IPNNPart(torch.autograd.Function):
         grad_rows, _ = hip_ops.segment_sum_rows(plan, dslot)
         g_emb, _ = hip_ops.rows_to_dense(plan, V, grad_rows)
         return None, g_emb
+
+
+class _FFMPart(torch.autograd.Function):
+    """FFM logit (p_model.py:82-97) on ctr_ffm_forward; backward: every example's table-row
+    gradients (ctr_ffm_backward), summed per (table, row) in slot order through a sparse plan
+    over the F*V key space, returned dense per table like embedding_dense_backward."""
+
+    @staticmethod
+    def forward(ctx, x, lin, bias, ptrs, *tables):
+        ctx.save_for_backward(x, ptrs, *tables)
+        return hip_ops.ffm_forward(x, tables, ptrs, lin, bias)["z"].view(-1, 1)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, ptrs, *tables = ctx.saved_tensors
+        B, F = x.shape
+        V, K = tables[0].shape
+        dev = gz.device
+        gz = gz.reshape(-1).contiguous()
+        keys, vals = hip_ops.ffm_backward(x, tables, ptrs, gz)
+        plan = hip_ops.SparsePlanBuffers(keys.numel(), dev).build(keys, F * V)
+        rows, _ = hip_ops.segment_sum_rows(plan, vals)
+        dense, _ = hip_ops.rows_to_dense(plan, F * V, rows)
+        g_tables = [dense[t * V:(t + 1) * V] for t in range(F)]
+        plan_x = hip_ops.SparsePlanBuffers(B * F, dev).build(x, V)
+        slot_g = gz.view(B, 1).expand(B, F).reshape(-1, 1).contiguous()  # dL/dw[x_bf] = gz[b]
+        rows_w, _ = hip_ops.segment_sum_rows(plan_x, slot_g)
+        g_lin, _ = hip_ops.rows_to_dense(plan_x, V, rows_w)
+        return (None, g_lin, hip_ops.tensor_sum(gz).view(1), None, *g_tables)
 
 
 def _fm_part(x, emb, lin, bias, want_emb):
@@ -239,3 +268,30 @@ class InnerPNN(nn.Module):
             zero = torch.zeros(h.shape[0], dtype=torch.float32, device=h.device)
             head = hip_ops.deepfm_head(h, m[6].weight, m[6].bias, zero)
             return head["p"].view(-1, 1)
+
+
+class FFM(nn.Module):
+    """p_model.py:59-100: z = bias + sum_f w[x_f] + sum_{i<j} <E_j[x_i], E_i[x_j]>, one
+    nn.Embedding(V, K) per field (same construction order and state_dict keys)."""
+
+    def __init__(self, feature_nums, field_nums, latent_dims, output_dim=1):
+        super().__init__()
+        latent_dims = int(latent_dims)
+        if output_dim != 1:
+            raise NotImplementedError("FFM: output_dim must be 1 (the reference's only use)")
+        self.field_nums = field_nums
+        self.linear = nn.Embedding(feature_nums, output_dim)
+        self.bias = nn.Parameter(torch.zeros((output_dim,)))
+        self.field_feature_embeddings = nn.ModuleList([
+            nn.Embedding(feature_nums, latent_dims) for _ in range(field_nums)])
+        self._ptrs = hip_ops.FFMTables()
+
+    def forward(self, x):
+        tabs = [e.weight for e in self.field_feature_embeddings]
+        ptrs = self._ptrs.get(tabs)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            return torch.sigmoid(_FFMPart.apply(x, self.linear.weight, self.bias, ptrs, *tabs))
+        with torch.no_grad():
+            z = hip_ops.ffm_forward(x, [t.detach() for t in tabs], ptrs,
+                                    self.linear.weight.detach(), self.bias.detach())["z"]
+            return torch.sigmoid(z).view(-1, 1)

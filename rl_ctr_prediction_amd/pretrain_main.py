@@ -9,7 +9,8 @@ AUC over the concatenated test predictions, loss-/AUC-based early stopping with 
 of the checkpoint four epochs back.
 
 Differences, all deliberate: the training step is the fused HIP step (FM, DeepFM and
-IPNN; the other seven model families are out of scope); the batches are
+IPNN; FFM trains through autograd on its HIP kernels + torch.optim.Adam, AutogradTrainer;
+the other six model families are out of scope); the batches are
 sliced from one device-resident copy of the data instead of 8 DataLoader worker
 processes; the rotating-checkpoint cleanup skips files that were never written (the
 reference crashes there when epoch < 5, all_main/pretrain_main.py:201-202).
@@ -48,9 +49,38 @@ def get_model(model_name, feature_nums, field_nums, latent_dims):
         return Model.DeepFM(feature_nums, field_nums, latent_dims)
     if model_name == "IPNN":
         return Model.InnerPNN(feature_nums, field_nums, latent_dims)
+    if model_name == "FFM":
+        return Model.FFM(feature_nums, field_nums, latent_dims)
     raise NotImplementedError(
-        f"{model_name}: FM, DeepFM and IPNN are built on HIP; "
-        "LR/FFM/W&D/FNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
+        f"{model_name}: FM, FFM, DeepFM and IPNN are built on HIP; "
+        "LR/W&D/FNN/OPNN/DCN/AFM are out of scope (SURVEY.md §2 row 7)")
+
+
+class AutogradTrainer:
+    """The reference's own step (all_main/pretrain_main.py:72-79: forward, BCELoss,
+    zero_grad, backward, torch.optim.Adam.step) for models without a fused step (FFM): the
+    forward / backward run on the HIP kernels through autograd, the dense gradients go to
+    an unchanged torch.optim.Adam, re-created every epoch like the reference (line 153)."""
+
+    def __init__(self, model, lr, weight_decay):
+        self.model, self.lr, self.weight_decay = model, lr, weight_decay
+        self.loss = nn.BCELoss()
+        self.reset_optimizer()
+
+    def reset_optimizer(self):
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=self.lr,
+                                    weight_decay=self.weight_decay)
+
+    def step(self, features, labels):
+        y = self.model(features)
+        loss = self.loss(y, labels.view(-1, 1).float())
+        self.model.zero_grad()
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    def check_errors(self):
+        pass
 
 
 def get_dataset(datapath, dataset_name, campaign_id, binary=True):
@@ -153,7 +183,10 @@ def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, l
 
     model = get_model(model_name, feature_nums, field_nums, latent_dims).to(device)
     loss = nn.BCELoss()
-    trainer = FusedCTRTrainer(model, lr=learning_rate, weight_decay=weight_decay)
+    if model_name == "FFM":
+        trainer = AutogradTrainer(model, learning_rate, weight_decay)
+    else:
+        trainer = FusedCTRTrainer(model, lr=learning_rate, weight_decay=weight_decay)
 
     valid_aucs, valid_losses, history = [], [], []
     early_stop_index, is_early_stop = 0, False
@@ -211,7 +244,7 @@ def _parser():
     parser.add_argument("--data_path", default="../../data/")
     parser.add_argument("--dataset_name", default="avazu/", help="ipinyou, cretio, yoyi, avazu")
     parser.add_argument("--campaign_id", default="avazu/", help="1458, 3358, 3386, 3427, 3476, avazu")
-    parser.add_argument("--model_name", default="FM", help="FM, DeepFM, IPNN")
+    parser.add_argument("--model_name", default="FM", help="FM, FFM, DeepFM, IPNN")
     parser.add_argument("--latent_dims", type=int, default=10)
     parser.add_argument("--epoch", type=int, default=20)
     parser.add_argument("--learning_rate", type=float, default=1e-3)

@@ -13,13 +13,14 @@ Fixtures:
   g_fm.npz       FM fwd/bwd + 2 Adam steps (std 0.1 init) and an N(0,1) saturated case
   g_deepfm.npz   DeepFM fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
   g_ipnn.npz     InnerPNN fwd/bwd + 2 Adam steps, dropout p=0 (train mode)
+  g_ffm.npz      FFM fwd/bwd + 2 Adam steps (std 0.1 tables)
   g_ensemble.npz generate_preds of the RL drivers (hybrid_td3_main_per_v10.py:54-164) on
                  fixed pretrained-model pCTRs (stand-in models returning them)
   g_bce.npz      sigmoid + BCELoss values and d/dz incl. saturated logits
   g_fe.npz       Feature_Embedding forward
   g_pg.npz       PolicyGradient: discount_and_norm_rewards, loss_func (+ grads), choose_action
   toy/           C1 toy data (13 dense bucketised + 26 sparse fields, 1000 rows)
-  g_toy.json     pretrain_main.main on the toy (FM, and DeepFM with dropout p=0):
+  g_toy.json     pretrain_main.main on the toy (FM, FFM, and DeepFM / IPNN with dropout p=0):
                  per-epoch train loss / valid AUC / valid loss, final test AUC and preds
   manifest.json  versions and seeds
 """
@@ -192,6 +193,46 @@ def gen_ipnn(P):
     np.savez(HERE / "g_ipnn.npz", **out)
 
 
+def gen_ffm(P):
+    """FFM (p_model.py:59-100): same protocol as gen_deepfm."""
+    out = {}
+    V, F, K, B = 300, 6, 8, 64
+    torch.manual_seed(0)
+    m = P.FFM(V, F, K)
+    with torch.no_grad():
+        for e in m.field_feature_embeddings:
+            e.weight.normal_(0, 0.1)
+        m.linear.weight.normal_(0, 0.1)
+        m.bias.fill_(-0.1)
+    keys = list(m.state_dict().keys())
+    out["keys"] = np.array(keys)
+    sd = m.state_dict()
+    for k in keys:
+        out[f"init/{k}"] = _np(sd[k])
+    g = torch.Generator().manual_seed(4)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    crit = torch.nn.BCELoss()
+    for s in range(2):
+        x = _hot_ids(g, B, F, V)
+        y = (torch.rand(B, 1, generator=g) < 0.3).float()
+        p = m(x)
+        loss = crit(p, y)
+        m.zero_grad()
+        loss.backward()
+        out[f"x{s}"] = _np(x)
+        out[f"y{s}"] = _np(y)
+        out[f"p{s}"] = _np(p)
+        out[f"loss{s}"] = np.float32(loss.item())
+        named = dict(m.named_parameters())
+        for k in keys:
+            out[f"grad{s}/{k}"] = _np(named[k].grad)
+        opt.step()
+        sd = m.state_dict()
+        for k in keys:
+            out[f"step{s + 1}/{k}"] = _np(sd[k])
+    np.savez(HERE / "g_ffm.npz", **out)
+
+
 def gen_ensemble():
     """The reference's generate_preds with M stand-in models that return fixed pCTR columns
     (the function only calls model_dict[i](features).detach())."""
@@ -312,11 +353,16 @@ _EPOCH_RE = re.compile(r"epoch: (\d+) training average loss: (\S+) validation au
                        r"validation loss: (\S+)")
 
 
-def gen_toy(P, PM):
+def gen_toy(P, PM, models=("FM", "DeepFM"), merge=False):
+    """merge: add `models` to the existing g_toy.json, on the existing toy files."""
     toy = HERE / "toy"
-    V = gen_toy_data(toy)
-    result = {"V": V, "F": 39, "K": 10, "batch_size": 256, "epoch": 5, "lr": 1e-3, "wd": 1e-5}
-    for model_name in ("FM", "DeepFM"):
+    if merge:
+        result = json.loads((HERE / "g_toy.json").read_text())
+    else:
+        V = gen_toy_data(toy)
+        result = {"V": V, "F": 39, "K": 10, "batch_size": 256, "epoch": 5, "lr": 1e-3,
+                  "wd": 1e-5}
+    for model_name in models:
         with tempfile.TemporaryDirectory() as tmp:
             data_root = Path(tmp) / "data"
             (data_root / "toy").mkdir(parents=True)
@@ -359,10 +405,11 @@ def main():
     P, FE, PG, PM = _import_reference()
     torch.set_num_threads(4)
     gens = {"fm": lambda: gen_fm(P), "deepfm": lambda: gen_deepfm(P), "ipnn": lambda: gen_ipnn(P),
-            "ensemble": gen_ensemble,
+            "ensemble": gen_ensemble, "ffm": lambda: gen_ffm(P),
+            "toy_extra": lambda: gen_toy(P, PM, ("IPNN", "FFM"), merge=True),
             "bce": gen_bce, "fe": lambda: gen_fe(FE), "pg": lambda: gen_pg(PG),
             "toy": lambda: gen_toy(P, PM)}
-    for name in (sys.argv[1:] or list(gens)):
+    for name in (sys.argv[1:] or [n for n in gens if n != "toy_extra"] + ["toy_extra"]):
         gens[name]()
     (HERE / "manifest.json").write_text(json.dumps({
         "generator": "tests/golden/make_golden.py",

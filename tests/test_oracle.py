@@ -209,3 +209,23 @@ def test_ensemble_preds_matches_reference(golden, case):
     np.testing.assert_allclose(y, k("y").ravel(), rtol=1e-6, atol=0)
     np.testing.assert_array_equal(r, k("r").ravel())
     np.testing.assert_array_equal(rc, k("rc"))
+
+
+def test_ffm_matches_reference(golden):
+    """FFM (p_model.py:59-100): forward, every gradient and two Adam steps."""
+    g = golden("g_ffm.npz")
+    keys = [str(k) for k in g["keys"]]
+    params = {k: torch.tensor(g[f"init/{k}"]).clone().requires_grad_(True) for k in keys}
+    opt = O.make_optimizer(params, 1e-3, 1e-5)
+    for s in range(2):
+        x, y = torch.tensor(g[f"x{s}"]), torch.tensor(g[f"y{s}"])
+        loss, p, gr = O.grads("FFM", params, x, y)
+        np.testing.assert_allclose(p.numpy(), g[f"p{s}"], rtol=1e-6, atol=0)
+        assert loss == pytest.approx(float(g[f"loss{s}"]), rel=1e-6)
+        for k in keys:
+            np.testing.assert_allclose(gr[k].numpy(), g[f"grad{s}/{k}"], rtol=1e-5, atol=1e-9,
+                                       err_msg=k)
+        opt.step()
+        for k in keys:
+            np.testing.assert_allclose(params[k].detach().numpy(), g[f"step{s + 1}/{k}"],
+                                       rtol=1e-6, atol=1e-8, err_msg=k)
