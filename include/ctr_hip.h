@@ -144,6 +144,19 @@ int ctr_sum_f32(const float* x, int64_t n, float scale, float* out, void* ws, in
                 ctr_stream_t stream);
 int ctr_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx, const float* row_w,
                    float scale, float* out, void* ws, int64_t ws_bytes, ctr_stream_t stream);
+/* Up to 8 ctr_colsum_f32 jobs in one launch pair, each output bitwise ctr_colsum_f32's
+ * (same row partition and order): the DeepFM step's bias gradients (colsum dH1, dH2), the
+ * last layer's weight gradient (gz-weighted colsum of H2) and its bias (colsum of gz). */
+typedef struct ctr_colsum_job {
+  const float* X;
+  int64_t M, N, ldx;
+  const float* row_w;
+  float scale;
+  float* out;
+} ctr_colsum_job;
+int64_t ctr_colsum_multi_workspace_bytes(int n_jobs, const ctr_colsum_job* jobs);
+int ctr_colsum_multi_f32(int n_jobs, const ctr_colsum_job* jobs, void* ws, int64_t ws_bytes,
+                         ctr_stream_t stream);
 
 /* ------------------------------------------------ A3: embedding scatter-add -----------
  * A sparse plan groups the S = B*F slots (slot s = b*F + f) of a batch by feature id.

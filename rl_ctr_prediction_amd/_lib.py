@@ -28,6 +28,15 @@ class SparsePlan(C.Structure):
 
 _plan_p = C.POINTER(SparsePlan)
 
+
+class ColsumJob(C.Structure):
+    """Mirror of ``ctr_colsum_job`` (include/ctr_hip.h)."""
+    _fields_ = [("X", _vp), ("M", _i64), ("N", _i64), ("ldx", _i64), ("row_w", _vp),
+                ("scale", _f32), ("out", _vp)]
+
+
+_job_p = C.POINTER(ColsumJob)
+
 # name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
 # against the header.
 SIGNATURES = {
@@ -51,6 +60,8 @@ SIGNATURES = {
     "ctr_reduce_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sum_f32": (_i32, [_vp, _i64, _f32, _vp, _vp, _i64, _vp]),
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),
+    "ctr_colsum_multi_workspace_bytes": (_i64, [_i32, _job_p]),
+    "ctr_colsum_multi_f32": (_i32, [_i32, _job_p, _vp, _i64, _vp]),
     "ctr_sparse_plan_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sparse_plan_build": (_i32, [_vp, _i32, _i64, _plan_p, _vp, _i64, _vp, _vp]),
     "ctr_plan_slot_to_unique": (_i32, [_plan_p, _vp, _vp]),

@@ -100,6 +100,65 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ p
   }
 }
 
+// Several column sums in ONE launch pair (the DeepFM step's bias / last-layer weight
+// gradients): each job keeps exactly colsum_stage1/2's row partition and order, so every
+// output is bitwise what ctr_colsum_f32 gives; blocks enumerate (job, 64-column block).
+constexpr int kMaxColsumJobs = 8;
+struct ColsumJobs {
+  int n;
+  const float* X[kMaxColsumJobs];
+  int64_t M[kMaxColsumJobs], N[kMaxColsumJobs], ldx[kMaxColsumJobs], rps[kMaxColsumJobs];
+  const float* w[kMaxColsumJobs];
+  float scale[kMaxColsumJobs];
+  float* out[kMaxColsumJobs];
+  int rs[kMaxColsumJobs];
+  int64_t cb0[kMaxColsumJobs + 1];  // first 64-column block of each job
+  int64_t part0[kMaxColsumJobs];    // offset of each job's partials
+};
+
+__global__ __launch_bounds__(256) void colsum_multi_stage1(ColsumJobs J, float* __restrict__ part) {
+  __shared__ float sh[4][64];
+  int j = 0;
+  while (j + 1 < J.n && (int64_t)blockIdx.x >= J.cb0[j + 1]) ++j;
+  if ((int)blockIdx.y >= J.rs[j]) return;  // block-uniform
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t n = ((int64_t)blockIdx.x - J.cb0[j]) * 64 + cx;
+  const int64_t N = J.N[j], ldx = J.ldx[j];
+  const int64_t lo = (int64_t)blockIdx.y * J.rps[j];
+  const int64_t hi = min(J.M[j], lo + J.rps[j]);
+  const float* X = J.X[j];
+  const float* w = J.w[j];
+  float acc = 0.f;
+  if (n < N) {
+    if (w) {
+#pragma unroll 8
+      for (int64_t m = lo + ry; m < hi; m += 4) acc += w[m] * X[m * ldx + n];
+    } else {
+#pragma unroll 8
+      for (int64_t m = lo + ry; m < hi; m += 4) acc += X[m * ldx + n];
+    }
+  }
+  sh[ry][cx] = acc;
+  __syncthreads();
+  if (ry == 0 && n < N)
+    part[J.part0[j] + blockIdx.y * N + n] = (sh[0][cx] + sh[1][cx]) + (sh[2][cx] + sh[3][cx]);
+}
+
+__global__ __launch_bounds__(256) void colsum_multi_stage2(ColsumJobs J,
+                                                           const float* __restrict__ part) {
+  for (int j = 0; j < J.n; ++j) {
+    const int64_t N = J.N[j];
+    const float* pj = part + J.part0[j];
+    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
+         n += (int64_t)gridDim.x * blockDim.x) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < J.rs[j]; ++r) s += pj[(int64_t)r * N + n];
+      J.out[j][n] = s * J.scale[j];
+    }
+  }
+}
+
 static int colsum_splits(int64_t M) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 256), 64));
 }
@@ -311,6 +370,54 @@ extern "C" int ctr_colsum_f32(const float* X, int64_t M, int64_t N, int64_t ldx,
   hipLaunchKernelGGL(colsum_stage2, (unsigned)std::min<int64_t>(ceil_div(N, 256), 1024), 256, 0,
                      st, part, rs, N, scale, out);
   CTR_LAUNCH_CHECK("colsum_stage2");
+  return CTR_OK;
+}
+
+static int colsum_multi_plan(int n, const ctr_colsum_job* jobs, ColsumJobs& J, int64_t& need) {
+  CTR_REQUIRE(n >= 1 && n <= kMaxColsumJobs && jobs, "ctr_colsum_multi_f32: 1..%d jobs",
+              kMaxColsumJobs);
+  memset(&J, 0, sizeof(J));
+  J.n = n;
+  need = 0;
+  for (int j = 0; j < n; ++j) {
+    const ctr_colsum_job& c = jobs[j];
+    CTR_REQUIRE(c.M >= 0 && c.N >= 1 && c.ldx >= c.N && c.out && (c.X || c.M == 0),
+                "ctr_colsum_multi_f32: bad job %d", j);
+    J.X[j] = c.X; J.M[j] = c.M; J.N[j] = c.N; J.ldx[j] = c.ldx; J.w[j] = c.row_w;
+    J.scale[j] = c.scale; J.out[j] = c.out;
+    J.rs[j] = colsum_splits(c.M);
+    J.rps[j] = std::max<int64_t>(1, ceil_div(c.M, J.rs[j]));
+    J.cb0[j + 1] = J.cb0[j] + ceil_div(c.N, 64);
+    J.part0[j] = need;
+    need += (int64_t)J.rs[j] * c.N;
+  }
+  need *= 4;
+  return CTR_OK;
+}
+
+extern "C" int64_t ctr_colsum_multi_workspace_bytes(int n_jobs, const ctr_colsum_job* jobs) {
+  ColsumJobs J;
+  int64_t need = 0;
+  if (colsum_multi_plan(n_jobs, jobs, J, need) != CTR_OK) return -1;
+  return align_up(std::max<int64_t>(need, 4), 256);
+}
+
+extern "C" int ctr_colsum_multi_f32(int n_jobs, const ctr_colsum_job* jobs, void* ws,
+                                    int64_t ws_bytes, ctr_stream_t stream) {
+  ColsumJobs J;
+  int64_t need = 0;
+  int rc = colsum_multi_plan(n_jobs, jobs, J, need);
+  if (rc != CTR_OK) return rc;
+  CTR_REQUIRE(ws && ws_bytes >= need, "ctr_colsum_multi_f32: workspace too small");
+  int rs_max = 1;
+  for (int j = 0; j < n_jobs; ++j) rs_max = std::max(rs_max, J.rs[j]);
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(ws);
+  hipLaunchKernelGGL(colsum_multi_stage1, dim3((unsigned)J.cb0[n_jobs], (unsigned)rs_max), 256, 0,
+                     st, J, part);
+  CTR_LAUNCH_CHECK("colsum_multi_stage1");
+  hipLaunchKernelGGL(colsum_multi_stage2, 4, 256, 0, st, J, static_cast<const float*>(part));
+  CTR_LAUNCH_CHECK("colsum_multi_stage2");
   return CTR_OK;
 }
 

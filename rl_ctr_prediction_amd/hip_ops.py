@@ -218,6 +218,21 @@ def tensor_sum(x: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
     return out
 
 
+def colsum_multi(jobs) -> None:
+    """Several colsum() calls in one launch pair: jobs = [(X [M,N], row_w or None, out [N])];
+    each out is bitwise what colsum(X, row_w, out=out) writes."""
+    from ._lib import ColsumJob
+    arr = (ColsumJob * len(jobs))()
+    for i, (X, row_w, out) in enumerate(jobs):
+        _f32(X, "X")
+        if X.dim() != 2 or out.numel() != X.shape[1]:
+            raise ValueError("colsum_multi: X must be [M, N] and out N elements")
+        arr[i] = ColsumJob(_p(X), X.shape[0], X.shape[1], X.stride(0), _p(row_w), 1.0, _p(out))
+    nbytes = lib.ctr_colsum_multi_workspace_bytes(len(jobs), arr)
+    ws = Workspace.get(nbytes, jobs[0][0].device)
+    lib.ctr_colsum_multi_f32(len(jobs), arr, _p(ws), ws.numel(), _stream())
+
+
 def colsum(X: torch.Tensor, row_w: torch.Tensor | None = None, scale: float = 1.0,
            out=None) -> torch.Tensor:
     _f32(X, "X")

@@ -481,15 +481,15 @@ class FusedCTRTrainer:
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            # Linear(200,1): dW = gz^T H2, db = sum gz
-            hip_ops.colsum(b.h2, row_w=gz, out=gv["mlp.6.weight"].view(-1))
-            hip_ops.tensor_sum(gz, out=gv["mlp.6.bias"].view(1))
-            # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2
+            # the small reductions in one launch pair: Linear(200,1) dW = gz^T H2 and
+            # db = sum gz; Linear(300,200) db1 = colsum dH2; Linear(F*K,300) db0 = colsum dH1
+            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
+                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
+                                  (dh2, None, gv["mlp.3.bias"]),
+                                  (b.dh1, None, gv["mlp.0.bias"])])
+            # Linear(300,200): dW1 = dH2^T H1; Linear(F*K,300): dW0 = dH1^T X
             self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
-            hip_ops.colsum(dh2, out=gv["mlp.3.bias"])
-            # Linear(F*K,300): dW0 = dH1^T X, db0 = colsum dH1
             self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
-            hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
         return gz
 
     def _join_wgrad(self) -> None:

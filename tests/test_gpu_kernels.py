@@ -470,3 +470,17 @@ def test_generate_preds_drop_in(cuda):
                                    ca.cpu().numpy(), labels.cpu().numpy())
     np.testing.assert_allclose(y.cpu().numpy().ravel(), yo, rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(rc.cpu().numpy(), rco)
+
+
+def test_colsum_multi_is_bitwise_colsum(cuda):
+    """One launch pair for several column sums: each output bitwise the single colsum."""
+    H = _hip()
+    g = torch.Generator().manual_seed(3)
+    jobs = [(torch.randn(8192, 200, generator=g), torch.randn(8192, generator=g)),
+            (torch.randn(8192, 1, generator=g), None), (torch.randn(8192, 300, generator=g), None),
+            (torch.randn(77, 5, generator=g), None), (torch.randn(1, 70, generator=g), None)]
+    jobs = [(X.to(cuda), None if w is None else w.to(cuda)) for X, w in jobs]
+    outs = [torch.empty(X.shape[1], device=cuda) for X, _ in jobs]
+    H.colsum_multi([(X, w, o) for (X, w), o in zip(jobs, outs)])
+    for (X, w), o in zip(jobs, outs):
+        assert torch.equal(o, H.colsum(X, row_w=w)), X.shape
