@@ -604,7 +604,7 @@ static const KnownGemm kKnown[] = {
     {8192, 300, 200, 0, 0, CTR_GEMM_SPLIT_BF16, 0, 1},    // dH1 = dH2.W1
     {8192, 1664, 300, 0, 0, CTR_GEMM_SPLIT_BF16, 1, 1},   // dX  = dH1.W0
     {200, 300, 8192, 1, 0, CTR_GEMM_EXACT_F32, 0, 16},    // dW1 = dH2^T.H1
-    {300, 1664, 8192, 1, 0, CTR_GEMM_SPLIT_BF16, 1, 16},  // dW0 = dH1^T.X
+    {300, 1664, 8192, 1, 0, CTR_GEMM_SPLIT_BF16, 7, 8},   // dW0 = dH1^T.X (160x128 tiles)
     {4096, 1024, 741, 0, 1, CTR_GEMM_SPLIT_BF16, 2, 1},   // PG policy fwd0
     {1024, 741, 4096, 1, 0, CTR_GEMM_SPLIT_BF16, 3, 4},   // dW0
     {4096, 512, 1024, 0, 1, CTR_GEMM_SPLIT_BF16, 0, 1},   // fwd1

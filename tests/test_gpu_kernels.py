@@ -198,7 +198,7 @@ def _gemm_tilings(n_tiles, algo_name):
 
 
 # every compiled tiling of csrc/gemm.hip (kTiles) and csrc/gemm_sb16.hip (kSb16)
-@pytest.mark.parametrize("algo,tile", _gemm_tilings(10, "exact") + _gemm_tilings(7, "split"))
+@pytest.mark.parametrize("algo,tile", _gemm_tilings(10, "exact") + _gemm_tilings(8, "split"))
 def test_gemm_every_tiling(cuda, algo, tile, monkeypatch):
     """Force each tiling (and split-K) on shapes with M/N edges and K tails, both the float4
     path (extents % 4 == 0) and the scalar path, every transpose: fp32 parity vs fp64."""
