@@ -125,7 +125,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
                                   grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
         self._span("scatter", t)
-        hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
+        if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream (joined below)
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         # 5. gradients to the owners, summed per row in (source rank, position) order
         t = self._mark("exchange")
         G = alltoallv(b.grad_rows, send_c, recv_c, self.group)

@@ -400,7 +400,8 @@ class FusedCTRTrainer:
             hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
                                       grad_rows=b.grad_rows, grad_lin=b.grad_lin)
         self._span("scatter", t)
-        hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
+        if self.kind == "FM":  # MLP kinds: on the weight-gradient stream, off this chain
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         grad_rows, grad_lin, plan = b.grad_rows, (b.grad_lin if w is not None else None), b.plan
         if ws > 1:
             self._join_wgrad()  # the exchange all-reduces the dense gradient
@@ -483,6 +484,7 @@ class FusedCTRTrainer:
         with torch.cuda.stream(side) if side is not None else _nullctx():
             # the small reductions in one launch pair: Linear(200,1) dW = gz^T H2 and
             # db = sum gz; Linear(300,200) db1 = colsum dH2; Linear(F*K,300) db0 = colsum dH1
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
             hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
                                   (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
                                   (dh2, None, gv["mlp.3.bias"]),
