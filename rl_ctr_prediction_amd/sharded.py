@@ -120,7 +120,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             gz = b.fm.gz
         else:
             gz = self._deepfm_forward_backward(ids, y, b, T, T_lin, bias, mean_div)
-        hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream
+            hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         t = self._mark("scatter")
         hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
                                   grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)

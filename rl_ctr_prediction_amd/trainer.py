@@ -388,7 +388,7 @@ class FusedCTRTrainer:
             gz = b.fm.gz
         else:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
-        if bias is not None:
+        if self.kind == "FM":  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         if self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)  # the plan
@@ -469,6 +469,22 @@ class FusedCTRTrainer:
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], z_fm, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
         gz, dh2 = head["gz"], head["dh_pre"]
+        # the weight / bias gradients are needed only by the dense Adam at the end of the
+        # step: they run on one side stream, the small layers' from the head on (under the
+        # dH1 / dX GEMMs), dW0 from dX on (under the scatter and the embedding Adam)
+        side = self._wgrad_stream
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
+            if "bias" in gv:  # DeepFM's FM bias: sum gz
+                hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+            # Linear(200,1): dW = gz^T H2, db = sum gz; Linear(300,200): db1 = colsum dH2
+            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
+                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
+                                  (dh2, None, gv["mlp.3.bias"])])
+            # Linear(300,200): dW1 = dH2^T H1
+            self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
                    scale=1.0 / (1.0 - p0), out=b.dh1)
@@ -476,21 +492,11 @@ class FusedCTRTrainer:
         self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
             hip_ops.ipnn_backward(x, E, b.dx, out=b.dslot)
-        # the weight / bias gradients are needed only by the dense Adam at the end of the
-        # step: on the side stream they run under the scatter and the embedding Adam
-        side = self._wgrad_stream
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            # the small reductions in one launch pair: Linear(200,1) dW = gz^T H2 and
-            # db = sum gz; Linear(300,200) db1 = colsum dH2; Linear(F*K,300) db0 = colsum dH1
-            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
-            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
-                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
-                                  (dh2, None, gv["mlp.3.bias"]),
-                                  (b.dh1, None, gv["mlp.0.bias"])])
-            # Linear(300,200): dW1 = dH2^T H1; Linear(F*K,300): dW0 = dH1^T X
-            self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
+            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X
+            hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
             self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
         return gz
 
