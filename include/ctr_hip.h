@@ -158,6 +158,12 @@ int64_t ctr_colsum_multi_workspace_bytes(int n_jobs, const ctr_colsum_job* jobs)
 int ctr_colsum_multi_f32(int n_jobs, const ctr_colsum_job* jobs, void* ws, int64_t ws_bytes,
                          ctr_stream_t stream);
 
+/* dst[c * ld_dst + r] = src[r * ld_src + c] (r < rows, c < cols), bit-exact copy: dH1^T and
+ * X^T for the k-contiguous dW0 = dH1^T X GEMM of DeepFM / IPNN (p_model.py:279-293, the
+ * weight gradient autograd forms for mlp.0). */
+int ctr_transpose_f32(const float* src, int64_t rows, int64_t cols, int64_t ld_src, float* dst,
+                      int64_t ld_dst, ctr_stream_t stream);
+
 /* ------------------------------------------------ A3: embedding scatter-add -----------
  * A sparse plan groups the S = B*F slots (slot s = b*F + f) of a batch by feature id.
  * All arrays are caller-owned device buffers of S int32 (seg_offsets: S+1, num_unique: 1):

@@ -62,6 +62,7 @@ SIGNATURES = {
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),
     "ctr_colsum_multi_workspace_bytes": (_i64, [_i32, _job_p]),
     "ctr_colsum_multi_f32": (_i32, [_i32, _job_p, _vp, _i64, _vp]),
+    "ctr_transpose_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "ctr_sparse_plan_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sparse_plan_build": (_i32, [_vp, _i32, _i64, _plan_p, _vp, _i64, _vp, _vp]),
     "ctr_plan_slot_to_unique": (_i32, [_plan_p, _vp, _vp]),

@@ -15,7 +15,7 @@ from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS
 
 __all__ = [
     "embedding_gather", "fm_forward", "bce_sigmoid", "deepfm_head", "gemm", "linear",
-    "tensor_sum", "colsum", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
+    "tensor_sum", "colsum", "transpose", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
     "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
@@ -242,6 +242,23 @@ def colsum(X: torch.Tensor, row_w: torch.Tensor | None = None, scale: float = 1.
     ws = Workspace.get(lib.ctr_reduce_workspace_bytes(M, N), X.device)
     lib.ctr_colsum_f32(_p(X), M, N, X.stride(0), _p(row_w), float(scale), _p(out), _p(ws),
                        ws.numel(), _stream())
+    return out
+
+
+def transpose(src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[c, r] = src[r, c] (bit-exact; src rows may be strided, out contiguous)."""
+    _dev(src, "src")
+    if src.dtype != torch.float32:
+        raise TypeError(f"src: expected float32, got {src.dtype}")
+    R, Cn = src.shape
+    if src.numel() and src.stride(1) != 1:
+        raise ValueError("transpose: src rows must be contiguous")
+    if out is None:
+        out = torch.empty(Cn, R, dtype=torch.float32, device=src.device)
+    if tuple(out.shape) != (Cn, R) or (out.numel() and out.stride(1) != 1):
+        raise ValueError(f"transpose: out must be a row-contiguous [{Cn}, {R}] tensor")
+    lib.ctr_transpose_f32(_p(src), R, Cn, max(src.stride(0), Cn), _p(out), max(out.stride(0), R),
+                          _stream())
     return out
 
 

@@ -26,6 +26,7 @@ Optimizer modes (identical results, bitwise — tests/test_gpu_deferred.py):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -62,6 +63,8 @@ class _Bufs:
     head: dict | None = None
     dh1: torch.Tensor | None = None
     dx: torch.Tensor | None = None
+    xT: torch.Tensor | None = None     # MLP input, transposed [W, B] (k-contiguous dW0)
+    dh1T: torch.Tensor | None = None   # dH1 transposed [H1, B]
     loss: torch.Tensor | None = None
     gplan: hip_ops.SparsePlanBuffers | None = None
     g_rows: torch.Tensor | None = None
@@ -146,6 +149,9 @@ class FusedCTRTrainer:
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self._wgrad_stream = (torch.cuda.Stream(device=self.device) if self.kind in _MLP_KINDS
                               else None)
+        # dW0 = dH1^T X on transposed copies of both operands (k-contiguous GEMM operands,
+        # csrc/layout.hip); CTR_DW0_KC=0 keeps the strided form (A/B only)
+        self.dw0_kc = os.environ.get("CTR_DW0_KC", "1") != "0"
         self._sweep_stream = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
@@ -270,6 +276,8 @@ class FusedCTRTrainer:
             mlp = self.model.mlp
             H1, H2 = mlp[0].out_features, mlp[3].out_features
             b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, W)
+            if self.dw0_kc:
+                b.xT, b.dh1T = e(W, B), e(H1, B)
             if self.kind == "IPNN":
                 b.dslot = e(S, K)
                 b.zero = torch.zeros(B, dtype=torch.float32, device=dev)
@@ -485,6 +493,8 @@ class FusedCTRTrainer:
                                   (dh2, None, gv["mlp.3.bias"])])
             # Linear(300,200): dW1 = dH2^T H1
             self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
+            if self.dw0_kc:  # X^T for dW0, beside the dH1 / dX GEMMs
+                hip_ops.transpose(X, out=b.xT)
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
                    scale=1.0 / (1.0 - p0), out=b.dh1)
@@ -492,13 +502,23 @@ class FusedCTRTrainer:
         self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
             hip_ops.ipnn_backward(x, E, b.dx, out=b.dslot)
+        self._dw0(side, b, X, gv)  # after dX: forking dW0 beside dX measured slower
+        return gz
+
+    def _dw0(self, side, b: _Bufs, X, gv) -> None:
+        """mlp.0's weight / bias gradients on the weight-gradient stream, under the scatter
+        chain. k-contiguous form (default): 11.5 -> 11.7 M ex/s at C3 (interleaved A/B, 3
+        runs each); dW0 itself 120 -> 77 us in the step, the transposes ride beside dX."""
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side) if side is not None else _nullctx():
             # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X
             hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
-            self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
-        return gz
+            if self.dw0_kc:  # both operands k-contiguous (csrc/layout.hip)
+                hip_ops.transpose(b.dh1, out=b.dh1T)
+                self._gemm(b.dh1T, b.xT, trans_b=True, out=gv["mlp.0.weight"])
+            else:
+                self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""

@@ -484,3 +484,16 @@ def test_colsum_multi_is_bitwise_colsum(cuda):
     H.colsum_multi([(X, w, o) for (X, w), o in zip(jobs, outs)])
     for (X, w), o in zip(jobs, outs):
         assert torch.equal(o, H.colsum(X, row_w=w)), X.shape
+
+
+@pytest.mark.parametrize("shape", [(8192, 300), (8192, 1989), (200, 1664), (4, 8), (70, 130),
+                                   (1, 1), (64, 1), (3, 200), (0, 5)])
+def test_transpose_bitwise(cuda, shape):
+    """ctr_transpose_f32 (dH1^T / X^T for the k-contiguous dW0): a bit-exact copy, ragged
+    tiles and strided source rows included."""
+    H = _hip()
+    g = torch.Generator().manual_seed(shape[0] + shape[1])
+    X = torch.randn(*shape, generator=g).to(cuda)
+    assert torch.equal(H.transpose(X), X.t().contiguous())
+    if shape[0] and shape[1] > 2:  # a column slice: ld_src > cols
+        assert torch.equal(H.transpose(X[:, 1:-1]), X[:, 1:-1].t().contiguous())

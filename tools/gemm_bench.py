@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--algo", default="split", choices=["exact", "split"])
     ap.add_argument("--c4", action="store_true", help="the C4 policy-MLP shapes instead")
     ap.add_argument("--configs", default=None)
+    ap.add_argument("--dw0-layouts", action="store_true",
+                    help="dW0 as stored today (TN) vs with both operands pre-transposed (NT)")
     ap.add_argument("--square", type=int, default=0,
                     help="time only an NxNxN NN product (kernel's intrinsic rate)")
     args = ap.parse_args()
@@ -50,6 +52,10 @@ def main():
             if i > 0:
                 SHAPES[f"dX{i} {n}->{k}"] = (b, k, n, False, False)
             SHAPES[f"dW{i} {k}x{n}"] = (n, k, b, True, False)
+    if args.dw0_layouts:
+        SHAPES.clear()
+        SHAPES["dW0 TN (dH1, X as stored)"] = (300, 1664, B, True, False)
+        SHAPES["dW0 NT (dH1^T, X^T pre-transposed)"] = (300, 1664, B, False, True)
     if args.square:
         n = args.square
         SHAPES.clear()
@@ -57,7 +63,7 @@ def main():
         SHAPES[f"square {n} NT"] = (n, n, n, False, True)
         SHAPES[f"square {n} TN"] = (n, n, n, True, False)
     if args.configs is None:
-        nt = 10 if args.algo == "exact" else 7
+        nt = 10 if args.algo == "exact" else 8
         args.configs = "auto," + ",".join(f"{t}x{s}" for t in range(nt) for s in (1, 2, 4, 8, 16))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
