@@ -135,6 +135,60 @@ int ctr_gemm_f32_ex(int algo, int trans_a, int trans_b, int64_t M, int64_t N, in
 /* The algorithm CTR_GEMM_AUTO (or any value) resolves to in this process. */
 int ctr_gemm_resolved_algo(int algo);
 
+/* ------------------------------------------- A2: MLP GEMM on pre-split planes -------
+ * The fused trainer's MLP GEMMs (the six products of DeepFM's / InnerPNN's MLP per step,
+ * p_model.py:276-293,322 forward and backward). An fp32 matrix travels as its exact
+ * three-plane bf16 split x = x0 + x1 + x2 (CTR_GEMM_SPLIT_BF16's numerics), written once
+ * by its producer, so the GEMM stages operands by LDS-DMA without any split work.
+ *
+ * ctr_planes: bf16 bits [3][rows][cols] with row stride `ld` and plane stride
+ * `plane_stride` (elements); `rows`/`cols` = the allocated storage extents. CONTRACT: the
+ * storage beyond the matrix's logical extent is ZERO and stays zero (the GEMM reads whole
+ * 32-deep k tiles), ld % 8 == 0, data 16-B aligned.
+ *
+ * ctr_split_planes: planes of src [rows, cols] (row stride ld); writes the valid region.
+ *
+ * ctr_gemm_planes: C[M,N] = A.B with the ctr_gemm_f32 epilogues. Orientation per operand:
+ *   a_rc = 0: A stored [M][K] (k contiguous)     a_rc = 1: A stored [K][M] (A^T product)
+ *   b_rc = 0: B stored [N][K] (nn.Linear weight) b_rc = 1: B stored [K][N]
+ * Storage must cover align_up(K, 32) along k, zero-padded. Outputs: C (fp32, ldc) and/or Cp
+ * (the planes of the epilogue's result, for the next GEMM). Split-K scratch is sized by
+ * ctr_gemm_planes_workspace_bytes. ctr_gemm_planes_config reports the tiling chosen
+ * (tuning and tests). */
+typedef struct ctr_planes {
+  void* data;
+  int64_t ld;
+  int64_t plane_stride;
+  int64_t rows;
+  int64_t cols;
+} ctr_planes;
+int ctr_split_planes(const float* src, int64_t rows, int64_t cols, int64_t ld,
+                     const ctr_planes* dst, ctr_stream_t stream);
+int64_t ctr_gemm_planes_workspace_bytes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K);
+int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                    const ctr_planes* A, const ctr_planes* B, float* C, int64_t ldc,
+                    const ctr_planes* Cp, int epi, const float* bias, const float* aux,
+                    int64_t ldaux, float scale, float drop_p, uint64_t seed, uint64_t offset,
+                    const int32_t* step_ptr, void* ws, int64_t ws_bytes, ctr_stream_t stream);
+int ctr_gemm_planes_config(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K, int* tile,
+                           int* splits, int* bm, int* bn);
+
+/* The producers of the MLP's GEMM operands writing planes directly (no fp32 round trip):
+ * ctr_fm_forward_planes: ctr_fm_forward (no BCE head; DeepFM's FM part) whose flattened
+ *   embeddings (emb_out [B, F*K]) are written as planes; needs K % 4 == 0, (K/4) | 64,
+ *   F <= 64. Replaces: p_model.py:303,320 (the two gathers of DeepFM.forward).
+ * ctr_deepfm_head_planes: ctr_deepfm_head with labels, writing dh_pre [B, H] in fp32 and
+ *   as planes (the dH1 / dW1 GEMM operand). Replaces: p_model.py:290-293,322 backward. */
+int ctr_fm_forward_planes(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                          const float* emb, const float* lin, const float* bias, float* z,
+                          float* sum_e, const ctr_planes* emb_planes, int32_t* err_flag,
+                          ctr_stream_t stream);
+int ctr_deepfm_head_planes(const float* h, int64_t B, int H, const float* w_out,
+                           const float* b_out, const float* z_fm, const float* labels,
+                           float mean_div, float drop_scale, float* z, float* p, float* loss_elem,
+                           float* gz, float* dh_pre, const ctr_planes* dh_planes,
+                           ctr_stream_t stream);
+
 /* Deterministic reductions (fixed order; identical bits run to run).
  * ctr_sum_f32:    out[0] = scale * sum_i x[i]
  * ctr_colsum_f32: out[n] = scale * sum_m (row_w ? row_w[m] : 1) * X[m,n]   (bias / dW of

@@ -37,6 +37,15 @@ class ColsumJob(C.Structure):
 
 _job_p = C.POINTER(ColsumJob)
 
+
+class PlanesDesc(C.Structure):
+    """Mirror of ``ctr_planes`` (include/ctr_hip.h)."""
+    _fields_ = [("data", _vp), ("ld", _i64), ("plane_stride", _i64), ("rows", _i64),
+                ("cols", _i64)]
+
+
+_planes_p = C.POINTER(PlanesDesc)
+
 # name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
 # against the header.
 SIGNATURES = {
@@ -57,6 +66,16 @@ SIGNATURES = {
                                _i64, _i32, _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp,
                                _i64, _vp]),
     "ctr_gemm_resolved_algo": (_i32, [_i32]),
+    "ctr_split_planes": (_i32, [_vp, _i64, _i64, _i64, _planes_p, _vp]),
+    "ctr_gemm_planes_workspace_bytes": (_i64, [_i32, _i32, _i64, _i64, _i64]),
+    "ctr_gemm_planes": (_i32, [_i32, _i32, _i64, _i64, _i64, _planes_p, _planes_p, _vp, _i64,
+                               _planes_p, _i32, _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp,
+                               _i64, _vp]),
+    "ctr_gemm_planes_config": (_i32, [_i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "ctr_fm_forward_planes": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp,
+                                     _planes_p, _vp, _vp]),
+    "ctr_deepfm_head_planes": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp,
+                                      _vp, _vp, _vp, _planes_p, _vp]),
     "ctr_reduce_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sum_f32": (_i32, [_vp, _i64, _f32, _vp, _vp, _i64, _vp]),
     "ctr_colsum_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _f32, _vp, _vp, _i64, _vp]),

@@ -89,6 +89,54 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// ------------------------------------------- exact three-plane bf16 split (MLP) -----
+// x = x0 + x1 + x2, x0 = bf16_rne(x), x1 = bf16_rne(x - x0), x2 = x - x0 - x1 (exact: the
+// residuals have <= 16 and <= 8 significant bits); x0 + (x1 + x2) == x in fp32. The planes
+// feed the split-bf16 MLP GEMM (csrc/gemm_planes.hip); producers write them directly.
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pbf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t psplit_pair(float x, float y, float& rx, float& ry) {
+  const pbf16x2 hv = __builtin_convertvector((pf32x2){x, y}, pbf16x2);
+  const pf32x2 hf = __builtin_convertvector(hv, pf32x2);
+  rx = x - hf.x;
+  ry = y - hf.y;
+  return __builtin_bit_cast(uint32_t, hv);
+}
+
+__device__ __forceinline__ uint32_t ppack_pair(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((pf32x2){x, y}, pbf16x2));
+}
+
+// four consecutive elements -> their 8-byte piece of each plane
+__device__ __forceinline__ void psplit4(float4 v, uint2 (&o)[3]) {
+  float r0, r1, r2, r3, q0, q1, q2, q3;
+  o[0].x = psplit_pair(v.x, v.y, r0, r1);
+  o[0].y = psplit_pair(v.z, v.w, r2, r3);
+  o[1].x = psplit_pair(r0, r1, q0, q1);
+  o[1].y = psplit_pair(r2, r3, q2, q3);
+  o[2].x = ppack_pair(q0, q1);
+  o[2].y = ppack_pair(q2, q3);
+}
+
+__device__ __forceinline__ void psplit1(float v, uint16_t (&o)[3]) {
+  const __bf16 h0 = (__bf16)v;
+  const float r = v - (float)h0;
+  const __bf16 h1 = (__bf16)r;
+  const __bf16 h2 = (__bf16)(r - (float)h1);
+  o[0] = __builtin_bit_cast(uint16_t, h0);
+  o[1] = __builtin_bit_cast(uint16_t, h1);
+  o[2] = __builtin_bit_cast(uint16_t, h2);
+}
+
+// store the planes of 4 consecutive elements at (row base) + p * ps
+__device__ __forceinline__ void store_planes4_at(uint16_t* base, int64_t ps, float4 v) {
+  uint2 pl[3];
+  psplit4(v, pl);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * ps) = pl[p];
+}
+
 // -------------------------------------------- BCE after sigmoid (reference exact) ---
 // torch.sigmoid then nn.BCELoss(mean) then autograd, UNFUSED, in
 // ATen's own operation order (checked bit-exact on CPU, tests/test_oracle.py):

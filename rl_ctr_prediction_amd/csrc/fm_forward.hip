@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256) void fm_forward_vec(
     const float* __restrict__ lin, const float* __restrict__ bias, float* __restrict__ z_out,
     float4* __restrict__ sum_out, float4* __restrict__ emb_out, const float* __restrict__ labels,
     float mean_div, float* __restrict__ p_out, float* __restrict__ loss_out,
-    float* __restrict__ gz_out, int32_t* err) {
+    float* __restrict__ gz_out, int32_t* err, uint16_t* __restrict__ xpl, int64_t xpl_ld,
+    int64_t xpl_ps) {
   constexpr int RPI = kWave / K4;
   constexpr int MAXIT = (FMAX + RPI - 1) / RPI;
   const int lane = threadIdx.x & (kWave - 1);
@@ -89,6 +90,8 @@ __global__ __launch_bounds__(256) void fm_forward_vec(
       q.x += e[it].x * e[it].x; q.y += e[it].y * e[it].y;
       q.z += e[it].z * e[it].z; q.w += e[it].w * e[it].w;
       if (emb_out) emb_out[(b * F + f) * K4 + c] = e[it];
+      // DeepFM's MLP input as its three bf16 planes (csrc/gemm_planes.hip's operand)
+      if (xpl) store_planes4_at(xpl + b * xpl_ld + (int64_t)f * (4 * K4) + 4 * c, xpl_ps, e[it]);
     }
   }
   // Sum over the RPI lanes that share column c (lanes c, c+K4, c+2*K4, ...).
@@ -191,7 +194,8 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
     const float* __restrict__ h, int64_t B, int H, const float* __restrict__ w,
     const float* __restrict__ bo, const float* __restrict__ z_fm, const float* __restrict__ y,
     float mean_div, float drop_scale, float* z_out, float* p_out, float* loss_out,
-    float* gz_out, float* __restrict__ dh_pre) {
+    float* gz_out, float* __restrict__ dh_pre, uint16_t* __restrict__ dpl, int64_t dpl_ld,
+    int64_t dpl_ps) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
   if (b >= B) return;
@@ -216,7 +220,16 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
   }
   if (dh_pre && y) {
     float* d = dh_pre + b * H;
-    for (int j = lane; j < H; j += kWave) d[j] = hb[j] > 0.f ? (g * w[j]) * drop_scale : 0.f;
+    for (int j = lane; j < H; j += kWave) {
+      const float v = hb[j] > 0.f ? (g * w[j]) * drop_scale : 0.f;
+      d[j] = v;
+      if (dpl) {  // dH2's planes for the dH1 / dW1 GEMMs (csrc/gemm_planes.hip)
+        uint16_t h3[3];
+        psplit1(v, h3);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) dpl[p * dpl_ps + b * dpl_ld + j] = h3[p];
+      }
+    }
   }
 }
 
@@ -270,7 +283,8 @@ template <typename IdxT>
 static int launch_fm_forward(const IdxT* idx, int64_t B, int F, int K, int64_t V,
                              const float* emb, const float* lin, const float* bias, float* z,
                              float* sum_e, float* emb_out, const float* labels, float mean_div,
-                             float* p, float* loss, float* gz, int32_t* err, hipStream_t st) {
+                             float* p, float* loss, float* gz, int32_t* err, hipStream_t st,
+                             const ctr_planes* xpl = nullptr) {
   const int waves_per_block = 4;
   const dim3 grid((unsigned)ceil_div(B, waves_per_block)), block(256);
   const bool vec_ok = (K % 4 == 0) && (kWave % (K / 4) == 0) && F <= 64 &&
@@ -281,7 +295,9 @@ static int launch_fm_forward(const IdxT* idx, int64_t B, int F, int K, int64_t V
   hipLaunchKernelGGL((fm_forward_vec<IdxT, K4_, FMAX_>), grid, block, 0, st, idx, B, F, V,  \
                      reinterpret_cast<const float4*>(emb), lin, bias, z,                    \
                      reinterpret_cast<float4*>(sum_e), reinterpret_cast<float4*>(emb_out),  \
-                     labels, mean_div, p, loss, gz, err)
+                     labels, mean_div, p, loss, gz, err,                                    \
+                     xpl ? static_cast<uint16_t*>(xpl->data) : nullptr, xpl ? xpl->ld : 0,  \
+                     xpl ? xpl->plane_stride : 0)
   if (vec_ok) {
     const int K4 = K / 4;
     const bool f32 = F <= 32;
@@ -300,6 +316,7 @@ static int launch_fm_forward(const IdxT* idx, int64_t B, int F, int K, int64_t V
     return CTR_OK;
   }
 generic:
+  CTR_REQUIRE(!xpl, "ctr_fm_forward_planes: needs K %% 4 == 0, (K/4) | 64, F <= 64, 16-B rows");
   hipLaunchKernelGGL((fm_forward_generic<IdxT>), grid, block, 0, st, idx, B, F, K, V, emb, lin,
                      bias, z, sum_e, emb_out, labels, mean_div, p, loss, gz, err);
   CTR_LAUNCH_CHECK("fm_forward_generic");
@@ -366,6 +383,30 @@ extern "C" int ctr_fm_forward(const void* idx, int idx_type, int64_t B, int F, i
                            sum_e, emb_out, labels, mean_div, p, loss_elem, gz, err_flag, st);
 }
 
+extern "C" int ctr_fm_forward_planes(const void* idx, int idx_type, int64_t B, int F, int K,
+                                     int64_t V, const float* emb, const float* lin,
+                                     const float* bias, float* z, float* sum_e,
+                                     const ctr_planes* emb_planes, int32_t* err_flag,
+                                     ctr_stream_t stream) {
+  CTR_REQUIRE(idx && emb && lin && bias && emb_planes && emb_planes->data,
+              "ctr_fm_forward_planes: null pointer");
+  CTR_REQUIRE(B >= 0 && F > 0 && K > 0 && V > 0 && V < (int64_t(1) << 31),
+              "ctr_fm_forward_planes: bad sizes");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  CTR_REQUIRE(emb_planes->rows >= B && emb_planes->cols >= (int64_t)F * K &&
+                  emb_planes->ld % 4 == 0 && (uintptr_t)emb_planes->data % 8 == 0,
+              "ctr_fm_forward_planes: planes must hold [B, F*K] with 8-B aligned rows");
+  if (B == 0) return CTR_OK;
+  hipStream_t st = as_stream(stream);
+  if (idx_type == CTR_IDX_I64)
+    return launch_fm_forward(static_cast<const int64_t*>(idx), B, F, K, V, emb, lin, bias, z,
+                             sum_e, nullptr, nullptr, 1.f, nullptr, nullptr, nullptr, err_flag, st,
+                             emb_planes);
+  return launch_fm_forward(static_cast<const int32_t*>(idx), B, F, K, V, emb, lin, bias, z, sum_e,
+                           nullptr, nullptr, 1.f, nullptr, nullptr, nullptr, err_flag, st,
+                           emb_planes);
+}
+
 extern "C" int ctr_bce_sigmoid(const float* z, const float* labels, int64_t B, float mean_div,
                                float* p, float* loss_elem, float* gz, ctr_stream_t stream) {
   CTR_REQUIRE(z && labels, "ctr_bce_sigmoid: null pointer");
@@ -388,8 +429,27 @@ extern "C" int ctr_deepfm_head(const float* h, int64_t B, int H, const float* w_
   if (B == 0) return CTR_OK;
   hipLaunchKernelGGL(deepfm_head_kernel, (unsigned)ceil_div(B, 4), 256, 0, as_stream(stream), h,
                      B, H, w_out, b_out, z_fm, labels, mean_div, drop_scale, z, p, loss_elem, gz,
-                     dh_pre);
+                     dh_pre, nullptr, 0, 0);
   CTR_LAUNCH_CHECK("ctr_deepfm_head");
+  return CTR_OK;
+}
+
+extern "C" int ctr_deepfm_head_planes(const float* h, int64_t B, int H, const float* w_out,
+                                      const float* b_out, const float* z_fm, const float* labels,
+                                      float mean_div, float drop_scale, float* z, float* p,
+                                      float* loss_elem, float* gz, float* dh_pre,
+                                      const ctr_planes* dh_planes, ctr_stream_t stream) {
+  CTR_REQUIRE(h && w_out && b_out && z_fm && labels && dh_pre && dh_planes && dh_planes->data,
+              "ctr_deepfm_head_planes: null pointer");
+  CTR_REQUIRE(B >= 0 && H > 0 && mean_div > 0.f, "ctr_deepfm_head_planes: bad sizes");
+  CTR_REQUIRE(dh_planes->rows >= B && dh_planes->cols >= H && dh_planes->ld >= H,
+              "ctr_deepfm_head_planes: planes smaller than dh [B, H]");
+  if (B == 0) return CTR_OK;
+  hipLaunchKernelGGL(deepfm_head_kernel, (unsigned)ceil_div(B, 4), 256, 0, as_stream(stream), h,
+                     B, H, w_out, b_out, z_fm, labels, mean_div, drop_scale, z, p, loss_elem, gz,
+                     dh_pre, static_cast<uint16_t*>(dh_planes->data), dh_planes->ld,
+                     dh_planes->plane_stride);
+  CTR_LAUNCH_CHECK("ctr_deepfm_head_planes");
   return CTR_OK;
 }
 

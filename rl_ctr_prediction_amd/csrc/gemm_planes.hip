@@ -1,0 +1,719 @@
+// fp32-accurate GEMM on PRE-SPLIT operand planes — the DeepFM / IPNN MLP of the fused
+// training step (p_model.py:276-293,322: Linear(F*K,300) -> Linear(300,200) -> Linear(200,1),
+// forward and backward: 6 GEMMs per step, SURVEY.md §8d C3: 27.5 GFLOP).
+//
+// Numerics (as csrc/gemm_sb16.hip): every fp32 operand x is split EXACTLY into three bf16
+// planes x = x0 + x1 + x2 (x0 = bf16_rne(x), x1 = bf16_rne(x - x0), x2 = x - x0 - x1); a
+// product sums the six plane products with i + j <= 2 on the bf16 matrix cores, fp32
+// accumulation (a0b0 in one accumulator, the five smaller products in a second; the
+// dropped terms are <= 2^-23 |ab|). The fp32 value is recovered exactly as x0 + (x1 + x2).
+//
+// What is different here: the operands arrive ALREADY split, written once by their
+// producers (the forward gather writes the MLP input's planes, each GEMM epilogue and the
+// head kernel write the planes of the activations / gradients they produce, the weights
+// are split once per step). A plane tensor is bf16 [3][rows_pad][cols_pad], rows and
+// columns padded to multiples of 32 with ZEROS, so the k loop never has a tail and the
+// kernel's staging is pure data movement: LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction) straight into a 3-deep LDS ring, no VALU split, no register staging.
+// Operands are read in the orientation they are stored in:
+//   KC (k contiguous: X [B][F*K] for fwd0, nn.Linear weights [out][in]):
+//       LDS image [rows][32 k] per plane, fragments by ds_read_b128;
+//   RC (rows contiguous, k strided: W0 [300][1664] as dX's B operand, dH1 / X as dW0's
+//       operands — the transposed products of the backward):
+//       LDS image [32 k][rows] per plane, fragments by ds_read_b64_tr_b16 (the hardware
+//       transpose read), so no transposed copy of any operand is ever written.
+// Both images are XOR-swizzled (on the DMA's per-lane SOURCE address; the DMA destination is
+// lane-linear) so that every fragment read is bank-conflict free.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 — a 32-deep k step per instruction (one LDS stage), 16-row
+// granularity (N = 300 pads to 320, not 384), and per the MI355X measurements the shape the
+// chip holds the higher clock on.
+#include "gemm_common.h"
+
+namespace ctr {
+
+typedef __bf16 pbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 pbf16x4 __attribute__((ext_vector_type(4)));
+typedef float pf32x4 __attribute__((ext_vector_type(4)));
+#define CTR_LDS __attribute__((address_space(3)))
+
+constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
+
+struct PlaneSrc {
+  const uint16_t* p;  // plane 0 (bf16 bits); planes `ps` elements apart
+  int64_t ld;         // elements per storage row
+  int64_t ps;         // elements between planes
+  int64_t rows;       // storage rows
+  int64_t cols;       // storage columns
+};
+
+struct PlanesArgs {
+  int64_t Kp;           // padded k extent (multiple of 32)
+  int64_t k_per_split;  // multiple of 32
+  PlaneSrc A, B;
+  GemmArgs g;           // M, N, C, ldc, epilogue, split-K slab stride
+  uint16_t* cpl;        // output planes (nullptr: none)
+  int64_t cpl_ld, cpl_ps;
+};
+
+// ---- LDS image swizzles ----------------------------------------------------------------
+// KC image: [rows][32 k] bf16 = 64-B rows, four 16-B chunks. The 16x16x32 A/B fragment of
+// lane l is row (l & 15), chunk (l >> 4); a ds_read_b128 is serviced in 16-lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... The chunk is XORed with g(row quad) where
+// g = {0, 2, 3, 1}: every group then touches 16 distinct 16-B slots of a 256-B bank row.
+__device__ __forceinline__ int kc_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+// RC image: [32 k][R] bf16, R in {64, 128} (128- or 256-B rows) in 32-B blocks of 16
+// columns. A ds_read_b64_tr_b16 16-lane group reads 4 k rows x one block; the two groups of
+// a 32-lane half read k rows {4j..4j+3} and {8+4j..8+4j+3} of the same block. The block is
+// XORed with a key of the row that spreads those 8 rows over 8 distinct 32-B slots.
+template <int R>
+__device__ __forceinline__ int rc_swz(int k) {
+  if (R == 128) return (k & 3) | (((k >> 3) & 1) << 2);
+  return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);  // R == 64: two rows per bank row
+}
+
+// ---- LDS-DMA source addresses (one lane's 16 B of a 1 KiB piece) -------------------
+// KC: piece c covers image rows 16c..16c+15, lane -> (row lane/4, swizzled chunk lane%4).
+__device__ __forceinline__ const uint16_t* piece_kc(const PlaneSrc& s, int plane, int c,
+                                                    int64_t row0, int64_t k0, int lane) {
+  const int r = c * 16 + (lane >> 2);
+  const int ch = (lane & 3) ^ kc_swz(r);
+  int64_t row = row0 + r;
+  row = row < s.rows ? row : s.rows - 1;  // clamped rows only feed never-stored outputs
+  return s.p + plane * s.ps + row * s.ld + k0 + 8 * ch;
+}
+
+// RC: piece c covers image rows c*RPI .. +RPI-1 (k), lane -> (row, 16-B piece of the row).
+template <int R>
+__device__ __forceinline__ const uint16_t* piece_rc(const PlaneSrc& s, int plane, int c,
+                                                    int64_t col0, int64_t k0, int lane) {
+  constexpr int PPR = R / 8;     // 16-B pieces per image row
+  constexpr int RPI = 64 / PPR;  // image rows per 1 KiB piece
+  const int kr = c * RPI + lane / PPR;
+  const int pc = lane % PPR;
+  const int blk = (pc >> 1) ^ rc_swz<R>(kr);
+  int64_t col = col0 + 16 * blk;
+  col = col <= s.cols - 16 ? col : s.cols - 16;
+  return s.p + plane * s.ps + (k0 + kr) * s.ld + col + 8 * (pc & 1);
+}
+
+// ---- fragment reads ---------------------------------------------------------------
+// Byte offsets (within one plane image) of a lane's fragment reads: computed once per
+// kernel, so the k loop issues bare LDS reads.
+__device__ __forceinline__ int frag_kc_off(int rb, int lane) {
+  const int r = rb + (lane & 15);
+  return r * 64 + ((lane >> 4) ^ kc_swz(r)) * 16;
+}
+
+template <int R>
+__device__ __forceinline__ int frag_rc_off(int cb, int lane, int j) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int k = 8 * g + 4 * j + q;
+  return k * (2 * R) + 32 * ((cb >> 4) ^ rc_swz<R>(k)) + 8 * pp;
+}
+
+__device__ __forceinline__ pbf16x8 frag_kc_at(const char* p) {
+  return *reinterpret_cast<const pbf16x8*>(p);
+}
+
+__device__ __forceinline__ pbf16x8 frag_rc_at(const char* p0, const char* p1) {
+  const pbf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CTR_LDS pbf16x4*)p0);
+  const pbf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CTR_LDS pbf16x4*)p1);
+  return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// ---- epilogue --------------------------------------------------------------------
+__device__ __forceinline__ void store_planes4(const PlanesArgs& a, int64_t m, int64_t n, float4 o) {
+  uint16_t* base = a.cpl + m * a.cpl_ld + n;
+  if (n + 3 < a.g.N) {
+    uint2 pl[3];
+    psplit4(o, pl);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * a.cpl_ps) = pl[p];
+  } else {
+    const float e[4] = {o.x, o.y, o.z, o.w};
+    for (int j = 0; j < 4 && n + j < a.g.N; ++j) {
+      uint16_t h[3];
+      psplit1(e[j], h);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) base[p * a.cpl_ps + j] = h[p];
+    }
+  }
+}
+
+// one wave's TM x TN 16x16 accumulators (C/D map: col = lane & 15, row = 4*(lane>>4) + r)
+// through a wave-private [16][WN+4] LDS strip, then row-contiguous float4 stores
+template <int TM, int TN>
+__device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[TM][TN],
+                                             float* strip, int64_t mb, int64_t nb, int lane) {
+  constexpr int WN = 16 * TN, LD = WN + 4, C4 = WN / 4;
+  const GemmArgs& g = a.g;
+  float* C = g.C + (int64_t)blockIdx.z * g.slab_stride;
+  const bool slab = g.slab_stride != 0;
+  const int epi = slab ? (int)CTR_EPI_NONE : g.epi;
+  GemmArgs ge = g;
+  if (epi == CTR_EPI_BIAS_RELU_DROP && ge.step_ptr) ge.offset += (uint64_t)(*ge.step_ptr) << 32;
+  const bool planes = a.cpl && !slab;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) strip[(4 * (lane >> 4) + r) * LD + 16 * tn + (lane & 15)] = acc[i][tn][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): wave-private strip, no barrier
+    __builtin_amdgcn_wave_barrier();
+    for (int idx = lane; idx < 16 * C4; idx += 64) {
+      const int row = idx / C4, c4 = idx - row * C4;
+      const int64_t m = mb + 16 * i + row;
+      const int64_t n = nb + 4 * c4;
+      if (m >= g.M || n >= g.N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(strip + row * LD + 4 * c4);
+      float4 o;
+      o.x = apply_epi(ge, epi, v.x, m, n + 0);
+      o.y = n + 1 < g.N ? apply_epi(ge, epi, v.y, m, n + 1) : 0.f;
+      o.z = n + 2 < g.N ? apply_epi(ge, epi, v.z, m, n + 2) : 0.f;
+      o.w = n + 3 < g.N ? apply_epi(ge, epi, v.w, m, n + 3) : 0.f;
+      if (C) {
+        float* crow = C + m * g.ldc;
+        if (g.vec_c && n + 3 < g.N) {
+          *reinterpret_cast<float4*>(crow + n) = o;
+        } else {
+          crow[n] = o.x;
+          if (n + 1 < g.N) crow[n + 1] = o.y;
+          if (n + 2 < g.N) crow[n + 2] = o.z;
+          if (n + 3 < g.N) crow[n + 3] = o.w;
+        }
+      }
+      if (planes) store_planes4(a, m, n, o);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ---- the kernel ---------------------------------------------------------------------
+// Block = WAVES_M x WAVES_N waves, tile BM x BN; a wave owns (BM/WAVES_M) x (BN/WAVES_N) as
+// TM x TN 16x16 accumulators (x2: the a0b0 accumulator and the small-products one).
+// NS-deep LDS ring of 32-deep k stages; one barrier per stage; the DMA of stage t+NS-1 is
+// issued right after the barrier of stage t and stays in flight (counted vmcnt) under the
+// MFMAs of stages t .. t+NS-2.
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool A_RC, bool B_RC, int NS>
+__global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(PlanesArgs a) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile in 16x16 MFMA blocks");
+  static_assert(!A_RC || BM == 64 || BM == 128, "RC operand tiles of 64 or 128");
+  static_assert(!B_RC || BN == 64 || BN == 128, "RC operand tiles of 64 or 128");
+  static_assert(NS >= 2 && NS <= 7, "2- to 7-deep LDS ring");
+  constexpr int A_PL = BM * kPBK * 2, B_PL = BN * kPBK * 2;  // bytes per plane image
+  constexpr int STAGE = 3 * (A_PL + B_PL);
+  constexpr int NIA = 3 * BM / 16, NIB = 3 * BN / 16;  // 1 KiB pieces per stage
+  constexpr int EPI = NW * 16 * (WN + 4) * 4;
+  constexpr int LDS = NS * STAGE > EPI ? NS * STAGE : EPI;
+  // ONE shared object: a second one can make hipcc wait vmcnt(0) before LDS reads
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+
+  const int64_t gn = (a.g.N + BN - 1) / BN;
+  const int64_t tix = xcd_tile_index();
+  const int64_t m0 = (tix / gn) * BM;
+  const int64_t n0 = (tix % gn) * BN;
+  const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
+  const int64_t ke = min(a.Kp, kb + a.k_per_split);
+  const int nt = kb < ke ? (int)((ke - kb) / kPBK) : 0;
+
+  pf32x4 acc[TM][TN], lo[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = lo[i][j] = (pf32x4){0.f, 0.f, 0.f, 0.f};
+
+  // The wave's LDS-DMA pieces: A's 3*BM/16 and B's 3*BN/16 1-KiB pieces of a stage are dealt
+  // round-robin over the waves (a wave short of a piece re-issues the operand's last one:
+  // the same bytes to the same place), so every wave issues exactly IPW per stage and the
+  // counted vmcnt is a constant. Per piece: the lane's byte offset from the operand base at
+  // the split's first k (computed once) and the uniform LDS offset in a stage; stage t adds
+  // t * (32 k) to the base.
+  constexpr int IPWA = (NIA + NW - 1) / NW, IPWB = (NIB + NW - 1) / NW;
+  const PlaneSrc SA = a.A, SB = a.B;
+  uint32_t offA[IPWA], offB[IPWB];
+  int ldsA[IPWA], ldsB[IPWB];
+#pragma unroll
+  for (int j = 0; j < IPWA; ++j) {
+    const int ins = min(wave + NW * j, NIA - 1);
+    const int plane = ins / (BM / 16), c = ins % (BM / 16);
+    ldsA[j] = plane * A_PL + c * 1024;
+    const uint16_t* p = A_RC ? piece_rc<A_RC ? BM : 64>(SA, plane, c, m0, kb, lane)
+                             : piece_kc(SA, plane, c, m0, kb, lane);
+    offA[j] = (uint32_t)((const char*)p - (const char*)SA.p);
+  }
+#pragma unroll
+  for (int j = 0; j < IPWB; ++j) {
+    const int ins = min(wave + NW * j, NIB - 1);
+    const int plane = ins / (BN / 16), c = ins % (BN / 16);
+    ldsB[j] = 3 * A_PL + plane * B_PL + c * 1024;
+    const uint16_t* p = B_RC ? piece_rc<B_RC ? BN : 64>(SB, plane, c, n0, kb, lane)
+                             : piece_kc(SB, plane, c, n0, kb, lane);
+    offB[j] = (uint32_t)((const char*)p - (const char*)SB.p);
+  }
+  const int64_t stepA = 2 * (A_RC ? kPBK * SA.ld : kPBK);  // bytes per stage along k
+  const int64_t stepB = 2 * (B_RC ? kPBK * SB.ld : kPBK);
+  // (the source is passed as `const void*`: with a type-dependent `const char*` argument the
+  // host-side pass of hipcc 7.2 fails substitution on this builtin and silently drops the
+  // kernel's launch stub)
+#define CTR_PL_ISSUE(t_)                                                                       \
+  do {                                                                                         \
+    char* st_ = smem + ((t_) % NS) * STAGE;                                                    \
+    const char* ba_ = (const char*)SA.p + (int64_t)(t_) * stepA;                               \
+    const char* bb_ = (const char*)SB.p + (int64_t)(t_) * stepB;                               \
+    _Pragma("unroll") for (int j_ = 0; j_ < IPWA; ++j_)                                        \
+        __builtin_amdgcn_global_load_lds((const void*)(ba_ + offA[j_]), (CTR_LDS void*)(st_ + ldsA[j_]), 16, 0, 0); \
+    _Pragma("unroll") for (int j_ = 0; j_ < IPWB; ++j_)                                        \
+        __builtin_amdgcn_global_load_lds((const void*)(bb_ + offB[j_]), (CTR_LDS void*)(st_ + ldsB[j_]), 16, 0, 0); \
+  } while (0)
+
+  int aoff[TM][2], boff[TN][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    aoff[i][0] = A_RC ? frag_rc_off<A_RC ? BM : 64>(wm0 + 16 * i, lane, 0) : frag_kc_off(wm0 + 16 * i, lane);
+    aoff[i][1] = A_RC ? frag_rc_off<A_RC ? BM : 64>(wm0 + 16 * i, lane, 1) : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    boff[i][0] = B_RC ? frag_rc_off<B_RC ? BN : 64>(wn0 + 16 * i, lane, 0) : frag_kc_off(wn0 + 16 * i, lane);
+    boff[i][1] = B_RC ? frag_rc_off<B_RC ? BN : 64>(wn0 + 16 * i, lane, 1) : 0;
+  }
+
+  auto compute = [&](int slot) {
+    const char* st = smem + slot * STAGE;
+    pbf16x8 af[TM][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const char* img = st + p * A_PL;
+        af[i][p] = A_RC ? frag_rc_at(img + aoff[i][0], img + aoff[i][1]) : frag_kc_at(img + aoff[i][0]);
+      }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      pbf16x8 bf[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const char* img = st + 3 * A_PL + p * B_PL;
+        bf[p] = B_RC ? frag_rc_at(img + boff[tn][0], img + boff[tn][1]) : frag_kc_at(img + boff[tn][0]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        // a0b0 into the main accumulator; the five products <= 2^-7 of it (smallest first)
+        // into the second, summed at the end
+        pf32x4 v = lo[i][tn];
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[1], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[2], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bf[0], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[1], v, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[0], v, 0, 0, 0);
+        lo[i][tn] = v;
+        acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[0], acc[i][tn], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: stages 0 .. NS-2 in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nt) CTR_PL_ISSUE(s);
+  constexpr int IPW = IPWA + IPWB;
+  for (int t = 0; t < nt; ++t) {
+    // this wave's pieces of stage t have landed; the q younger stages stay in flight ...
+    const int q = min(nt - 1 - t, NS - 2);
+    if (q <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#define CTR_PL_WAITQ(Q_)                                                          \
+    if constexpr (NS - 2 >= Q_) {                                                 \
+      if (q == Q_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * Q_) : "memory"); \
+    }
+    CTR_PL_WAITQ(1) CTR_PL_WAITQ(2) CTR_PL_WAITQ(3) CTR_PL_WAITQ(4) CTR_PL_WAITQ(5)
+#undef CTR_PL_WAITQ
+    // ... and every wave's (and every wave is done reading the slot refilled next)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
+    compute(t % NS);
+  }
+#undef CTR_PL_ISSUE
+  __syncthreads();  // every stage read before the epilogue reuses the LDS
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += lo[i][j];
+  planes_store<TM, TN>(a, acc, reinterpret_cast<float*>(smem) + wave * 16 * (WN + 4),
+                       m0 + wm0, n0 + wn0, lane);
+}
+
+// split-K: sum the fp32 slabs in split order (4 independent loads in flight per step of
+// the chain), then the epilogue (fp32 out and/or planes); one thread per 4 columns
+__global__ __launch_bounds__(64) void planes_reduce_kernel(PlanesArgs a, const float* __restrict__ slabs,
+                                                           int splits) {
+  GemmArgs g = a.g;
+  if (g.epi == CTR_EPI_BIAS_RELU_DROP && g.step_ptr) g.offset += (uint64_t)(*g.step_ptr) << 32;
+  const int64_t n4 = (g.N + 3) / 4;
+  const int64_t total = g.M * n4;
+  const int64_t slab = g.M * g.N;
+  const bool vec = g.N % 4 == 0;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = t / n4, n = 4 * (t - m * n4);
+    const int64_t o = m * g.N + n;
+    float e[4];
+    if (vec) {
+      float4 s = *reinterpret_cast<const float4*>(slabs + o);
+      int z = 1;
+      for (; z + 3 < splits; z += 4) {
+        const float4 v1 = *reinterpret_cast<const float4*>(slabs + (int64_t)z * slab + o);
+        const float4 v2 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 1) * slab + o);
+        const float4 v3 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 2) * slab + o);
+        const float4 v4 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 3) * slab + o);
+        s.x += v1.x; s.y += v1.y; s.z += v1.z; s.w += v1.w;
+        s.x += v2.x; s.y += v2.y; s.z += v2.z; s.w += v2.w;
+        s.x += v3.x; s.y += v3.y; s.z += v3.z; s.w += v3.w;
+        s.x += v4.x; s.y += v4.y; s.z += v4.z; s.w += v4.w;
+      }
+      for (; z < splits; ++z) {
+        const float4 v = *reinterpret_cast<const float4*>(slabs + (int64_t)z * slab + o);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      e[0] = s.x; e[1] = s.y; e[2] = s.z; e[3] = s.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = 0.f;
+        if (n + j >= g.N) continue;
+        float s = slabs[o + j];
+        for (int z = 1; z < splits; ++z) s += slabs[(int64_t)z * slab + o + j];
+        e[j] = s;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n + j < g.N) e[j] = apply_epi(g, g.epi, e[j], m, n + j);
+    if (g.C) {
+      float* crow = g.C + m * g.ldc;
+      for (int j = 0; j < 4 && n + j < g.N; ++j) crow[n + j] = e[j];
+    }
+    if (a.cpl) store_planes4(a, m, n, make_float4(e[0], e[1], e[2], e[3]));
+  }
+}
+
+// fp32 [rows][cols] (row stride ld) -> planes [3][.][.] (row stride dst_ld, plane stride
+// dst_ps); only the valid region is written (the zero padding is the allocation's)
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ src, int64_t rows,
+                                                           int64_t cols, int64_t ld,
+                                                           uint16_t* __restrict__ dst,
+                                                           int64_t dst_ld, int64_t dst_ps,
+                                                           bool vec) {
+  const int64_t c4 = (cols + 3) / 4;
+  const int64_t total = rows * c4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / c4, c = 4 * (t - r * c4);
+    const float* s = src + r * ld + c;
+    uint16_t* d = dst + r * dst_ld + c;
+    if (vec && c + 3 < cols) {
+      uint2 pl[3];
+      psplit4(*reinterpret_cast<const float4*>(s), pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(d + p * dst_ps) = pl[p];
+    } else {
+      for (int j = 0; j < 4 && c + j < cols; ++j) {
+        uint16_t h[3];
+        psplit1(s[j], h);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) d[p * dst_ps + j] = h[p];
+      }
+    }
+  }
+}
+
+// ---- tilings + chooser ----------------------------------------------------------------
+struct PlDef {
+  int bm, bn, wm, wn, ns;
+  int occ;     // blocks resident per CU (LDS bound)
+  double eff;  // sustained fraction of the per-CU bf16 MFMA peak (model only)
+};
+static const PlDef kPl[] = {
+    {64, 160, 2, 2, 3, 1, 0.60},   // 0: fwd0 / dH1-shaped (N = 300 -> 320), 256 blocks at B = 8192
+    {128, 128, 2, 2, 3, 1, 0.62},  // 1
+    {64, 128, 2, 2, 3, 1, 0.58},   // 2
+    {128, 64, 2, 2, 3, 1, 0.58},   // 3
+    {64, 64, 2, 2, 3, 2, 0.50},    // 4
+    {128, 128, 2, 2, 2, 1, 0.55},  // 5
+    {64, 160, 2, 2, 2, 1, 0.55},   // 6
+    {64, 64, 2, 2, 2, 3, 0.45},    // 7
+    // 8 waves (two per SIMD: one wave's LDS / barrier waits under the other's MFMAs)
+    {64, 160, 4, 2, 3, 1, 0.70},   // 8
+    {64, 160, 4, 2, 2, 1, 0.65},   // 9
+    {128, 128, 4, 2, 3, 1, 0.70},  // 10
+    {64, 128, 4, 2, 3, 1, 0.65},   // 11
+    {128, 64, 4, 2, 3, 1, 0.65},   // 12
+    {64, 64, 4, 2, 3, 2, 0.55},    // 13
+    // deep rings: more bytes in flight per CU (the k loop waits on its DMA otherwise)
+    {64, 64, 2, 2, 6, 1, 0.55},    // 14
+    {64, 64, 4, 2, 6, 1, 0.60},    // 15
+    {64, 128, 4, 2, 4, 1, 0.68},   // 16
+    {128, 64, 4, 2, 4, 1, 0.68},   // 17
+    {64, 64, 4, 2, 4, 1, 0.60},    // 18
+    {64, 64, 4, 2, 2, 3, 0.55},    // 19: 8 waves, 3 blocks per CU
+};
+constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
+
+struct PlCfg {
+  int tile, splits;
+  int64_t kps;
+};
+
+static bool pl_valid(int ti, bool a_rc, bool b_rc) {
+  const PlDef& d = kPl[ti];
+  return (!a_rc || d.bm == 64 || d.bm == 128) && (!b_rc || d.bn == 64 || d.bn == 128);
+}
+
+static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
+  auto mk = [&](int ti, int s) {
+    PlCfg c{ti, 1, Kp};
+    if (s > 1) {
+      c.kps = align_up(ceil_div(Kp, s), kPBK);
+      c.splits = (int)ceil_div(Kp, c.kps);
+    }
+    return c;
+  };
+  if (const char* env = getenv("CTR_GEMM_PLANES_CFG")) {
+    int ti = -1, sp = 1;
+    if (sscanf(env, "%d,%d", &ti, &sp) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
+        pl_valid(ti, a_rc, b_rc))
+      return mk(ti, sp);
+  }
+  // measured on MI355X (tools/gemm_planes_bench.py --sweep, profiles/r02_gemm_planes_sweep.jsonl):
+  // large-M products with a narrow N (the forward) on the 8-wave 64x160 tiling, large-M
+  // products with a k-strided B (the dH1 / dX backward) on 64x64 x3 blocks per CU, the
+  // transposed weight gradients (both operands k-strided, long K) on 64x64 with split-K
+  // sized to ~2 blocks per CU
+  if (!a_rc && !b_rc && M >= 2048 && N > 192 && N <= 320) return mk(8, 1);
+  if (!a_rc && !b_rc && M >= 2048 && N <= 192) return mk(17, 1);
+  if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
+  if (a_rc && b_rc && Kp >= 2048) {
+    const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
+    const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(
+                      ceil_div(512, tiles), Kp / 256), 32));
+    return mk(7, s);
+  }
+  // otherwise a makespan model: blocks dealt to 256 CUs x occ slots in rounds; a round costs one block's
+  // padded bf16 MFMA work (6 products) at the tiling's sustained per-CU rate, plus fill and
+  // drain; split-K adds its fp32 slab round trip and the reduce launch
+  const double per_cu = 2.5e15 / 256.0 / 1e6;  // bf16 flop per us per CU
+  PlCfg best = mk(0, 1);
+  double best_t = 1e30;
+  for (int ti = 0; ti < kNumPl; ++ti) {
+    if (!pl_valid(ti, a_rc, b_rc)) continue;
+    const PlDef& d = kPl[ti];
+    const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
+    for (int s = 1; s <= 32; ++s) {
+      if (s > 1 && Kp / s < 128) break;
+      const PlCfg c = mk(ti, s);
+      if (c.splits != s) continue;
+      const int64_t blocks = tiles * c.splits;
+      const double rounds = (double)ceil_div(blocks, 256 * (int64_t)d.occ);
+      const int64_t per_cu_blocks = std::min<int64_t>(d.occ, ceil_div(blocks, 256));
+      const double t_block =
+          6.0 * 2.0 * d.bm * d.bn * (double)c.kps * per_cu_blocks / (per_cu * d.eff) + 2.5;
+      double t = rounds * t_block;
+      if (c.splits > 1) t += 2.0 * c.splits * (double)M * N * 4 / 5e6 + 3.0;
+      if (t < best_t * 0.98) {
+        best_t = t;
+        best = c;
+      }
+    }
+  }
+  return best;
+}
+
+// every (tiling, orientation) pair is instantiated explicitly (RC operands only on 64- or
+// 128-wide tiles; pl_valid keeps the chooser inside this list)
+#define CTR_PL_K(BM, BN, WMW, WNW, NS, AR, BR)                                          \
+  hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WMW, WNW, AR, BR, NS>), grid, 64 * WMW * WNW, \
+                     0, st, a)
+#define CTR_PL_ALL4(BM, BN, WMW, WNW, NS)                          \
+  if (!a_rc && !b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false); \
+  else if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, true);      \
+  else if (!b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, true, false);      \
+  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, true);
+#define CTR_PL_AONLY(BM, BN, WMW, WNW, NS)                          \
+  if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false);          \
+  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, false);
+
+static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc, dim3 grid,
+                      hipStream_t st) {
+  switch (c.tile) {
+    case 0: CTR_PL_AONLY(64, 160, 2, 2, 3) break;
+    case 1: CTR_PL_ALL4(128, 128, 2, 2, 3) break;
+    case 2: CTR_PL_ALL4(64, 128, 2, 2, 3) break;
+    case 3: CTR_PL_ALL4(128, 64, 2, 2, 3) break;
+    case 4: CTR_PL_ALL4(64, 64, 2, 2, 3) break;
+    case 5: CTR_PL_ALL4(128, 128, 2, 2, 2) break;
+    case 6: CTR_PL_AONLY(64, 160, 2, 2, 2) break;
+    case 7: CTR_PL_ALL4(64, 64, 2, 2, 2) break;
+    case 8: CTR_PL_AONLY(64, 160, 4, 2, 3) break;
+    case 9: CTR_PL_AONLY(64, 160, 4, 2, 2) break;
+    case 10: CTR_PL_ALL4(128, 128, 4, 2, 3) break;
+    case 11: CTR_PL_ALL4(64, 128, 4, 2, 3) break;
+    case 12: CTR_PL_ALL4(128, 64, 4, 2, 3) break;
+    case 13: CTR_PL_ALL4(64, 64, 4, 2, 3) break;
+    case 14: CTR_PL_ALL4(64, 64, 2, 2, 6) break;
+    case 15: CTR_PL_ALL4(64, 64, 4, 2, 6) break;
+    case 16: CTR_PL_ALL4(64, 128, 4, 2, 4) break;
+    case 17: CTR_PL_ALL4(128, 64, 4, 2, 4) break;
+    case 18: CTR_PL_ALL4(64, 64, 4, 2, 4) break;
+    case 19: CTR_PL_ALL4(64, 64, 4, 2, 2) break;
+  }
+}
+#undef CTR_PL_AONLY
+#undef CTR_PL_ALL4
+#undef CTR_PL_K
+
+static int64_t pl_ws_bytes(const PlCfg& c, int64_t M, int64_t N) {
+  return c.splits > 1 ? (int64_t)c.splits * M * N * 4 : 0;
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+static bool plane_src_ok(const ctr_planes* p) {
+  return p && p->data && p->ld > 0 && p->ld % 8 == 0 && p->plane_stride % 8 == 0 &&
+         p->rows > 0 && p->cols > 0 && p->cols <= p->ld &&
+         p->plane_stride >= p->rows * p->ld && (uintptr_t)p->data % 16 == 0;
+}
+
+extern "C" int ctr_split_planes(const float* src, int64_t rows, int64_t cols, int64_t ld,
+                                const ctr_planes* dst, ctr_stream_t stream) {
+  CTR_REQUIRE(rows >= 0 && cols >= 0, "ctr_split_planes: bad sizes");
+  if (rows == 0 || cols == 0) return CTR_OK;
+  CTR_REQUIRE(src && plane_src_ok(dst), "ctr_split_planes: bad pointers / plane layout");
+  CTR_REQUIRE(ld >= cols && dst->rows >= rows && dst->cols >= cols,
+              "ctr_split_planes: destination smaller than the source");
+  const bool vec = ld % 4 == 0 && (uintptr_t)src % 16 == 0;
+  const int64_t total = rows * ceil_div(cols, 4);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 8192));
+  hipLaunchKernelGGL(split_planes_kernel, grid, 256, 0, as_stream(stream), src, rows, cols, ld,
+                     static_cast<uint16_t*>(dst->data), dst->ld, dst->plane_stride, vec);
+  CTR_LAUNCH_CHECK("split_planes_kernel");
+  return CTR_OK;
+}
+
+extern "C" int64_t ctr_gemm_planes_workspace_bytes(int a_rc, int b_rc, int64_t M, int64_t N,
+                                                   int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const PlCfg c = pl_choose(a_rc != 0, b_rc != 0, M, N, align_up(K, kPBK));
+  return pl_ws_bytes(c, M, N);
+}
+
+extern "C" int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                               const ctr_planes* A, const ctr_planes* B, float* C, int64_t ldc,
+                               const ctr_planes* Cp, int epi, const float* bias, const float* aux,
+                               int64_t ldaux, float scale, float drop_p, uint64_t seed,
+                               uint64_t offset, const int32_t* step_ptr, void* ws,
+                               int64_t ws_bytes, ctr_stream_t stream) {
+  CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "ctr_gemm_planes: negative size");
+  if (M == 0 || N == 0) return CTR_OK;
+  CTR_REQUIRE(C || Cp, "ctr_gemm_planes: no output");
+  CTR_REQUIRE(plane_src_ok(A) && plane_src_ok(B), "ctr_gemm_planes: bad operand plane layout");
+  CTR_REQUIRE(!Cp || (plane_src_ok(Cp) && Cp->rows >= M && Cp->cols >= N),
+              "ctr_gemm_planes: bad output plane layout");
+  CTR_REQUIRE(!C || ldc >= N, "ctr_gemm_planes: ldc < N");
+  const int64_t Kp = align_up(std::max<int64_t>(K, 1), kPBK);
+  // KC operand: storage [rows >= extent][cols >= Kp]; RC: storage [rows >= Kp][cols >= extent]
+  CTR_REQUIRE(a_rc ? (A->rows >= Kp && A->cols >= M && A->cols % 16 == 0)
+                   : (A->rows >= M && A->cols >= Kp),
+              "ctr_gemm_planes: A planes must cover the (32-padded) operand, zero-padded");
+  CTR_REQUIRE(b_rc ? (B->rows >= Kp && B->cols >= N && B->cols % 16 == 0)
+                   : (B->rows >= N && B->cols >= Kp),
+              "ctr_gemm_planes: B planes must cover the (32-padded) operand, zero-padded");
+  CTR_REQUIRE(epi != CTR_EPI_BIAS_RELU_DROP || (drop_p >= 0.f && drop_p < 1.f),
+              "ctr_gemm_planes: drop_p out of range");
+  CTR_REQUIRE(epi != CTR_EPI_GRAD_MASK || aux, "ctr_gemm_planes: GRAD_MASK needs aux");
+  CTR_REQUIRE((epi != CTR_EPI_BIAS && epi != CTR_EPI_BIAS_RELU && epi != CTR_EPI_BIAS_RELU_DROP) || bias,
+              "ctr_gemm_planes: bias epilogue without bias");
+  const bool arc = a_rc != 0, brc = b_rc != 0;
+  const PlCfg c = pl_choose(arc, brc, M, N, Kp);
+  const PlDef& d = kPl[c.tile];
+  const int64_t need = pl_ws_bytes(c, M, N);
+  CTR_REQUIRE(ws_bytes >= need && (need == 0 || ws), "ctr_gemm_planes: workspace too small");
+
+  PlanesArgs a{};
+  a.Kp = Kp;
+  a.k_per_split = c.kps;
+  auto src = [](const ctr_planes* p) {
+    return PlaneSrc{static_cast<const uint16_t*>(p->data), p->ld, p->plane_stride, p->rows, p->cols};
+  };
+  a.A = src(A);
+  a.B = src(B);
+  GemmArgs& g = a.g;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.C = C;
+  g.ldc = ldc;
+  g.epi = epi;
+  g.bias = bias;
+  g.aux = aux;
+  g.ldaux = ldaux;
+  g.scale = scale;
+  g.drop_thr = epi == CTR_EPI_BIAS_RELU_DROP
+                   ? (uint32_t)std::min<double>((double)drop_p * 4294967296.0, 4294967295.0)
+                   : 0u;
+  g.drop_scale = epi == CTR_EPI_BIAS_RELU_DROP ? 1.0f / (1.0f - drop_p) : 1.0f;
+  g.seed = seed;
+  g.offset = offset;
+  g.step_ptr = step_ptr;
+  g.vec_c = C && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+  if (Cp) {
+    a.cpl = static_cast<uint16_t*>(Cp->data);
+    a.cpl_ld = Cp->ld;
+    a.cpl_ps = Cp->plane_stride;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
+  CTR_REQUIRE(tiles <= INT32_MAX && c.splits <= 65535, "ctr_gemm_planes: grid too large");
+  const dim3 grid((unsigned)tiles, 1, (unsigned)c.splits);
+  if (c.splits > 1) {
+    PlanesArgs s = a;
+    s.g.C = static_cast<float*>(ws);
+    s.g.ldc = N;
+    s.g.slab_stride = M * N;
+    s.g.vec_c = N % 4 == 0;
+    s.cpl = nullptr;
+    pl_launch(c, s, arc, brc, grid, st);
+    CTR_LAUNCH_CHECK("gemm_planes_kernel (split-K)");
+    const int64_t total = M * ceil_div(N, 4);
+    const unsigned g2 = (unsigned)std::min<int64_t>(ceil_div(total, 64), 16384);
+    hipLaunchKernelGGL(planes_reduce_kernel, g2, 64, 0, st, a, static_cast<const float*>(ws),
+                       c.splits);
+    CTR_LAUNCH_CHECK("planes_reduce_kernel");
+    return CTR_OK;
+  }
+  pl_launch(c, a, arc, brc, grid, st);
+  CTR_LAUNCH_CHECK("gemm_planes_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_gemm_planes_config(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                                      int* tile, int* splits, int* bm, int* bn) {
+  const PlCfg c = pl_choose(a_rc != 0, b_rc != 0, M, N, align_up(std::max<int64_t>(K, 1), kPBK));
+  if (tile) *tile = c.tile;
+  if (splits) *splits = c.splits;
+  if (bm) *bm = kPl[c.tile].bm;
+  if (bn) *bn = kPl[c.tile].bn;
+  return CTR_OK;
+}

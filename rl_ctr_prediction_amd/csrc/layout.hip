@@ -95,7 +95,8 @@ extern "C" int ctr_transpose_f32(const float* src, int64_t rows, int64_t cols, i
   CTR_REQUIRE(ld_src >= cols && ld_dst >= rows, "ctr_transpose_f32: need ld_src >= cols and "
               "ld_dst >= rows");
   const int64_t col_tiles = ceil_div(cols, kTT), row_tiles = ceil_div(rows, kTT);
-  CTR_REQUIRE(col_tiles <= INT32_MAX, "ctr_transpose_f32: too many columns");
+  // gridDim.x * blockDim.x must fit 32 bits
+  CTR_REQUIRE(col_tiles <= (int64_t)(UINT32_MAX / 256), "ctr_transpose_f32: too many columns");
   const dim3 grid((unsigned)col_tiles, (unsigned)std::min<int64_t>(row_tiles, 65535));
   const bool vec = rows % 4 == 0 && cols % 4 == 0 && ld_src % 4 == 0 && ld_dst % 4 == 0 &&
                   reinterpret_cast<uintptr_t>(src) % 16 == 0 &&

@@ -11,11 +11,11 @@ from dataclasses import dataclass
 import torch
 
 from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
-                   EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, SparsePlan, lib)
+                   EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, SparsePlan, lib)
 
 __all__ = [
-    "embedding_gather", "fm_forward", "bce_sigmoid", "deepfm_head", "gemm", "linear",
-    "tensor_sum", "colsum", "transpose", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
+    "embedding_gather", "fm_forward", "fm_forward_planes", "bce_sigmoid", "deepfm_head", "gemm", "linear",
+    "tensor_sum", "colsum", "transpose", "Planes", "split_planes", "gemm_planes", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
     "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
@@ -137,6 +137,26 @@ def fm_forward(idx: torch.Tensor, emb: torch.Tensor, lin: torch.Tensor, bias: to
     return out
 
 
+def fm_forward_planes(idx: torch.Tensor, emb: torch.Tensor, lin: torch.Tensor,
+                      bias: torch.Tensor, x_planes: "Planes", z: torch.Tensor,
+                      sum_e: torch.Tensor, err_flag=None) -> None:
+    """DeepFM's FM part (z, sum_e) with the flattened embeddings written as the MLP input's
+    three bf16 planes (no fp32 copy): ctr_fm_forward_planes."""
+    idx, it = _idx(idx)
+    B, F = idx.shape
+    _f32(emb, "feature_embedding.weight")
+    _f32(lin, "linear.weight")
+    V, K = emb.shape
+    if (x_planes.rows, x_planes.cols) != (B, F * K):
+        raise ValueError(f"fm_forward_planes: planes must be [{B}, {F * K}]")
+    lib.ctr_fm_forward_planes(_p(idx), it, B, F, K, V, _p(emb), _p(lin), _p(bias), _p(z),
+                              _p(sum_e), x_planes.desc, _p(err_flag), _stream())
+
+
+def fm_forward_planes_ok(K: int, F: int) -> bool:
+    return K % 4 == 0 and 64 % (K // 4 or 1) == 0 and K <= 256 and F <= 64
+
+
 def bce_sigmoid(z: torch.Tensor, labels: torch.Tensor, mean_div: float | None = None):
     _f32(z, "z")
     _f32(labels, "labels")
@@ -147,7 +167,9 @@ def bce_sigmoid(z: torch.Tensor, labels: torch.Tensor, mean_div: float | None = 
     return p, loss, gz
 
 
-def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.0, out=None):
+def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.0, out=None,
+                dh_planes: "Planes | None" = None):
+    """dh_planes: also write dh_pre as its three bf16 planes (ctr_deepfm_head_planes)."""
     _f32(h, "h")
     B, H = h.shape
     dev = h.device
@@ -156,6 +178,14 @@ def deepfm_head(h, w_out, b_out, z_fm, labels=None, mean_div=None, drop_scale=1.
         out = dict(z=e(B), p=e(B), loss_elem=e(B) if labels is not None else None,
                    gz=e(B) if labels is not None else None,
                    dh_pre=e(B, H) if labels is not None else None)
+    if dh_planes is not None:
+        if labels is None or (dh_planes.rows, dh_planes.cols) != (B, H):
+            raise ValueError(f"deepfm_head: dh_planes needs labels and [{B}, {H}] planes")
+        lib.ctr_deepfm_head_planes(_p(h), B, H, _p(w_out), _p(b_out), _p(z_fm), _p(labels),
+                                   float(B if mean_div is None else mean_div), float(drop_scale),
+                                   _p(out["z"]), _p(out["p"]), _p(out["loss_elem"]),
+                                   _p(out["gz"]), _p(out["dh_pre"]), dh_planes.desc, _stream())
+        return out
     lib.ctr_deepfm_head(_p(h), B, H, _p(w_out), _p(b_out), _p(z_fm), _p(labels),
                         float(B if mean_div is None else mean_div), float(drop_scale),
                         _p(out["z"]), _p(out["p"]), _p(out["loss_elem"]), _p(out["gz"]),
@@ -197,6 +227,84 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool 
                         int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _p(step_dev), _p(ws),
                         0 if ws is None else ws.numel(), _stream())
     return out
+
+
+class Planes:
+    """An fp32 matrix [rows, cols] held as its exact three-plane bf16 split (ctr_planes):
+    one bf16 tensor [3, rows_pad, cols_pad], both extents padded to multiples of 32 with
+    zeros (allocated zeroed; producers write only the valid region, so the pad stays zero).
+    x = x0 + (x1 + x2) recovers every fp32 element exactly (to_float)."""
+
+    def __init__(self, rows: int, cols: int, device, pad: int = 32):
+        self.rows, self.cols = int(rows), int(cols)
+        self.rows_pad = -(-max(self.rows, 1) // pad) * pad
+        self.cols_pad = -(-max(self.cols, 1) // pad) * pad
+        self.t = torch.zeros(3, self.rows_pad, self.cols_pad, dtype=torch.bfloat16, device=device)
+        self.desc = PlanesDesc(self.t.data_ptr(), self.cols_pad, self.rows_pad * self.cols_pad,
+                               self.rows_pad, self.cols_pad)
+
+    @property
+    def device(self):
+        return self.t.device
+
+    def to_float(self) -> torch.Tensor:
+        """The fp32 matrix (x0 + (x1 + x2), exact)."""
+        p = self.t[:, :self.rows, :self.cols].float()
+        return p[0] + (p[1] + p[2])
+
+
+def split_planes(src: torch.Tensor, out: Planes | None = None) -> Planes:
+    """The exact three-plane bf16 split of an fp32 [rows, cols] matrix (row-contiguous)."""
+    _dev(src, "src")
+    if src.dtype != torch.float32 or src.dim() != 2 or (src.numel() and src.stride(1) != 1):
+        raise ValueError("split_planes: src must be a float32 [rows, cols] row-contiguous matrix")
+    R, Cn = src.shape
+    if out is None:
+        out = Planes(R, Cn, src.device)
+    elif out.rows != R or out.cols != Cn:
+        raise ValueError(f"split_planes: out planes are [{out.rows}, {out.cols}], src [{R}, {Cn}]")
+    lib.ctr_split_planes(_p(src), R, Cn, src.stride(0) if R > 1 else Cn, out.desc, _stream())
+    return out
+
+
+def gemm_planes(a: Planes, b: Planes, a_rc: bool, b_rc: bool, *, out: torch.Tensor | None = None,
+                out_planes: Planes | None = None, epi: int = EPI_NONE, bias=None, aux=None,
+                scale: float = 1.0, drop_p: float = 0.0, seed: int = 0, offset: int = 0,
+                step_dev: torch.Tensor | None = None) -> torch.Tensor | None:
+    """C = A.B on pre-split planes (ctr_gemm_planes). a_rc: A holds A^T ([K, M]); b_rc: B holds
+    B itself ([K, N]) rather than the nn.Linear form [N, K]. Writes `out` (fp32 [M, N]) and/or
+    `out_planes` (the planes of the epilogue's result)."""
+    M, K = (a.cols, a.rows) if a_rc else (a.rows, a.cols)
+    N, Kb = (b.cols, b.rows) if b_rc else (b.rows, b.cols)
+    if K != Kb:
+        raise ValueError(f"gemm_planes: inner dims differ ({K} vs {Kb})")
+    if out is None and out_planes is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    if out is not None:
+        _f32(out, "out")
+        if tuple(out.shape) != (M, N):
+            raise ValueError(f"gemm_planes: out must be [{M}, {N}]")
+    if out_planes is not None and (out_planes.rows, out_planes.cols) != (M, N):
+        raise ValueError(f"gemm_planes: out_planes must be [{M}, {N}]")
+    if aux is not None:
+        _f32(aux, "aux")
+    nbytes = lib.ctr_gemm_planes_workspace_bytes(int(a_rc), int(b_rc), M, N, K)
+    ws = Workspace.get(nbytes, a.device)
+    lib.ctr_gemm_planes(int(a_rc), int(b_rc), M, N, K, a.desc, b.desc, _p(out),
+                        out.stride(0) if out is not None else 0,
+                        out_planes.desc if out_planes is not None else None, int(epi), _p(bias),
+                        _p(aux), aux.stride(0) if aux is not None else 0, float(scale),
+                        float(drop_p), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+                        _p(step_dev), _p(ws), 0 if ws is None else ws.numel(), _stream())
+    return out
+
+
+def gemm_planes_config(a_rc: bool, b_rc: bool, M: int, N: int, K: int) -> dict:
+    """The tiling ctr_gemm_planes picks for a shape (tuning / tests)."""
+    import ctypes
+    v = [ctypes.c_int(0) for _ in range(4)]
+    lib.ctr_gemm_planes_config(int(a_rc), int(b_rc), M, N, K, *(ctypes.byref(x) for x in v))
+    return dict(tile=v[0].value, splits=v[1].value, bm=v[2].value, bn=v[3].value)
 
 
 def linear(x, weight, bias, *, relu=False, drop_p=0.0, seed=0, offset=0, step_dev=None, out=None):
@@ -253,11 +361,13 @@ def transpose(src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
     R, Cn = src.shape
     if src.numel() and src.stride(1) != 1:
         raise ValueError("transpose: src rows must be contiguous")
+    if R > 1 and src.stride(0) < Cn:  # a stride-0 / overlapping row view (x.expand(R, C))
+        raise ValueError("transpose: src rows must not overlap (stride(0) >= columns)")
     if out is None:
         out = torch.empty(Cn, R, dtype=torch.float32, device=src.device)
     if tuple(out.shape) != (Cn, R) or (out.numel() and out.stride(1) != 1):
         raise ValueError(f"transpose: out must be a row-contiguous [{Cn}, {R}] tensor")
-    lib.ctr_transpose_f32(_p(src), R, Cn, max(src.stride(0), Cn), _p(out), max(out.stride(0), R),
+    lib.ctr_transpose_f32(_p(src), R, Cn, src.stride(0) if R > 1 else Cn, _p(out), max(out.stride(0), R),
                           _stream())
     return out
 

@@ -63,8 +63,12 @@ class _Bufs:
     head: dict | None = None
     dh1: torch.Tensor | None = None
     dx: torch.Tensor | None = None
-    xT: torch.Tensor | None = None     # MLP input, transposed [W, B] (k-contiguous dW0)
-    dh1T: torch.Tensor | None = None   # dH1 transposed [H1, B]
+    # exact three-plane bf16 splits (hip_ops.Planes) of the MLP GEMM operands, written by
+    # their producers; the GEMMs read them in the stored orientation (csrc/gemm_planes.hip)
+    xp: hip_ops.Planes | None = None    # MLP input X [B, W]
+    h1p: hip_ops.Planes | None = None   # H1 [B, H1]
+    dh2p: hip_ops.Planes | None = None  # dH2 [B, H2]
+    dh1p: hip_ops.Planes | None = None  # dH1 [B, H1]
     loss: torch.Tensor | None = None
     gplan: hip_ops.SparsePlanBuffers | None = None
     g_rows: torch.Tensor | None = None
@@ -149,9 +153,13 @@ class FusedCTRTrainer:
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self._wgrad_stream = (torch.cuda.Stream(device=self.device) if self.kind in _MLP_KINDS
                               else None)
-        # dW0 = dH1^T X on transposed copies of both operands (k-contiguous GEMM operands,
-        # csrc/layout.hip); CTR_DW0_KC=0 keeps the strided form (A/B only)
-        self.dw0_kc = os.environ.get("CTR_DW0_KC", "1") != "0"
+        # the MLP weights' planes, re-split from the fp32 parameters at the start of every step
+        # (the parameters stay the source of truth: state_dict / load_state_dict see fp32)
+        self._wplanes = None
+        if self.kind in _MLP_KINDS:
+            w0, w1 = self.views["mlp.0.weight"], self.views["mlp.3.weight"]
+            self._wplanes = (hip_ops.Planes(*w0.shape, self.device),
+                             hip_ops.Planes(*w1.shape, self.device))
         self._sweep_stream = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
@@ -200,6 +208,13 @@ class FusedCTRTrainer:
             M, K = (a.shape[1], a.shape[0]) if ta else a.shape
             N = bb.shape[0] if tb else bb.shape[1]
             self._span("gemm", t, 2.0 * M * N * K)
+        return out
+
+    def _gemm_planes(self, a, b, a_rc, b_rc, M, N, K, **kw):
+        """hip_ops.gemm_planes with a timing span carrying the product's flop count."""
+        t = self._mark("gemm")
+        out = hip_ops.gemm_planes(a, b, a_rc, b_rc, **kw)
+        self._span("gemm", t, 2.0 * M * N * K)
         return out
 
     def _linear(self, x, w, b, **kw):
@@ -267,7 +282,9 @@ class FusedCTRTrainer:
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
         deep = self.kind in _MLP_KINDS
         W = F * K + (F * (F - 1) // 2 if self.kind == "IPNN" else 0)  # MLP input width
-        fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, W) if deep else None,
+        # DeepFM writes its MLP input straight as planes (b.xp): no fp32 copy of X
+        x_fp32 = deep and not (self.kind == "DeepFM" and hip_ops.fm_forward_planes_ok(K, F))
+        fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, W) if x_fp32 else None,
                                p=None, loss_elem=e(B), gz=e(B))
         S = B * F
         b = _Bufs(B=B, fm=fm, plan=hip_ops.SparsePlanBuffers(S, dev), grad_rows=e(S, K),
@@ -276,8 +293,8 @@ class FusedCTRTrainer:
             mlp = self.model.mlp
             H1, H2 = mlp[0].out_features, mlp[3].out_features
             b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, W)
-            if self.dw0_kc:
-                b.xT, b.dh1T = e(W, B), e(H1, B)
+            P = hip_ops.Planes
+            b.xp, b.h1p, b.dh2p, b.dh1p = P(B, W, dev), P(B, H1, dev), P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
                 b.dslot = e(S, K)
                 b.zero = torch.zeros(B, dtype=torch.float32, device=dev)
@@ -294,6 +311,10 @@ class FusedCTRTrainer:
     def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
         batch's mean BCE as a 1-element device tensor (no host sync).
+
+        The returned tensor is the trainer's persistent loss buffer for this batch shape
+        (a captured HIP graph writes it in place): it is valid until the next step() with
+        the same shape. Keep a value with ``loss.item()`` or ``loss.clone()``.
 
         Single process: the step's ~40 launches are captured once per (x, y) buffer pair
         into a HIP graph and replayed (every per-step scalar — the Adam step, the dropout
@@ -453,29 +474,53 @@ class FusedCTRTrainer:
             torch.cuda.current_stream().wait_stream(self._sweep_stream)
 
     def _deepfm_forward_backward(self, x, y, b: _Bufs, E, w, bias, mean_div):
+        """The MLP part of DeepFM / InnerPNN (p_model.py:276-293,322 and 185-200) on
+        pre-split planes: 6 GEMMs per step, every operand read in the orientation its
+        producer wrote it (the transposed products of the backward by the GEMM's transpose
+        read), no transposed copy anywhere."""
         mlp, gv, vw = self.model.mlp, self.grad_views, self.views
         training = self.model.training
         p0 = float(mlp[2].p) if training else 0.0
         p1 = float(mlp[5].p) if training else 0.0
         B = x.shape[0]
         H1, H2 = b.h1.shape[1], b.h2.shape[1]
-        # dropout stream of this step: (completed steps) << 32 is added on the device
-        off = 0
+        W = b.xp.cols
+        w0p, w1p = self._wplanes
+        # dropout stream of this step: (completed steps) << 32 is added on the device.
+        # The counter is the GLOBAL-batch element index (rank r's local row m is global row
+        # r*B + m), so N ranks draw exactly the masks one process draws on the global batch
+        # (independent masks per rank; tests/test_gpu_sharded.py checks the equality)
+        rank, ws = world()
+        off1 = rank * B * H1
+        off2 = ws * B * H1 + rank * B * H2
+        hip_ops.split_planes(vw["mlp.0.weight"], out=w0p)
+        hip_ops.split_planes(vw["mlp.3.weight"], out=w1p)
         t = self._mark("gather")
         if self.kind == "IPNN":  # cat = flat(E[x]) ++ pairwise inner products
             X = hip_ops.ipnn_forward(x, E, out=b.fm.emb_out, err_flag=self.err)
             z_fm = b.zero
+        elif b.fm.emb_out is None:  # gather + FM, the MLP input written as its planes
+            hip_ops.fm_forward_planes(x, E, w, bias, b.xp, b.fm.z, b.fm.sum_e, err_flag=self.err)
+            X, z_fm = None, b.fm.z
         else:
             fm = hip_ops.fm_forward(x, E, w, bias, want_sum=True, want_emb=True, want_p=False,
                                     err_flag=self.err, out=b.fm)
             X, z_fm = fm.emb_out, fm.z
+        if X is not None:
+            hip_ops.split_planes(X, out=b.xp)
         self._span("gather", t)
-        self._linear(X, vw["mlp.0.weight"], vw["mlp.0.bias"], relu=True, drop_p=p0,
-                     seed=self.seed, offset=off, step_dev=self.step_done, out=b.h1)
-        self._linear(b.h1, vw["mlp.3.weight"], vw["mlp.3.bias"], relu=True, drop_p=p1,
-                     seed=self.seed, offset=off + B * H1, step_dev=self.step_done, out=b.h2)
+        # Linear(F*K,300)+ReLU+Dropout: H1 (fp32 for the mask, planes for the next GEMMs)
+        self._gemm_planes(b.xp, w0p, False, False, B, H1, W, out=b.h1, out_planes=b.h1p,
+                          epi=hip_ops.EPI_BIAS_RELU_DROP if p0 > 0 else hip_ops.EPI_BIAS_RELU,
+                          bias=vw["mlp.0.bias"], drop_p=p0, seed=self.seed, offset=off1,
+                          step_dev=self.step_done)
+        self._gemm_planes(b.h1p, w1p, False, False, B, H2, H1, out=b.h2,
+                          epi=hip_ops.EPI_BIAS_RELU_DROP if p1 > 0 else hip_ops.EPI_BIAS_RELU,
+                          bias=vw["mlp.3.bias"], drop_p=p1, seed=self.seed, offset=off2,
+                          step_dev=self.step_done)
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], z_fm, y,
-                                   mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head)
+                                   mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head,
+                                   dh_planes=b.dh2p)
         gz, dh2 = head["gz"], head["dh_pre"]
         # the weight / bias gradients are needed only by the dense Adam at the end of the
         # step: they run on one side stream, the small layers' from the head on (under the
@@ -491,34 +536,28 @@ class FusedCTRTrainer:
             hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
                                   (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
                                   (dh2, None, gv["mlp.3.bias"])])
-            # Linear(300,200): dW1 = dH2^T H1
-            self._gemm(dh2, b.h1, trans_a=True, out=gv["mlp.3.weight"])
-            if self.dw0_kc:  # X^T for dW0, beside the dH1 / dX GEMMs
-                hip_ops.transpose(X, out=b.xT)
+            # Linear(300,200): dW1 = dH2^T H1 (both operands k-strided: transpose reads)
+            self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B, out=gv["mlp.3.weight"])
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
-        self._gemm(dh2, vw["mlp.3.weight"], epi=hip_ops.EPI_GRAD_MASK, aux=b.h1,
-                   scale=1.0 / (1.0 - p0), out=b.dh1)
+        self._gemm_planes(b.dh2p, w1p, False, True, B, H1, H2, out=b.dh1, out_planes=b.dh1p,
+                          epi=hip_ops.EPI_GRAD_MASK, aux=b.h1, scale=1.0 / (1.0 - p0))
         # Linear(F*K,300): dX = dH1 @ W0, the MLP-input gradient the scatter needs
-        self._gemm(b.dh1, vw["mlp.0.weight"], out=b.dx)
+        self._gemm_planes(b.dh1p, w0p, False, True, B, W, H1, out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
             hip_ops.ipnn_backward(x, E, b.dx, out=b.dslot)
-        self._dw0(side, b, X, gv)  # after dX: forking dW0 beside dX measured slower
+        self._dw0(side, b, gv)  # after dX: forking dW0 beside dX measured slower
         return gz
 
-    def _dw0(self, side, b: _Bufs, X, gv) -> None:
+    def _dw0(self, side, b: _Bufs, gv) -> None:
         """mlp.0's weight / bias gradients on the weight-gradient stream, under the scatter
-        chain. k-contiguous form (default): 11.5 -> 11.7 M ex/s at C3 (interleaved A/B, 3
-        runs each); dW0 itself 120 -> 77 us in the step, the transposes ride beside dX."""
+        chain: db0 = colsum dH1, dW0 = dH1^T X (both operands k-strided planes)."""
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X
             hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
-            if self.dw0_kc:  # both operands k-contiguous (csrc/layout.hip)
-                hip_ops.transpose(b.dh1, out=b.dh1T)
-                self._gemm(b.dh1T, b.xT, trans_b=True, out=gv["mlp.0.weight"])
-            else:
-                self._gemm(b.dh1, X, trans_a=True, out=gv["mlp.0.weight"])
+            H1, W = b.dh1.shape[1], b.dx.shape[1]
+            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, b.dh1.shape[0],
+                              out=gv["mlp.0.weight"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""

@@ -1,0 +1,163 @@
+"""The pre-split-plane GEMM (csrc/gemm_planes.hip, ctr_gemm_planes) — the fused trainer's
+MLP GEMMs (p_model.py:276-293,322).
+
+* the three-plane split is exact: x0 + (x1 + x2) == x bitwise, padding stays zero;
+* layouts: small-integer operands make every product and partial sum exact in fp32, so any
+  fragment / swizzle / transpose-read mistake shows as a bit difference against fp64;
+* accuracy on random data against fp64, relative to the L1 bound: no worse than the
+  exact-fp32 MFMA kernel (v_mfma_f32_32x32x2_f32) on the same product;
+* every tiling x orientation, split-K, M/N/K edges; the epilogues (bias, ReLU, dropout mask
+  identical to ctr_gemm_f32's, GRAD_MASK) and the output planes == split(fp32 output).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N_TILES = 20
+AONLY = {0, 6, 8, 9}  # 64x160 tilings: the B operand must be KC (160 is not an RC tile width)
+
+
+def _H():
+    from rl_ctr_prediction_amd import hip_ops
+    return hip_ops
+
+
+def _planes(H, X, rc, dev):
+    """Planes of operand X [rows, K] in the requested orientation: KC stores X itself,
+    RC stores X^T ([K, rows])."""
+    src = (X.t() if rc else X).contiguous().to(dev)
+    return H.split_planes(src)
+
+
+def _run(H, A, Bm, a_rc, b_rc, dev, **kw):
+    """C = A @ Bm with A [M,K], Bm [K,N]; B planes hold Bm^T ([N,K]) unless b_rc."""
+    pa = _planes(H, A, a_rc, dev)
+    pb = H.split_planes((Bm if b_rc else Bm.t()).contiguous().to(dev))
+    return H.gemm_planes(pa, pb, a_rc, b_rc, **kw)
+
+
+def test_split_planes_exact(cuda):
+    """Exact for every fp32 value whose three planes are normal bf16 numbers: |x| from
+    ~1e-33 (x2 ~ 2^-16 |x| stays above the bf16/fp32 normal minimum 2^-126; the hardware
+    conversion flushes subnormals) up to the bf16 overflow threshold (~3.39e38). Outside
+    that range the split is off by < 2^-126 absolute (tiny values) — never reached by the
+    MLP's activations, gradients or weights."""
+    H = _H()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(37, 101, generator=g) * torch.logspace(-30, 30, 101).float()
+    x[0, :5] = torch.tensor([0.0, -0.0, 1e-30, -3.3e38, 1.0])
+    p = H.split_planes(x.to(cuda))
+    assert (p.rows_pad, p.cols_pad) == (64, 128)
+    back = p.to_float().cpu()
+    assert torch.equal(back.view(torch.int32)[x != 0], x.view(torch.int32)[x != 0])
+    assert torch.equal(back[x == 0], x[x == 0])
+    t = p.t.float().cpu()
+    assert (t[:, 37:, :] == 0).all() and (t[:, :, 101:] == 0).all()
+
+
+@pytest.mark.parametrize("a_rc,b_rc", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(8192, 300, 1664), (8192, 200, 300), (8192, 300, 200),
+                                   (8192, 1664, 300), (200, 300, 8192), (300, 1664, 8192),
+                                   (1, 1, 1), (37, 50, 70), (130, 70, 33)])
+def test_gemm_planes_exact_integer_data(cuda, a_rc, b_rc, M, N, K):
+    """Integers in [-3, 3]: every product and every partial sum (|C| <= 9K < 2^24) is exact
+    in fp32, so the result must equal fp64 bit for bit — any layout error is caught."""
+    H = _H()
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randint(-3, 4, (M, K), generator=g).float()
+    Bm = torch.randint(-3, 4, (K, N), generator=g).float()
+    C = _run(H, A, Bm, a_rc, b_rc, cuda).cpu().double()
+    ref = A.double() @ Bm.double()
+    assert torch.equal(C, ref), (int((C != ref).sum()), M, N, K)
+
+
+@pytest.mark.parametrize("M,N,K,a_rc,b_rc", [(8192, 300, 1664, False, False),
+                                             (8192, 200, 300, False, False),
+                                             (8192, 300, 200, False, True),
+                                             (8192, 1664, 300, False, True),
+                                             (200, 300, 8192, True, True),
+                                             (300, 1664, 8192, True, True)])
+def test_gemm_planes_accuracy_vs_fp32_mfma(cuda, M, N, K, a_rc, b_rc):
+    """The DeepFM MLP shapes in their trainer orientations: error against fp64 relative to
+    the L1 bound is below 1e-6 and no larger than the exact-fp32 MFMA kernel's."""
+    H = _H()
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(M, K, generator=g) * 0.1
+    Bm = torch.randn(K, N, generator=g)
+    ref = A.double() @ Bm.double()
+    bound = A.double().abs() @ Bm.double().abs()
+    C = _run(H, A, Bm, a_rc, b_rc, cuda).cpu().double()
+    err = ((C - ref).abs() / bound).max().item()
+    Ce = H.gemm(A.to(cuda), Bm.to(cuda), algo=H.GEMM_EXACT_F32).cpu().double()
+    err_exact = ((Ce - ref).abs() / bound).max().item()
+    assert err < 1e-6, err
+    assert err <= err_exact, (err, err_exact)
+
+
+@pytest.mark.parametrize("tile", range(N_TILES))
+def test_gemm_planes_every_tiling(cuda, tile, monkeypatch):
+    """Each tiling forced, split-K 1 and 3, every orientation it supports, M/N edges and a
+    K that is not a multiple of 32: integer data (bitwise) and random data (fp32 bar)."""
+    H = _H()
+    g = torch.Generator().manual_seed(tile)
+    for splits in (1, 3):
+        monkeypatch.setenv("CTR_GEMM_PLANES_CFG", f"{tile},{splits}")
+        for (M, N, K) in ((333, 452, 1060), (97, 451, 259)):
+            Ai = torch.randint(-3, 4, (M, K), generator=g).float()
+            Bi = torch.randint(-3, 4, (K, N), generator=g).float()
+            A = torch.randn(M, K, generator=g)
+            Bm = torch.randn(K, N, generator=g)
+            ref = A.double() @ Bm.double()
+            bound = A.double().abs() @ Bm.double().abs()
+            for a_rc in (False, True):
+                for b_rc in (False, True):
+                    if b_rc and tile in AONLY:
+                        continue
+                    cfg = H.gemm_planes_config(a_rc, b_rc, M, N, K)
+                    assert cfg["tile"] == tile and cfg["splits"] == splits, cfg
+                    Ci = _run(H, Ai, Bi, a_rc, b_rc, cuda).cpu().double()
+                    assert torch.equal(Ci, Ai.double() @ Bi.double()), (tile, splits, a_rc, b_rc)
+                    C = _run(H, A, Bm, a_rc, b_rc, cuda).cpu().double()
+                    bad = (C - ref).abs() > 2e-6 * bound + 1e-30
+                    assert not bad.any(), (tile, splits, M, N, K, a_rc, b_rc, int(bad.sum()))
+
+
+def test_gemm_planes_epilogues_and_output_planes(cuda):
+    """bias / ReLU / dropout (the same stateless mask as ctr_gemm_f32 for the same seed,
+    offset and step) / GRAD_MASK; the output planes are exactly split(fp32 output)."""
+    H = _H()
+    g = torch.Generator().manual_seed(0)
+    M, N, K = 512, 300, 128
+    A, W, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    d = lambda t: t.contiguous().to(cuda)  # noqa: E731
+    pa, pw = H.split_planes(d(A)), H.split_planes(d(W))
+    step = torch.tensor([3], dtype=torch.int32, device=cuda)
+    for epi, kw in ((H.EPI_BIAS, {}), (H.EPI_BIAS_RELU, {}),
+                    (H.EPI_BIAS_RELU_DROP, dict(drop_p=0.2, seed=123, offset=777, step_dev=step))):
+        outp = H.Planes(M, N, cuda)
+        y = torch.empty(M, N, device=cuda)
+        H.gemm_planes(pa, pw, False, False, epi=epi, bias=d(bias), out=y, out_planes=outp, **kw)
+        yr = H.gemm(d(A), d(W), False, True, epi=epi, bias=d(bias), **kw)
+        ref = A.double() @ W.double().t() + bias.double()
+        if epi != H.EPI_BIAS:
+            ref = ref.clamp(min=0)
+        if epi == H.EPI_BIAS_RELU_DROP:  # identical mask as the fp32-operand GEMM
+            assert torch.equal(y == 0, yr == 0)
+            ref = torch.where(yr.cpu() == 0, torch.zeros_like(ref), ref * 1.25)
+        np.testing.assert_allclose(y.cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-4)
+        assert torch.equal(outp.to_float(), y)
+        assert torch.equal(outp.t, H.split_planes(y).t)
+    aux = d(torch.where(torch.rand(M, N, generator=g) < 0.3, 0.0, 1.0))
+    gm = H.gemm_planes(pa, pw, False, False, epi=H.EPI_GRAD_MASK, aux=aux, scale=1.25).cpu().double()
+    refm = torch.where(aux.cpu() > 0, (A.double() @ W.double().t()) * 1.25, torch.zeros(M, N).double())
+    np.testing.assert_allclose(gm.numpy(), refm.numpy(), rtol=1e-5, atol=1e-4)
+    # planes only (no fp32 output), through the split-K reduce too
+    outp = H.Planes(M, N, cuda)
+    H.gemm_planes(pa, pw, False, False, out_planes=outp)
+    ref = (A.double() @ W.double().t())
+    np.testing.assert_allclose(outp.to_float().cpu().double().numpy(), ref.numpy(), rtol=1e-5,
+                               atol=1e-4)

@@ -1,0 +1,60 @@
+"""Time the deferred-Adam flush (every row replays `steps` missed g = wd*p steps) at a
+config's table shape: python tools/flush_bench.py [--V 10000000] [--K 64] [--steps 20] [--reps 5]
+
+Each rep resets last[] to 0, so every row replays all `steps` steps (the bench's worst
+case: a row untouched for the whole timed region). Prints one JSON line: ms per flush,
+algorithmic HBM GB/s (24 B per element: read+write p, m, v; + the linear table and last[])
+and replayed element-steps per second.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from rl_ctr_prediction_amd import hip_ops as H  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--V", type=int, default=10_000_000)
+    ap.add_argument("--K", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-lin", action="store_true")
+    args = ap.parse_args()
+    V, K, T = args.V, args.K, args.steps
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    E = torch.randn(V, K, device=dev, generator=g).mul_(0.05)
+    mE = torch.randn(V, K, device=dev, generator=g).mul_(1e-4)
+    vE = torch.rand(V, K, device=dev, generator=g).mul_(1e-8)
+    lin = None if args.no_lin else torch.randn(V, device=dev, generator=g).mul_(0.05)
+    ml = None if lin is None else torch.zeros_like(lin)
+    vl = None if lin is None else torch.zeros_like(lin)
+    last = torch.zeros(V, dtype=torch.int32, device=dev)
+    tab = H.AdamStepTable(1e-3, (0.9, 0.999), dev)
+    times = []
+    for r in range(args.reps + 1):
+        last.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        H.adam_deferred_flush(E, mE, vE, lin, ml, vl, last, T, tab, weight_decay=1e-5)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            times.append(e0.elapsed_time(e1))
+    ms = sorted(times)[len(times) // 2]
+    nbytes = 24 * V * K + (0 if lin is None else 24 * V) + 8 * V
+    print(json.dumps({"kernel": "deferred_flush_vec (+deferred_flush_lin)", "V": V, "K": K,
+                      "steps_replayed": T, "ms": ms, "ms_all": times,
+                      "GBps": nbytes / (ms * 1e-3) / 1e9,
+                      "elem_steps_per_s": V * (K + (0 if lin is None else 1)) * T / (ms * 1e-3)}))
+
+
+if __name__ == "__main__":
+    main()

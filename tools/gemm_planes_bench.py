@@ -1,0 +1,92 @@
+"""Time the DeepFM MLP GEMMs (C3: B=8192, 1664-300-200) on pre-split planes, in the
+orientations the fused trainer uses, per tiling / split-K (CTR_GEMM_PLANES_CFG).
+
+    python tools/gemm_planes_bench.py [--reps 20] [--sweep] [--B 8192] [--W 1664]
+
+Prints one JSON line per (shape, config): microseconds per launch (HIP events around
+`reps` back-to-back launches, median of 3 groups), fp32-equivalent TFLOP/s (2*M*N*K) and
+the bf16 MFMA rate actually issued (6 products).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from rl_ctr_prediction_amd import hip_ops as H  # noqa: E402
+
+
+def shapes(B, W, H1=300, H2=200):
+    # name: (M, N, K, a_rc, b_rc)
+    return {"fwd0 X.W0^T": (B, H1, W, False, False),
+            "fwd1 H1.W1^T": (B, H2, H1, False, False),
+            "dH1 dH2.W1": (B, H1, H2, False, True),
+            "dX dH1.W0": (B, W, H1, False, True),
+            "dW1 dH2^T.H1": (H2, H1, B, True, True),
+            "dW0 dH1^T.X": (H1, W, B, True, True)}
+
+
+def time_one(pa, pb, a_rc, b_rc, out, reps):
+    H.gemm_planes(pa, pb, a_rc, b_rc, out=out)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            H.gemm_planes(pa, pb, a_rc, b_rc, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+    return sorted(ts)[1]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true", help="every tiling x split-K in {1,2,4,8}")
+    ap.add_argument("--B", type=int, default=8192)
+    ap.add_argument("--W", type=int, default=1664)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    total = 0.0
+    for name, (M, N, K, a_rc, b_rc) in shapes(args.B, args.W).items():
+        A = torch.randn(*((K, M) if a_rc else (M, K)), device=dev, generator=g)
+        Bm = torch.randn(*((K, N) if b_rc else (N, K)), device=dev, generator=g)
+        pa, pb = H.split_planes(A), H.split_planes(Bm)
+        out = torch.empty(M, N, device=dev)
+        cfgs = ["auto"]
+        if args.sweep:
+            cfgs += [f"{t},{s}" for t in range(20) for s in (1, 2, 4, 8)
+                     if not (b_rc and t in (0, 6, 8, 9))]
+        best = None
+        for cfg in cfgs:
+            if cfg == "auto":
+                os.environ.pop("CTR_GEMM_PLANES_CFG", None)
+            else:
+                os.environ["CTR_GEMM_PLANES_CFG"] = cfg
+            chosen = H.gemm_planes_config(a_rc, b_rc, M, N, K)
+            us = time_one(pa, pb, a_rc, b_rc, out, args.reps)
+            tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+            print(json.dumps({"shape": name, "cfg": cfg, "chosen": chosen, "us": round(us, 2),
+                              "TFLOPs_fp32eq": round(tf, 1), "bf16_TFLOPs": round(6 * tf, 1)}),
+                  flush=True)
+            if cfg == "auto":
+                auto_us = us
+            if best is None or us < best[1]:
+                best = (cfg, us)
+        os.environ.pop("CTR_GEMM_PLANES_CFG", None)
+        total += auto_us
+        if args.sweep:
+            print(json.dumps({"shape": name, "best": best[0], "us": round(best[1], 2)}), flush=True)
+    print(json.dumps({"sum_auto_us": round(total, 1)}))
+
+
+if __name__ == "__main__":
+    main()
