@@ -416,7 +416,7 @@ def main():
                  f"by HIP events; ms per step",
         "adam_rows" if args.optimizer == "deferred" else "adam_embedding_vec":
             {"ms_per_step": per_step["adam"]},
-        "flush (deferred_flush_vec, once per region)": {"ms_per_step": per_step["flush"]},
+        "flush (deferred_flush_tile, once per region)": {"ms_per_step": per_step["flush"]},
         "_graphs": "timed region: HIP-graph replay of the whole step (N=1); breakdown and "
                    "roofline passes: eager launches with HIP events",
         "gemm_f32_kernel (MLP, fwd+bwd)": {
@@ -467,7 +467,7 @@ def main():
                      "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each launch of this "
                                "kernel over K eager steps right after the timed region"})
-    kernels["flush (deferred_flush_vec, once per region)"]["region_of_K_steps_ms_total"] = \
+    kernels["flush (deferred_flush_tile, once per region)"]["region_of_K_steps_ms_total"] = \
         total_ms(timing["flush"])
     gather_ms, scatter_ms = avg_ms(bd["gather"]), avg_ms(bd["scatter"])
     value = world * B * args.steps / elapsed

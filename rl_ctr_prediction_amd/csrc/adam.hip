@@ -352,15 +352,29 @@ __global__ __launch_bounds__(256) void deferred_sweep_vec(
   }
 }
 
-// Every row to `step` (epoch end / checkpoint / eval). Rows already current cost 4 B.
-// The per-step scalars of steps 1..step are staged once per block in LDS (one ds_read_b64
-// per replayed step instead of a dependent global load); the linear table has its own
-// thread-per-row pass (deferred_flush_lin, run first: it reads last[] without writing it).
+// Every row to `step` (epoch end / checkpoint / eval; deferred_flush_tile below). Rows
+// already current cost 4 B. The per-step scalars of steps 1..step are staged once per block
+// in LDS (one ds_read_b64 per replayed step instead of a dependent global load).
 constexpr int kMaxLdsSteps = 8192;  // 64 KiB of float2
 
-template <int K4, bool LDS_TAB>
-__global__ __launch_bounds__(256) void deferred_flush_vec(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE, int64_t V,
+// tiled flush tuning (tools/build_variant.py): rows per batch = CTR_FLUSH_UNR wave-
+// instructions (4 measured best: 2.59 ms at 1 replayed step, 4.46 ms at 20, C3 table)
+#ifndef CTR_FLUSH_UNR
+#define CTR_FLUSH_UNR 4
+#endif
+
+// The flush, tiled (what ctr_adam_deferred_flush launches): a wave owns 64 consecutive
+// rows. Lane l holds last[base + l] and the linear weight's (p, m, v) of row base + l —
+// coalesced 256-B accesses, replayed in-lane — and the [64, K] slabs of E, m_E, v_E stream
+// through in float4 columns, UNR wave-instructions' worth of rows per batch: every load of
+// a batch is issued before its replay, so each wave keeps 3 x UNR KiB in flight, and the
+// replay of the batch's rows runs as one step loop over all of them (4 x UNR independent
+// chains per lane). Tiles whose rows are all current are skipped on one vote; last[] is
+// written back coalesced. Same adam_elem, same per-step scalars: bitwise the old pass.
+template <int K4, int UNR, bool LDS_TAB>
+__global__ __launch_bounds__(256) void deferred_flush_tile(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
     int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
   extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
   if (LDS_TAB) {
@@ -368,42 +382,70 @@ __global__ __launch_bounds__(256) void deferred_flush_vec(
       s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
     __syncthreads();
   }
-  const int c = threadIdx.x % K4;
-  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  constexpr int RPI = kWave / K4;  // rows per wave-instruction
+  constexpr int ITERS = K4;        // wave-instructions per 64-row tile
+  static_assert(ITERS % UNR == 0, "batches of UNR instructions");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = lane % K4, r_in = lane / K4;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int64_t n_tiles = (V + kWave - 1) / kWave;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; r < V; r += groups) {
-    const int from = last[r];
-    if (from >= step) continue;
-    const int64_t e = r * K4 + c;
-    float4 pp = E[e], mm = mE[e], vv = vE[e];
-    for (int s = from + 1; s <= step; ++s) {
-      if (LDS_TAB) {
-        const float2 t = s_tab[s];
-        h.neg_step_size = t.x;
-        h.inv_bc2_sqrt = t.y;
-      } else {
-        load_step(h, tab, s);
+  auto set_step = [&](int t) {
+    if (LDS_TAB) {
+      const float2 v = s_tab[t];
+      h.neg_step_size = v.x;
+      h.inv_bc2_sqrt = v.y;
+    } else {
+      load_step(h, tab, t);
+    }
+  };
+  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+       tile < n_tiles; tile += waves) {
+    const int64_t base = tile * kWave;
+    const int64_t my = base + lane;
+    const bool ok = my < V;
+    const int from_l = ok ? last[my] : step;
+    if (__all(from_l >= step)) continue;  // every row of the tile is current
+    if (w && from_l < step) {
+      float pp = w[my], mm = mw[my], vv = vw[my];
+      for (int s = from_l + 1; s <= step; ++s) {
+        set_step(s);
+        adam_elem(pp, 0.f, mm, vv, h);
       }
-      adam_vec(pp, z4, mm, vv, h);
+      w[my] = pp; mw[my] = mm; vw[my] = vv;
     }
-    E[e] = pp; mE[e] = mm; vE[e] = vv;
-    if (c == 0) last[r] = step;
-  }
-}
-
-__global__ __launch_bounds__(256) void deferred_flush_lin(
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
-    const int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < V;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int from = last[r];
-    if (from >= step) continue;
-    float pp = w[r], mm = mw[r], vv = vw[r];
-    for (int s = from + 1; s <= step; ++s) {
-      load_step(h, tab, s);
-      adam_elem(pp, 0.f, mm, vv, h);
+    // (measured: issuing batch b+1's loads before batch b's replay, through a second
+    // register buffer, made the 20-step flush 12 % slower; the unprefetched batch loop is
+    // kept — tools/_run_flush2.sh variants)
+#pragma unroll 1
+    for (int it0 = 0; it0 < ITERS; it0 += UNR) {
+      float4 pp[UNR], mm[UNR], vv[UNR];
+      int from[UNR];
+      int64_t e[UNR];
+      int f0 = step;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = (it0 + u) * RPI + r_in;
+        from[u] = __shfl(from_l, r, kWave);  // lanes past V hold `step`: skipped
+        e[u] = (base + r) * K4 + c;
+        f0 = min(f0, from[u]);
+        if (from[u] < step) {
+          pp[u] = E[e[u]]; mm[u] = mE[e[u]]; vv[u] = vE[e[u]];
+        }
+      }
+      for (int s = f0 + 1; s <= step; ++s) {
+        set_step(s);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (s > from[u]) adam_vec(pp[u], z4, mm[u], vv[u], h);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (from[u] < step) {
+          E[e[u]] = pp[u]; mE[e[u]] = mm[u]; vE[e[u]] = vv[u];
+        }
     }
-    w[r] = pp; mw[r] = mm; vw[r] = vv;
+    if (from_l < step) last[my] = step;
   }
 }
 
@@ -631,36 +673,33 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
   const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
   hipStream_t st = as_stream(stream);
   if (deferred_vec_ok(K, emb, m_emb, v_emb, nullptr)) {
-    if (lin) {  // first: it reads last[] and the E pass below rewrites it
-      const unsigned gl = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
-      hipLaunchKernelGGL(deferred_flush_lin, gl, 256, 0, st, lin, m_lin, v_lin, V, last,
-                         (int)step, step_table, h);
-      CTR_LAUNCH_CHECK("deferred_flush_lin");
-    }
     const int K4 = K / 4;
-    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V * K4, 256), 8192);
+    const int64_t n_tiles = ceil_div(V, kWave);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_tiles, 4), 8192));
     const bool lds = step < kMaxLdsSteps;
     const size_t lds_bytes = lds ? (size_t)(step + 1) * sizeof(float2) : 0;
-#define CTR_DEF_FLUSH(K4_)                                                                      \
+#define CTR_DEF_FLUSH(K4_, UNR_)                                                                 \
   if (lds)                                                                                      \
-    hipLaunchKernelGGL((deferred_flush_vec<K4_, true>), grid, 256, lds_bytes, st,               \
+    hipLaunchKernelGGL((deferred_flush_tile<K4_, UNR_, true>), grid, 256, lds_bytes, st,        \
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
-                       reinterpret_cast<float4*>(v_emb), V, last, (int)step, step_table, h);    \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
+                       step_table, h);                                                          \
   else                                                                                          \
-    hipLaunchKernelGGL((deferred_flush_vec<K4_, false>), grid, 256, 0, st,                      \
+    hipLaunchKernelGGL((deferred_flush_tile<K4_, UNR_, false>), grid, 256, 0, st,               \
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
-                       reinterpret_cast<float4*>(v_emb), V, last, (int)step, step_table, h)
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
+                       step_table, h)
     switch (K4) {
-      case 1: CTR_DEF_FLUSH(1); break;
-      case 2: CTR_DEF_FLUSH(2); break;
-      case 4: CTR_DEF_FLUSH(4); break;
-      case 8: CTR_DEF_FLUSH(8); break;
-      case 16: CTR_DEF_FLUSH(16); break;
-      case 32: CTR_DEF_FLUSH(32); break;
-      case 64: CTR_DEF_FLUSH(64); break;
+      case 1: CTR_DEF_FLUSH(1, 1); break;
+      case 2: CTR_DEF_FLUSH(2, 2); break;
+      case 4: CTR_DEF_FLUSH(4, 4); break;
+      case 8: CTR_DEF_FLUSH(8, CTR_FLUSH_UNR); break;
+      case 16: CTR_DEF_FLUSH(16, CTR_FLUSH_UNR); break;
+      case 32: CTR_DEF_FLUSH(32, CTR_FLUSH_UNR); break;
+      case 64: CTR_DEF_FLUSH(64, CTR_FLUSH_UNR); break;
     }
 #undef CTR_DEF_FLUSH
-    CTR_LAUNCH_CHECK("deferred_flush_vec");
+    CTR_LAUNCH_CHECK("deferred_flush_tile");
     return CTR_OK;
   }
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 256), 8192);
