@@ -17,10 +17,14 @@ one episode over the ranks with the single-process result (pg_model.py).
 c5 = configs[4]: FM, Avazu-shape 22 fields, 40M vocab, dim 128, batch 8192 per GPU; N>1
 row-shards the table across the ranks (all-to-all), the configuration it is quoted on.
 
-The JSON line carries `roofline` for the dominant kernel (the dense Adam pass over the
-table, adam_embedding_vec, timed per launch with HIP events on its stream inside the
-timed region) and `cpu_baseline` (the oracle = torch-CPU restatement of the reference,
-timed on this host's cores on a bounded sample of the same workload, rank 0 at N=1).
+The JSON line carries `roofline` for the dominant kernel group of the step — chosen by an
+un-timed breakdown pass among the MLP GEMMs (C3/IPNN: gemm_planes_kernel, fp32-equivalent
+TFLOP/s against the fp32 MFMA peak), the deferred-Adam flush (C2/C5: deferred_flush_tile,
+HBM GB/s: 24 B per element + 8 B per row), the gather, the sparse plan, the scatter and the
+Adam row passes — with its per-launch duration measured by HIP events on the launch stream
+in eager steps right after the timed region; and `cpu_baseline` (the oracle = torch-CPU
+restatement of the reference, timed on this host's cores on a bounded sample of the same
+workload, rank 0 at N=1, with the CPU model named).
 """
 from __future__ import annotations
 
@@ -41,6 +45,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "CTR train examples/sec at 1/2/4/8 MI355X; HBM GB/s on embedding gather/scatter"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32), spec
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (the split GEMM's pipe)
 
 CONFIGS = {
     "c3": dict(kind="DeepFM", V=10_000_000, F=26, K=64, B=8192,
@@ -94,6 +99,22 @@ def plan_bytes(S, U):
     return S * 20 + U * 8
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def flush_bytes(V, K, lin=True):
+    """deferred_flush_tile, algorithmic: read + write p, m, v of every element (24 B) and of
+    the linear weight, read + write last[] (8 B per row)."""
+    return 24 * V * K + (24 * V if lin else 0) + 8 * V
+
+
 def cpu_baseline(cfg, batches, max_seconds=25.0):
     """The oracle (torch-CPU restatement, pinned to the reference) on this host."""
     from oracle import ctr_oracle as O
@@ -116,6 +137,7 @@ def cpu_baseline(cfg, batches, max_seconds=25.0):
             break
     eps = n * cfg["B"] / t
     return {"value": eps, "unit": "examples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{n} timed steps (+1 warm-up) of the same workload and batches on the "
                       f"host CPU, oracle/ctr_oracle.py train_step (torch-CPU ops as the "
                       f"reference: dense nn.Embedding grads, torch.optim.Adam); "
@@ -141,6 +163,7 @@ def cpu_baseline_pg(cfg, episodes, max_seconds=25.0):
         t += time.perf_counter() - s
         n += 1
     return {"value": n * cfg["B"] / t, "unit": "transitions/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{n} timed learn() calls (+1 warm-up) on the same episodes, "
                       f"oracle/ctr_oracle.py pg_learn (torch-CPU: FE state, policy MLP, "
                       f"loss_func, Adam); {t / n * 1e3:.0f} ms per episode"}
@@ -160,9 +183,18 @@ def bench_pg(args, cfg, world, rank, dev):
     n_eps = max(1, min(args.batches, args.warmup))
     rng = np.random.default_rng([4, rank])
     host = []
+    # reward r_b = -BCE(y_b, p_{a_b}) (SURVEY.md §8d's C4 definition; the reference's is
+    # commented out, hybrid_td3_main_per_v10.py:147-150): p_{b,a} = the pCTR of candidate
+    # model a — synthetic here: the planted FM logit of the batch with a fixed per-action
+    # distortion (model a's logit shrunk by 1/(1+0.1a) and shifted by 0.25a)
     for x, y in synth.batches(n_eps, B, rank=rank):
         a = rng.integers(1, A + 1, size=(B, 1)).astype(np.int64)
-        host.append((x, a, y.reshape(-1, 1).astype(np.float32)))
+        z0 = np.log(0.25 / 0.75) + synth.planted_logit(x)
+        za = z0[:, None] / (1.0 + 0.1 * np.arange(1, A + 1)) + 0.25 * np.arange(1, A + 1)
+        pa = 1.0 / (1.0 + np.exp(-za[np.arange(B), a[:, 0] - 1]))
+        yb = y.astype(np.float64)
+        bce = -(yb * np.maximum(np.log(pa), -100.0) + (1 - yb) * np.maximum(np.log1p(-pa), -100.0))
+        host.append((x, a, (-bce).reshape(-1, 1).astype(np.float32)))
     eps = [tuple(torch.from_numpy(t).to(dev) for t in e) for e in host]
 
     def step(i):
@@ -239,8 +271,8 @@ def bench_pg(args, cfg, world, rank, dev):
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: Criteo-shape ids as states, uniform actions, reward = click label "
-                "(planted-FM); random-init weights",
+        "data": "synthetic: Criteo-shape ids as states, uniform actions, reward = -BCE(y, "
+                "p_a) of the chosen candidate model's pCTR (SURVEY §8d C4); random-init weights",
         "config": {"workload": cfg["workload"], "model": "PolicyGradient (Net, fix_input_dims)",
                    "episode_transitions": B * world, "fields": F, "vocab": V, "embed_dim": K,
                    "actions": A, "parallelism": f"dp{world}" + (
@@ -372,7 +404,8 @@ def main():
     torch.cuda.synchronize()
     bd, trainer.timing = trainer.timing, None
     per_step = {k: total_ms(v) / n_bd for k, v in bd.items()}
-    dominant = max(("adam", "gather", "plan", "scatter", "gemm"), key=lambda k: per_step[k])
+    dominant = max(("adam", "gather", "plan", "scatter", "gemm", "flush"),
+                   key=lambda k: per_step[k])
 
     if world > 1:
         dist.barrier()
@@ -419,7 +452,7 @@ def main():
         "flush (deferred_flush_tile, once per region)": {"ms_per_step": per_step["flush"]},
         "_graphs": "timed region: HIP-graph replay of the whole step (N=1); breakdown and "
                    "roofline passes: eager launches with HIP events",
-        "gemm_f32_kernel (MLP, fwd+bwd)": {
+        "MLP GEMMs (gemm_planes_kernel + split-K reduce, fwd+bwd)": {
             "ms_per_step": per_step["gemm"],
             "TFLOP/s": gemm_flops_bd / (total_ms(bd["gemm"]) * 1e-3) / 1e12 if bd["gemm"] else None},
         "gather (fm_forward_vec)": {"ms_per_step": per_step["gather"]},
@@ -433,13 +466,16 @@ def main():
     if dominant == "gemm":
         flops = sum(w for _, _, w in spans) / len(spans)
         achieved = flops / (launch_ms * 1e-3) / 1e12
-        roofline = {"kernel": "MLP GEMMs (gemm_sb16_kernel: fp32-accurate split-bf16 MFMA; "
-                              "gemm_f32_kernel: fp32 MFMA), the 6 of a step averaged per launch",
+        roofline = {"kernel": "MLP GEMMs (gemm_planes_kernel: fp32-accurate split-bf16 MFMA on "
+                              "pre-split operand planes, + split-K reduce), the 6 of a step "
+                              "averaged per launch",
                     "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
-                    "peak_note": "fp32 matrix peak (the path's dtype); the split-bf16 "
-                                 "algorithm's own ceiling is 2.5 PF bf16 / 6 products = "
-                                 "417 TF",
+                    "peak_note": "fp32 matrix peak (the path's dtype; achieved = 2*M*N*K / "
+                                 "launch time); the split-bf16 algorithm issues 6 bf16 MFMA "
+                                 "products per fp32 product: bf16_mfma_frac = 6*achieved / "
+                                 "2500 TF bf16 dense",
+                    "bf16_mfma_frac": 6.0 * achieved / MFMA_BF16_PEAK_TFS,
                     "algorithmic_flops_per_launch": flops}
         traffic, src = load_traffic(args.config, "gemm")
     else:
@@ -450,6 +486,10 @@ def main():
             else:  # catch-up or apply of the batch's U rows: read+write p,m,v (+grad rows)
                 nbytes = U * 24 * (K + 1) + U * (4 * K + 8) // 2
                 kname = "deferred_rows_vec (catch-up / apply of the batch's rows, per launch)"
+        elif dominant == "flush":
+            nbytes = flush_bytes(trainer.V_tab, K, lin=trainer.w_tab is not None)
+            kname = ("deferred_flush_tile (every row of the table brought to the region's last "
+                     "step, once per timed region)")
         elif dominant == "gather":
             nbytes, kname = gather_bytes(S, K, B, deep), "fm_forward_vec (embedding gather + FM)"
         elif dominant == "scatter":
@@ -462,7 +502,8 @@ def main():
         roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": nbytes}
-        traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec"}.get(dominant, dominant))
+        traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec",
+                                                  "flush": "deferred_flush_tile"}.get(dominant, dominant))
     roofline.update({"traffic": traffic, "traffic_source": src, "avg_launch_ms": launch_ms,
                      "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each launch of this "

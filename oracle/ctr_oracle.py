@@ -381,9 +381,11 @@ def pg_learn(policy: torch.nn.Sequential, opt, E: torch.Tensor, states: torch.Te
 
 # --------------------------------------------------------------------- driver -------
 def pretrain_run(kind: str, train: np.ndarray, test: np.ndarray, V: int, K: int, epochs: int,
-                 lr: float, wd: float, batch: int, seed: int = 1, drop_p: float = 0.0):
+                 lr: float, wd: float, batch: int, seed: int = 1, drop_p: float = 0.0,
+                 lr_step: float = 0.0):
     """all_main/pretrain_main.main without files: Adam re-created every epoch, batches in
-    file order, train loss = mean of batch losses, AUC over the test split."""
+    file order, train loss = mean of batch losses, AUC over the test split.
+    lr_step: main/pretrain_main.py:180 adds 1e-4 to the learning rate before every epoch."""
     from sklearn.metrics import roc_auc_score
     F = train.shape[1] - 1
     params = init_params(kind, V, F, K, seed=seed)
@@ -391,6 +393,7 @@ def pretrain_run(kind: str, train: np.ndarray, test: np.ndarray, V: int, K: int,
     xt = torch.from_numpy(test[:, 1:]).long()
     yt = torch.from_numpy(test[:, 0]).float()
     for _ in range(epochs):
+        lr += lr_step
         opt = make_optimizer(params, lr, wd)
         losses = []
         for s in range(0, len(train), batch):

@@ -534,18 +534,30 @@ class AdamStepTable:
         self.tab = torch.zeros(2, dtype=torch.float32, device=device)
         self.ensure(capacity)
 
+    def _host(self, cap: int) -> torch.Tensor:
+        host = torch.zeros(2 * (cap + 1), dtype=torch.float64)
+        for t in range(1, cap + 1):
+            ss, bc2s = adam_scalars(t, self.lr, self.betas)
+            host[2 * t] = -ss
+            host[2 * t + 1] = 1.0 / bc2s
+        return host.to(torch.float32)
+
     def ensure(self, step: int) -> torch.Tensor:
         if step > self.capacity:
             cap = max(step, 2 * self.capacity, 1024)
-            host = torch.zeros(2 * (cap + 1), dtype=torch.float64)
-            for t in range(1, cap + 1):
-                ss, bc2s = adam_scalars(t, self.lr, self.betas)
-                host[2 * t] = -ss
-                host[2 * t + 1] = 1.0 / bc2s
-            self.tab = host.to(torch.float32).to(self.device)
+            self.tab = self._host(cap).to(self.device)
             self.capacity = cap
             self.version += 1
         return self.tab
+
+    def set_lr(self, lr: float) -> None:
+        """A new learning rate (the driver's `learning_rate += 1e-4` before each epoch's
+        Adam): the values are rewritten IN PLACE, so captured HIP graphs, which hold the
+        table's address, stay valid and read the new scalars at their next replay."""
+        if float(lr) == self.lr:
+            return
+        self.lr = float(lr)
+        self.tab.copy_(self._host(self.capacity), non_blocking=False)
 
 
 def adam_deferred_rows(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "SparsePlanBuffers",

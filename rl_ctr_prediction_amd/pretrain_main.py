@@ -67,7 +67,9 @@ class AutogradTrainer:
         self.loss = nn.BCELoss()
         self.reset_optimizer()
 
-    def reset_optimizer(self):
+    def reset_optimizer(self, lr=None):
+        if lr is not None:
+            self.lr = lr
         self.opt = torch.optim.Adam(self.model.parameters(), lr=self.lr,
                                     weight_decay=self.weight_decay)
 
@@ -170,16 +172,20 @@ def eva_stopping(valid_aucs, valid_losses, type):  # noqa: A002 (reference name)
 
 
 def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, learning_rate,
-         weight_decay, early_stop_type, batch_size, device, save_param_dir, verbose=True):
+         weight_decay, early_stop_type, batch_size, device, save_param_dir, verbose=True,
+         _epoch_fn=None):
+    """_epoch_fn(model, trainer, train_fm, loss, device, batch_size) -> mean train loss: the
+    epoch loop of a driver variant (pretrain_main_2's slicing loop); default: DeviceBatches."""
     if not os.path.exists(save_param_dir + campaign_id):
         os.mkdir(save_param_dir + campaign_id)
     device = torch.device(device)
     train_fm, train_data, test_data, field_nums, feature_nums = get_dataset(
         data_path, dataset_name, campaign_id)
-    train_dataset = Data.libsvm_dataset(train_data[:, 1:], train_data[:, 0])
     test_dataset = Data.libsvm_dataset(test_data[:, 1:], test_data[:, 0])
-    train_data_loader = DeviceBatches(train_dataset, batch_size, device)
     test_data_loader = DeviceBatches(test_dataset, batch_size, device)
+    if _epoch_fn is None:
+        train_dataset = Data.libsvm_dataset(train_data[:, 1:], train_data[:, 0])
+        train_data_loader = DeviceBatches(train_dataset, batch_size, device)
 
     model = get_model(model_name, feature_nums, field_nums, latent_dims).to(device)
     loss = nn.BCELoss()
@@ -194,7 +200,10 @@ def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, l
     for epoch_i in range(epoch):
         train_start_time = datetime.datetime.now()
         trainer.reset_optimizer()  # torch.optim.Adam(...) re-created every epoch (line 153)
-        train_average_loss = train(model, trainer, train_data_loader, loss, device)
+        if _epoch_fn is None:
+            train_average_loss = train(model, trainer, train_data_loader, loss, device)
+        else:
+            train_average_loss = _epoch_fn(model, trainer, train_fm, loss, device, batch_size)
         torch.save(model.state_dict(),
                    save_param_dir + campaign_id + model_name + str(np.mod(epoch_i, 5)) + ".pth")
         auc, valid_loss = test(model, test_data_loader, loss, device)

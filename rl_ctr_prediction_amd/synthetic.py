@@ -87,6 +87,19 @@ class CriteoSynth:
             out[:, f] = self.offset[f] + local
         return out
 
+    def planted_logit(self, x: np.ndarray) -> np.ndarray:
+        """The planted FM's logit of each example, without the CTR shift (float64 [B])."""
+        w = 0.01 * _gauss_hash(x, 1)
+        z = w.sum(axis=1)
+        s = np.zeros(x.shape[0])
+        q = np.zeros(x.shape[0])
+        for d in range(4):
+            v = 0.01 * _gauss_hash(x, 100 + d)
+            s_d = v.sum(axis=1)
+            s += s_d * s_d
+            q += (v * v).sum(axis=1)
+        return z + 0.5 * (s - q)
+
     def labels(self, rng: np.random.Generator, x: np.ndarray) -> np.ndarray:
         w = 0.01 * _gauss_hash(x, 1)
         z = np.full(x.shape[0], math.log(0.25 / 0.75))

@@ -236,10 +236,15 @@ class FusedCTRTrainer:
             self._span("flush", t)
         self._dirty = False
 
-    def reset_optimizer(self) -> None:
+    def reset_optimizer(self, lr: float | None = None) -> None:
         """What ``torch.optim.Adam(...)`` re-created every epoch does
-        (all_main/pretrain_main.py:153): fresh moments, step 0."""
+        (all_main/pretrain_main.py:153): fresh moments, step 0 — with `lr`, at a new
+        learning rate (main/pretrain_main.py:180-181: ``learning_rate += 1e-4`` then a new
+        Adam): the per-step scalars are rewritten in place (captured graphs stay valid)."""
         self.flush()
+        if lr is not None:
+            self.lr = float(lr)
+            self.step_table.set_lr(self.lr)
         for t in (self.m_flat, self.v_flat, self.m_E, self.v_E, self.m_w, self.v_w):
             if t is not None:
                 t.zero_()

@@ -22,6 +22,9 @@ Fixtures:
   toy/           C1 toy data (13 dense bucketised + 26 sparse fields, 1000 rows)
   g_toy.json     pretrain_main.main on the toy (FM, FFM, and DeepFM / IPNN with dropout p=0):
                  per-epoch train loss / valid AUC / valid loss, final test AUC and preds
+  toy_days/ + g_toy_days.json  src/main/pretrain_main.py on the toy split into days 6..12
+                 (valid 11, test 12; lr += 1e-4 per epoch): FM, DeepFM
+  g_toy_2.json   src/all_main/pretrain_main_2.py (preloaded-tensor slicing) on the toy
   manifest.json  versions and seeds
 """
 from __future__ import annotations
@@ -401,6 +404,102 @@ def gen_toy(P, PM, models=("FM", "DeepFM"), merge=False):
     (HERE / "g_toy.json").write_text(json.dumps(result, indent=1))
 
 
+def gen_toy_days(P):
+    """toy_days/: the C1 toy rows as ONE train.txt + day_index.csv (days 6..12, ~143 rows
+    each; valid day 11, test day 12) for src/main/pretrain_main.py (lr += 1e-4 per epoch);
+    g_toy_days.json: its per-epoch log, test AUC and both days' submissions (FM, DeepFM
+    with dropout p=0)."""
+    import src.main.pretrain_main as PMD  # noqa: E402
+    toy, days = HERE / "toy", HERE / "toy_days"
+    days.mkdir(exist_ok=True)
+    rows = (toy / "train_.txt").read_text() + (toy / "test_.txt").read_text()
+    (days / "train.txt").write_text(rows)
+    n = len(rows.splitlines())
+    bounds = np.linspace(0, n, 8).astype(int)
+    with open(days / "day_index.csv", "w") as f:
+        for i, d in enumerate(range(6, 13)):
+            f.write(f"{d},{bounds[i]},{bounds[i + 1] - 1}\n")
+    result = {"valid_day": 11, "test_day": 12, "K": 10, "batch_size": 128, "epoch": 5,
+              "lr0": 1e-3, "wd": 1e-5}
+    for model_name in ("FM", "DeepFM"):
+        with tempfile.TemporaryDirectory() as tmp:
+            data_root = Path(tmp) / "data"
+            (data_root / "toy_days").mkdir(parents=True)
+            for f in days.iterdir():
+                (data_root / "toy_days" / f.name).write_bytes(f.read_bytes())
+            save_dir = Path(tmp) / "params"
+            save_dir.mkdir()
+            orig = PMD.get_model
+
+            def get_model(*a, **k):  # dropout off: RNG-free
+                m = orig(*a, **k)
+                for mod in m.modules():
+                    if isinstance(mod, torch.nn.Dropout):
+                        mod.p = 0.0
+                return m
+
+            PMD.get_model = get_model
+            PMD.setup_seed(1)
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(io.StringIO()):
+                PMD.main(str(data_root) + "/", "toy_days/", "", 11, 12, 10, model_name, 5, 1e-3,
+                         1e-5, "loss", 128, "cpu", str(save_dir) + "/")
+            PMD.get_model = orig
+            epochs = [dict(epoch=int(m.group(1)), train_loss=float(m.group(2)),
+                           valid_auc=float(m.group(3)), valid_loss=float(m.group(4)))
+                      for m in _EPOCH_RE.finditer(buf.getvalue())]
+            test_auc = float(re.search(r"test auc: (\S+)", buf.getvalue()).group(1))
+            sub = data_root / "toy_days" / model_name
+            preds = {day: [float(line.split(",")[1]) for line in
+                           (sub / f"{day}_test_submission.csv").read_text().splitlines()]
+                     for day in (11, 12)}
+            day_aucs = [[float(x) for x in line.split(",")[1:]]
+                        for line in (sub / "day_aucs.csv").read_text().splitlines()]
+            result[model_name] = dict(epochs=epochs, test_auc=test_auc, valid_preds=preds[11],
+                                      test_preds=preds[12], day_aucs=day_aucs)
+    (HERE / "g_toy_days.json").write_text(json.dumps(result, indent=1))
+
+
+def gen_toy_2(P):
+    """g_toy_2.json: src/all_main/pretrain_main_2.py (batches sliced from one preloaded
+    LongTensor) on the C1 toy (FM, DeepFM with dropout p=0), 5 epochs."""
+    import src.all_main.pretrain_main_2 as PM2  # noqa: E402
+    toy = HERE / "toy"
+    result = {"K": 10, "batch_size": 256, "epoch": 5, "lr": 1e-3, "wd": 1e-5}
+    for model_name in ("FM", "DeepFM"):
+        with tempfile.TemporaryDirectory() as tmp:
+            data_root = Path(tmp) / "data"
+            (data_root / "toy").mkdir(parents=True)
+            for f in toy.iterdir():
+                (data_root / "toy" / f.name).write_bytes(f.read_bytes())
+            save_dir = Path(tmp) / "params"
+            save_dir.mkdir()
+            orig = PM2.get_model
+
+            def get_model(*a, **k):
+                m = orig(*a, **k)
+                for mod in m.modules():
+                    if isinstance(mod, torch.nn.Dropout):
+                        mod.p = 0.0
+                return m
+
+            PM2.get_model = get_model
+            PM2.setup_seed(1)
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(io.StringIO()):
+                PM2.main(str(data_root) + "/", "toy/", "", 10, model_name, 5, 1e-3, 1e-5, "loss",
+                         256, "cpu", str(save_dir) + "/")
+            PM2.get_model = orig
+            epochs = [dict(epoch=int(m.group(1)), train_loss=float(m.group(2)),
+                           valid_auc=float(m.group(3)), valid_loss=float(m.group(4)))
+                      for m in _EPOCH_RE.finditer(buf.getvalue())]
+            test_auc = float(re.search(r"test auc: (\S+)", buf.getvalue()).group(1))
+            sub = data_root / "toy" / model_name / "test_submission.csv"
+            preds = [float(line.split(",")[1]) for line in sub.read_text().splitlines()]
+            result[model_name] = dict(epochs=epochs, test_auc=test_auc, test_preds=preds)
+    (HERE / "g_toy_2.json").write_text(json.dumps(result, indent=1))
+
+
 def main():
     P, FE, PG, PM = _import_reference()
     torch.set_num_threads(4)
@@ -408,7 +507,8 @@ def main():
             "ensemble": gen_ensemble, "ffm": lambda: gen_ffm(P),
             "toy_extra": lambda: gen_toy(P, PM, ("IPNN", "FFM"), merge=True),
             "bce": gen_bce, "fe": lambda: gen_fe(FE), "pg": lambda: gen_pg(PG),
-            "toy": lambda: gen_toy(P, PM)}
+            "toy": lambda: gen_toy(P, PM), "toy_days": lambda: gen_toy_days(P),
+            "toy_2": lambda: gen_toy_2(P)}
     for name in (sys.argv[1:] or [n for n in gens if n != "toy_extra"] + ["toy_extra"]):
         gens[name]()
     (HERE / "manifest.json").write_text(json.dumps({

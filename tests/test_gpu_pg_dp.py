@@ -21,7 +21,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import assert_adam_close
+from conftest import AdamBound, grad_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -47,11 +47,13 @@ def _agent(train: bool):
     return pg
 
 
-def _learn(pg, episodes, lo, hi):
+def _learn(pg, episodes, lo, hi, grads=None):
     losses = []
     for x, a, r in episodes:
         pg.store_transition(x[lo:hi].cuda(), a[lo:hi].cuda(), r[lo:hi].cuda())
         losses.append(float(pg.learn().item()))
+        if grads is not None:  # the episode's (all-reduced) MLP gradient
+            grads.append([g.detach().cpu().numpy().copy() for g in pg._gviews])
     return losses
 
 
@@ -70,9 +72,11 @@ def _rank_main(rank, world, port, train, cuts, q):
     try:
         torch.cuda.set_device(0)
         pg = _agent(train)
-        losses = _learn(pg, _episodes(), cuts[rank], cuts[rank + 1])
+        p0 = {k: v.detach().cpu().numpy().copy() for k, v in pg.policy_net.mlp.state_dict().items()}
+        grads = []
+        losses = _learn(pg, _episodes(), cuts[rank], cuts[rank + 1], grads)
         params = {k: v.detach().cpu().numpy() for k, v in pg.policy_net.mlp.state_dict().items()}
-        q.put((rank, losses, params))
+        q.put((rank, losses, params, p0, grads, pg.lr, pg.weight_decay))
     finally:
         dist.destroy_process_group()
 
@@ -99,13 +103,19 @@ def _run(world, train, cuts):
 def test_pg_dp_world2_matches_whole_episode(cuda, train, cuts):
     # the single-process reference also runs in a fresh process: the dropout seed is
     # drawn from a per-process counter (p_model._dropout_seed), as in the ranks
-    ref_losses, ref = _run(1, train, (0, N_EP))[0]
+    ref_losses, ref, p0, ref_grads, lr, wd = _run(1, train, (0, N_EP))[0]
     res = _run(2, train, cuts)
     nlp = N_EP * np.log(A)
+    # per-element Adam interval from the one-process run's per-episode gradients and the
+    # gradient bar (1e-5*|g| + 1e-6*max|g|) assumed for the ranks' all-reduced gradients
+    bd = {k: AdamBound(v, lr, wd) for k, v in p0.items()}
+    for step in ref_grads:
+        for k, g in zip(p0, step):
+            bd[k].step(g, grad_bound(g))
     for rank in range(2):
-        losses, params = res[rank]
+        losses, params = res[rank][:2]
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5, atol=4 * 2.0**-24 * nlp)
         for k, v in params.items():
-            assert_adam_close(v, ref[k], 1e-4, err_msg=f"{k} rank {rank}")
+            bd[k].check(v, ref[k], err_msg=f"{k} rank {rank}")
     for k in res[0][1]:  # replicas stay bit-identical
         assert np.array_equal(res[0][1][k], res[1][1][k]), k

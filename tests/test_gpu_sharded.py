@@ -6,7 +6,11 @@
   training their halves of a global batch must match one process training the whole
   batch, within the fp32 bar — the per-row gradient is summed per rank and then across
   ranks (another association order than one process's chunked sum), the dense MLP
-  gradient likewise through the all-reduce.
+  gradient likewise through the all-reduce. The parameters are checked element by element
+  against conftest.AdamBound, built from the one-process run's per-step gradients and the
+  gradient bar (assert_grad_close's, with the oracle's condition numbers), which is
+  assumed for the ranks' gradients here and checked directly against the oracle in
+  test_gpu_models.
 """
 from __future__ import annotations
 
@@ -18,7 +22,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import assert_adam_close
+from conftest import AdamBound, fused_grads, grad_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -130,21 +134,36 @@ def test_sharded_world2_matches_global_batch(cuda, kind, drop, V, F, K, B):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # one process, the whole global batch
+    # one process, the whole global batch; its per-step gradients and their bar build the
+    # per-element Adam interval the ranks' parameters must fall in
+    from oracle import ctr_oracle as O
     m = _model(kind, V, F, K, drop=drop)
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3)
-    ref_losses = [tr.step(torch.tensor(x, device=cuda), torch.tensor(y, device=cuda)).item()
-                  for x, y in CriteoSynth(V, F, seed=21).batches(steps, B * world)]
+    sd = m.state_dict()
+    bd = {k: AdamBound(v.cpu().numpy(), 1e-3, 1e-5) for k, v in sd.items()}
+    ref_losses = []
+    for x, y in CriteoSynth(V, F, seed=21).batches(steps, B * world):
+        cpu = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        cond = O.grad_condition(kind, cpu, torch.tensor(x), torch.tensor(y))
+        ref_losses.append(tr.step(torch.tensor(x, device=cuda),
+                                  torch.tensor(y, device=cuda)).item())
+        gE, gw, dense = fused_grads(tr)
+        n = np.bincount(np.asarray(x).reshape(-1), minlength=V)
+        grads = dict(dense, **{"feature_embedding.weight": gE, "linear.weight": gw})
+        for k, g in grads.items():
+            c = cond.get(k)
+            bd[k].step(g, grad_bound(g, cond=None if c is None else c.numpy(),
+                                     n_terms=None if c is None else n))
+    tr.flush()
     sd = m.state_dict()
     for rank in range(world):
         losses, E, w, dense = res[rank]
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
-        assert_adam_close(E, sd["feature_embedding.weight"].cpu().numpy(), 1e-3,
-                          err_msg=f"E rank {rank}")
-        assert_adam_close(w, sd["linear.weight"].cpu().numpy(), 1e-3,
-                          err_msg=f"w rank {rank}")
+        bd["feature_embedding.weight"].check(E, sd["feature_embedding.weight"].cpu().numpy(),
+                                             err_msg=f"E rank {rank}")
+        bd["linear.weight"].check(w, sd["linear.weight"].cpu().numpy(), err_msg=f"w rank {rank}")
         for k, v in dense.items():
-            assert_adam_close(v, sd[k].cpu().numpy(), 1e-3, err_msg=f"{k} rank {rank}")
+            bd[k].check(v, sd[k].cpu().numpy(), err_msg=f"{k} rank {rank}")
     # the replicated dense parameters are bitwise identical across ranks
     for k in res[0][3]:
         assert np.array_equal(res[0][3][k], res[1][3][k]), k

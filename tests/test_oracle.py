@@ -229,3 +229,51 @@ def test_ffm_matches_reference(golden):
         for k in keys:
             np.testing.assert_allclose(params[k].detach().numpy(), g[f"step{s + 1}/{k}"],
                                        rtol=1e-6, atol=1e-8, err_msg=k)
+
+
+def test_day_split_matches_reference_layout(golden):
+    """main/pretrain_main.get_dataset (:47-88): training days in day_index order minus the
+    valid / test days, feature_nums = largest id + 1."""
+    from rl_ctr_prediction_amd.main.pretrain_main import get_dataset
+    from conftest import GOLDEN
+    ref = golden("g_toy_days.json")
+    full, days, tr, va, te, F, V = get_dataset(str(GOLDEN) + "/", "toy_days/", "",
+                                               ref["valid_day"], ref["test_day"])
+    assert F == full.shape[1] - 1 and V == int(full[:, 1:].max()) + 1
+    assert len(va) == len(ref["FM"]["valid_preds"]) and len(te) == len(ref["FM"]["test_preds"])
+    keep = [d for d in days if d[0] not in (ref["valid_day"], ref["test_day"])]
+    np.testing.assert_array_equal(tr, np.concatenate([full[a:b + 1] for _, a, b in keep]))
+    np.testing.assert_array_equal(te, full[days[-1, 1]:days[-1, 2] + 1])
+
+
+@pytest.mark.parametrize("kind", ["FM", "DeepFM"])
+def test_day_split_driver_matches_reference(golden, kind):
+    """src/main/pretrain_main.main on toy_days (lr += 1e-4 before every epoch): the oracle's
+    restatement against the reference's own run (g_toy_days.json)."""
+    from rl_ctr_prediction_amd.main.pretrain_main import get_dataset
+    from conftest import GOLDEN
+    ref = golden("g_toy_days.json")
+    _, _, tr, va, _, _, V = get_dataset(str(GOLDEN) + "/", "toy_days/", "", ref["valid_day"],
+                                        ref["test_day"])
+    hist, _ = O.pretrain_run(kind, tr, va, V, ref["K"], ref["epoch"], ref["lr0"], ref["wd"],
+                             ref["batch_size"], seed=1, drop_p=0.0, lr_step=1e-4)
+    for h, r in zip(hist, ref[kind]["epochs"], strict=True):
+        assert h["train_loss"] == pytest.approx(r["train_loss"], rel=1e-6)
+        assert h["valid_loss"] == pytest.approx(r["valid_loss"], rel=1e-6)
+        assert h["valid_auc"] == pytest.approx(r["valid_auc"], abs=1e-9)
+
+
+@pytest.mark.parametrize("kind", ["FM", "DeepFM"])
+def test_slicing_driver_matches_reference(golden, kind):
+    """src/all_main/pretrain_main_2.main (batches sliced from one LongTensor) on the toy:
+    the oracle against the reference's own run (g_toy_2.json)."""
+    ref = golden("g_toy_2.json")
+    train = np.loadtxt(_toy("train_.txt"), delimiter=",", dtype=np.int64)
+    test = np.loadtxt(_toy("test_.txt"), delimiter=",", dtype=np.int64)
+    V = golden("g_toy.json")["V"]
+    hist, _ = O.pretrain_run(kind, train, test, V, ref["K"], ref["epoch"], ref["lr"], ref["wd"],
+                             ref["batch_size"], seed=1, drop_p=0.0)
+    for h, r in zip(hist, ref[kind]["epochs"], strict=True):
+        assert h["train_loss"] == pytest.approx(r["train_loss"], rel=1e-6)
+        assert h["valid_loss"] == pytest.approx(r["valid_loss"], rel=1e-6)
+        assert h["valid_auc"] == pytest.approx(r["valid_auc"], abs=1e-9)
