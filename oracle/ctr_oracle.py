@@ -159,7 +159,7 @@ def train_step(kind: str, params: dict, opt, x: torch.Tensor, y: torch.Tensor,
     """One reference step: forward, BCE, zero_grad, backward (dense embedding grads),
     Adam.step, loss.item()  (all_main/pretrain_main.py:72-79)."""
     p = forward(kind, params, x, drop_p, True)
-    loss = bce(p, y.reshape(-1, 1).float())
+    loss = bce(p, y.reshape(-1, 1).to(p.dtype))
     for t in params.values():
         t.grad = None
     loss.backward()
@@ -169,7 +169,7 @@ def train_step(kind: str, params: dict, opt, x: torch.Tensor, y: torch.Tensor,
 
 def grads(kind: str, params: dict, x, y, drop_p=0.0) -> tuple[float, torch.Tensor, dict]:
     p = forward(kind, params, x, drop_p, True)
-    loss = bce(p, y.reshape(-1, 1).float())
+    loss = bce(p, y.reshape(-1, 1).to(p.dtype))
     for t in params.values():
         t.grad = None
     loss.backward()
@@ -382,23 +382,29 @@ def pg_learn(policy: torch.nn.Sequential, opt, E: torch.Tensor, states: torch.Te
 # --------------------------------------------------------------------- driver -------
 def pretrain_run(kind: str, train: np.ndarray, test: np.ndarray, V: int, K: int, epochs: int,
                  lr: float, wd: float, batch: int, seed: int = 1, drop_p: float = 0.0,
-                 lr_step: float = 0.0):
+                 lr_step: float = 0.0, dtype=torch.float32, extra_eval=()):
     """all_main/pretrain_main.main without files: Adam re-created every epoch, batches in
     file order, train loss = mean of batch losses, AUC over the test split.
-    lr_step: main/pretrain_main.py:180 adds 1e-4 to the learning rate before every epoch."""
+    lr_step: main/pretrain_main.py:180 adds 1e-4 to the learning rate before every epoch.
+    dtype=torch.float64 replays the same run (same fp32 initial values) in double precision:
+    the exact-arithmetic trajectory the fp32 reference's rounding is measured against.
+    The last epoch's dict carries the eval split's predictions ("preds") and those of every
+    extra_eval matrix ("extra_preds"; the driver's test_submission of a run without early stop)."""
     from sklearn.metrics import roc_auc_score
     F = train.shape[1] - 1
     params = init_params(kind, V, F, K, seed=seed)
+    if dtype != torch.float32:
+        params = {k: v.detach().to(dtype).requires_grad_(True) for k, v in params.items()}
     hist = []
     xt = torch.from_numpy(test[:, 1:]).long()
-    yt = torch.from_numpy(test[:, 0]).float()
+    yt = torch.from_numpy(test[:, 0]).to(dtype)
     for _ in range(epochs):
         lr += lr_step
         opt = make_optimizer(params, lr, wd)
         losses = []
         for s in range(0, len(train), batch):
             xb = torch.from_numpy(train[s:s + batch, 1:]).long()
-            yb = torch.from_numpy(train[s:s + batch, 0]).float()
+            yb = torch.from_numpy(train[s:s + batch, 0]).to(dtype)
             losses.append(train_step(kind, params, opt, xb, yb, drop_p))
         with torch.no_grad():
             preds, vl = [], []
@@ -410,4 +416,10 @@ def pretrain_run(kind: str, train: np.ndarray, test: np.ndarray, V: int, K: int,
         hist.append(dict(train_loss=sum(losses) / len(losses),
                          valid_auc=float(roc_auc_score(test[:, 0], pr)),
                          valid_loss=sum(vl) / len(vl)))
+    with torch.no_grad():
+        hist[-1]["preds"] = pr
+        hist[-1]["extra_preds"] = [
+            torch.cat([forward(kind, params, torch.from_numpy(m[s:s + batch, 1:]).long(), drop_p,
+                               False).reshape(-1) for s in range(0, len(m), batch)]).numpy()
+            for m in extra_eval]
     return hist, params

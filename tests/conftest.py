@@ -178,3 +178,39 @@ def fused_grads(tr):
         gw = gw.cpu().numpy()
     dense = {n: v.detach().cpu().numpy() for n, v in tr.grad_views.items()}
     return gE.cpu().numpy(), gw, dense
+
+
+def pred_deviation(actual, desired) -> float:
+    """Largest deviation of predicted probabilities in logit space, relative to the logit:
+    max |logit(a) - logit(d)| / (|logit(d)| + 1) over the predictions strictly inside (0, 1)
+    in both; predictions at exactly 0 or 1 (fp32 sigmoid saturation) must match within 1e-6
+    absolute, and otherwise count as an infinite deviation. A sigmoid output's relative error
+    is (1 - p) times its logit's absolute error, so comparing p relatively punishes
+    saturated predictions (p ~ 1e-30 with logits ~ -70) for last-bit logit differences."""
+    a = np.asarray(actual, dtype=np.float64).reshape(-1)
+    d = np.asarray(desired, dtype=np.float64).reshape(-1)
+    inside = (a > 0) & (a < 1) & (d > 0) & (d < 1)
+    if (np.abs(a - d)[~inside] > 1e-6).any():
+        return float("inf")
+    if not inside.any():
+        return 0.0
+    za = np.log(a[inside]) - np.log1p(-a[inside])
+    zd = np.log(d[inside]) - np.log1p(-d[inside])
+    return float(np.max(np.abs(za - zd) / (np.abs(zd) + 1.0)))
+
+
+def assert_preds_within_spread(actual, desired, spread_key, *, factor=2.0, err_msg=""):
+    """Multi-epoch driver predictions vs the reference's run. The bar is the larger of the
+    1e-5 north-star tolerance and `factor` x the spread of the reference's own fp32 arithmetic
+    (toy_spread.json, make_toy_spread.py: the oracle at 1/2/3/4/8 CPU threads, with the
+    transposed GEMM, and with the FM sums in reverse order — equally valid evaluation orders
+    of the reference's formulas — deviates from the recorded run by up to 1.7e-5 (FM) and
+    1.3e-4 (DeepFM, day split) after five epochs of training, which amplify last-bit
+    differences), both in pred_deviation's logit space."""
+    kind, run = spread_key
+    spread = load_golden("toy_spread.json")[kind][run]["max"]
+    bar = max(1e-5, factor * spread)
+    dev = pred_deviation(actual, desired)
+    assert dev <= bar, (f"{err_msg}: prediction deviation {dev:.3g} > bar {bar:.3g} "
+                        f"(reference spread {spread:.3g})")
+    return dev

@@ -13,7 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import AdamBound, assert_grad_close, fused_grads as _fused_grads
+from conftest import (AdamBound, assert_grad_close, assert_preds_within_spread,
+                      fused_grads as _fused_grads)
 from oracle import ctr_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -207,9 +208,13 @@ def test_toy_driver_vs_reference(cuda, golden, tmp_path):
             assert h["valid_loss"] == pytest.approx(r["valid_loss"], rel=rel), (kind, h, r)
             assert h["valid_auc"] == pytest.approx(r["valid_auc"], abs=1e-3 if exact else 5e-3), \
                 (kind, h, r)
-        np.testing.assert_allclose(np.asarray(res["test_preds"]).reshape(-1),
-                                   np.asarray(ref[kind]["test_preds"]),
-                                   rtol=1e-5 if exact else 5e-2, atol=1e-6 if exact else 1e-4)
+        if exact:
+            dev = assert_preds_within_spread(res["test_preds"], ref[kind]["test_preds"],
+                                             (kind, "toy"), err_msg=kind)
+            print(f"[parity] toy {kind} test preds: logit deviation {dev:.3g}")
+        else:
+            np.testing.assert_allclose(np.asarray(res["test_preds"]).reshape(-1),
+                                       np.asarray(ref[kind]["test_preds"]), rtol=5e-2, atol=1e-4)
         assert (d / "params" / f"{kind}best.pth").exists()
         assert (d / "data" / "toy" / kind / "test_submission.csv").exists()
 
@@ -260,10 +265,10 @@ def test_day_split_driver_vs_reference(cuda, golden, tmp_path, kind):
     assert [h["lr"] for h in res["history"]] == pytest.approx(
         [ref["lr0"] + 1e-4 * (i + 1) for i in range(ref["epoch"])], rel=1e-12)
     _check_epochs(res["history"], r["epochs"])
-    np.testing.assert_allclose(np.asarray(res["valid_preds"]).reshape(-1), r["valid_preds"],
-                               rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(np.asarray(res["test_preds"]).reshape(-1), r["test_preds"],
-                               rtol=1e-5, atol=1e-6)
+    for split in ("valid", "test"):
+        dev = assert_preds_within_spread(res[f"{split}_preds"], r[f"{split}_preds"],
+                                         (kind, f"days_{split}"), err_msg=f"{kind} {split}")
+        print(f"[parity] day split {kind} {split} preds: logit deviation {dev:.3g}")
     assert res["test_auc"] == pytest.approx(r["test_auc"], abs=1e-3)
     sub = tmp_path / "data" / "toy_days" / kind
     day_aucs = [[float(v) for v in line.split(",")[1:]]
@@ -297,8 +302,9 @@ def test_slicing_driver_vs_reference(cuda, golden, tmp_path, kind):
     finally:
         PM.get_model = orig
     _check_epochs(res["history"], ref[kind]["epochs"])
-    np.testing.assert_allclose(np.asarray(res["test_preds"]).reshape(-1),
-                               ref[kind]["test_preds"], rtol=1e-5, atol=1e-6)
+    dev = assert_preds_within_spread(res["test_preds"], ref[kind]["test_preds"], (kind, "toy_2"),
+                                     err_msg=kind)
+    print(f"[parity] slicing {kind} test preds: logit deviation {dev:.3g}")
 
 
 def test_feature_embedding_module_and_load_embedding(cuda, golden):
