@@ -302,6 +302,22 @@ int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n, doub
                    double bc2_sqrt, const float* step_table, const int32_t* step_ptr,
                    double beta1, double beta2, double eps, double weight_decay,
                    ctr_stream_t stream);
+/* ctr_adam_dense_planes: ctr_adam_dense that also rewrites the bf16 planes (ctr_planes) of
+ *   up to two row-major [rows, cols] sub-matrices of p (the MLP weights: p[offset + r*cols
+ *   + c]) with the updated values, so the next step's plane GEMMs need no ctr_split_planes.
+ *   offset % 4 == 0, cols % 4 == 0, n % 4 == 0, 16-B aligned vectors.
+ *   Replaces: the same optimizer.step; the planes are this framework's GEMM operand format. */
+typedef struct ctr_plane_view {
+  int64_t offset;
+  int64_t rows;
+  int64_t cols;
+  ctr_planes planes;
+} ctr_plane_view;
+int ctr_adam_dense_planes(float* p, const float* g, float* m, float* v, int64_t n,
+                          double step_size, double bc2_sqrt, const float* step_table,
+                          const int32_t* step_ptr, double beta1, double beta2, double eps,
+                          double weight_decay, const ctr_plane_view* views, int n_views,
+                          ctr_stream_t stream);
 int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                        float* v_lin, int64_t V, int K, int32_t* rowmap,
                        const float* grad_rows, const float* grad_lin, double step_size,
@@ -345,9 +361,10 @@ int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float*
                                   double beta2, double eps, double weight_decay,
                                   ctr_stream_t stream);
 /* Device step counters (int32[2]): ctr[0] = completed steps, ctr[1] = the step in flight.
- * ctr_step_begin: ctr[1] = ctr[0] + 1;  ctr_step_end: ctr[0] = ctr[1]. Between the two,
- * both values are constant, so kernels on several streams can read them: the catch-up,
- * the sweep and the dropout stream read ctr[0], the Adam apply reads ctr[1].
+ * ctr_step_begin: ctr[1] = ctr[0] + 1;  ctr_step_end: ctr[0] = ctr[1], ctr[1] += 1. A
+ * counter initialised to {0, 1} therefore needs no ctr_step_begin (one launch less per
+ * step); within a step both values are constant, so kernels on several streams can read
+ * them: the catch-up, the sweep and the dropout stream read ctr[0], the Adam apply ctr[1].
  * ctr_adam_deferred_sweep: bring rows [s*ceil(V/n), (s+1)*ceil(V/n)), s = ctr[0] % n_slices,
  *   up to step ctr[0] — a background share of the flush, run concurrently with a step
  *   after its catch-up (it skips the batch's rows, which are current to ctr[0]) and

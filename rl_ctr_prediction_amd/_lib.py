@@ -46,6 +46,11 @@ class PlanesDesc(C.Structure):
 
 _planes_p = C.POINTER(PlanesDesc)
 
+
+class PlaneViewDesc(C.Structure):
+    """Mirror of ``ctr_plane_view`` (include/ctr_hip.h)."""
+    _fields_ = [("offset", _i64), ("rows", _i64), ("cols", _i64), ("planes", PlanesDesc)]
+
 # name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
 # against the header.
 SIGNATURES = {
@@ -94,6 +99,8 @@ SIGNATURES = {
     "ctr_rows_to_dense": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp]),
     "ctr_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp, _vp, _f64, _f64, _f64,
                               _f64, _vp]),
+    "ctr_adam_dense_planes": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp, _vp, _f64, _f64,
+                                     _f64, _f64, _vp, _i32, _vp]),
     "ctr_adam_embedding": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _f64,
                                   _f64, _vp, _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_rows": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _plan_p, _vp,

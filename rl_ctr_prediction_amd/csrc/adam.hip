@@ -62,16 +62,69 @@ __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4&
   adam_elem(p.w, g.w, m.w, v.w, h);
 }
 
+// The replay step of an absent row (g = 0 before weight decay) on four elements, in
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 operations per
+// lane per instruction, each bitwise the scalar one; sqrt and rcp stay scalar). The
+// flush is VALU-bound at long replays (SQ_ACTIVE_INST_VALU ~95 % of the SIMD quad-cycles
+// at 20 replayed steps, profiles/r02_flush_pmc.txt). Measured on MI355X (tools/ab_flush.sh,
+// C3 table): 4.32 vs 4.42 ms at 20 steps, but 3.06 vs 2.64 ms at 1 step and 21.6 vs 21.5 ms
+// at the C5 shape (10 steps) — packed fp32 issues at about the scalar rate on gfx950, so the
+// scalar form stays the default (CTR_FLUSH_PK=1 selects this one).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+#ifndef CTR_FLUSH_PK
+#define CTR_FLUSH_PK 0
+#endif
+
+__device__ __forceinline__ void adam_replay_pk2(pf2& p, pf2& m, pf2& v, const AdamHP& h) {
+#pragma clang fp contract(off)
+  const pf2 zero = {0.f, 0.f};
+  const pf2 g = __builtin_elementwise_fma((pf2){h.wd, h.wd}, p, zero);        // grad.add(p, wd)
+  m = __builtin_elementwise_fma((pf2){h.w1, h.w1}, g - m, m);                 // lerp_
+  v = __builtin_elementwise_fma((pf2){h.w2, h.w2} * g, g, v * (pf2){h.beta2, h.beta2});
+  const pf2 sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  const pf2 den = __builtin_elementwise_fma(sq, (pf2){h.inv_bc2_sqrt, h.inv_bc2_sqrt},
+                                            (pf2){h.eps, h.eps});
+  const pf2 r = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  p = __builtin_elementwise_fma((pf2){h.neg_step_size, h.neg_step_size} * m, r, p);
+}
+
+__device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v, const AdamHP& h) {
+#if CTR_FLUSH_PK
+  pf2 p0 = {p.x, p.y}, p1 = {p.z, p.w}, m0 = {m.x, m.y}, m1 = {m.z, m.w};
+  pf2 v0 = {v.x, v.y}, v1 = {v.z, v.w};
+  adam_replay_pk2(p0, m0, v0, h);
+  adam_replay_pk2(p1, m1, v1, h);
+  p = make_float4(p0.x, p0.y, p1.x, p1.y);
+  m = make_float4(m0.x, m0.y, m1.x, m1.y);
+  v = make_float4(v0.x, v0.y, v1.x, v1.y);
+#else
+  adam_vec(p, make_float4(0.f, 0.f, 0.f, 0.f), m, v, h);
+#endif
+}
+
 // ------------------------------------------------------------------ dense -----------
 // step_ptr != NULL: the step's scalars come from the device step table (HIP-graph replay)
 __device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s);
+
+// Up to two row-major [rows, cols] sub-matrices of the flat parameter vector (the MLP
+// weights the GEMMs read as bf16 planes) whose planes are rewritten with the updated values,
+// so the next step's GEMMs need no split pass. off and cols are multiples of 4: a float4
+// never straddles two rows.
+constexpr int kMaxPlaneViews = 2;
+struct PlaneViews {
+  int n;
+  int64_t off[kMaxPlaneViews], len[kMaxPlaneViews], cols[kMaxPlaneViews];
+  int64_t ld[kMaxPlaneViews], ps[kMaxPlaneViews];
+  uint16_t* d[kMaxPlaneViews];
+};
 
 __global__ __launch_bounds__(256) void adam_dense_vec(float4* __restrict__ p,
                                                       const float4* __restrict__ g,
                                                       float4* __restrict__ m,
                                                       float4* __restrict__ v, int64_t n4,
                                                       AdamHP h, const float* __restrict__ tab,
-                                                      const int32_t* __restrict__ step_ptr) {
+                                                      const int32_t* __restrict__ step_ptr,
+                                                      PlaneViews pv) {
   if (step_ptr) load_step(h, tab, *step_ptr);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -80,6 +133,14 @@ __global__ __launch_bounds__(256) void adam_dense_vec(float4* __restrict__ p,
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
+#pragma unroll
+    for (int j = 0; j < kMaxPlaneViews; ++j) {
+      const int64_t e = 4 * i - pv.off[j];
+      if (j < pv.n && e >= 0 && e < pv.len[j]) {
+        const int64_t r = e / pv.cols[j], c = e - r * pv.cols[j];
+        store_planes4_at(pv.d[j] + r * pv.ld[j] + c, pv.ps[j], pp);
+      }
+    }
   }
 }
 
@@ -294,7 +355,11 @@ __global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
 // Within a step, ctr[0] stays at t-1 (catch-up, sweep and dropout read it) and ctr[1] = t
 // (the Adam apply reads it), so work on several streams never sees the counter move.
 __global__ void step_begin_kernel(int32_t* ctr) { ctr[1] = ctr[0] + 1; }
-__global__ void step_end_kernel(int32_t* ctr) { ctr[0] = ctr[1]; }
+__global__ void step_end_kernel(int32_t* ctr) {
+  const int32_t t = ctr[1];
+  ctr[0] = t;
+  ctr[1] = t + 1;  // the next step's: ctr_step_begin is then a no-op
+}
 
 // Background sweep (deferred Adam): bring one slice of the rows — slice ctr[0] % n_slices —
 // up to the completed step ctr[0], while a training step runs on other streams. Rows of the
@@ -437,7 +502,7 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
         set_step(s);
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-          if (s > from[u]) adam_vec(pp[u], z4, mm[u], vv[u], h);
+          if (s > from[u]) adam_replay_vec(pp[u], mm[u], vv[u], h);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u)
@@ -514,10 +579,10 @@ static AdamHP make_hp(double step_size, double bc2_sqrt, double beta1, double be
 
 using namespace ctr;
 
-extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n,
-                              double step_size, double bc2_sqrt, const float* step_table,
-                              const int32_t* step_ptr, double beta1, double beta2, double eps,
-                              double weight_decay, ctr_stream_t stream) {
+static int adam_dense_impl(float* p, const float* g, float* m, float* v, int64_t n,
+                           double step_size, double bc2_sqrt, const float* step_table,
+                           const int32_t* step_ptr, double beta1, double beta2, double eps,
+                           double weight_decay, const PlaneViews& pv, ctr_stream_t stream) {
   CTR_REQUIRE(n >= 0, "ctr_adam_dense: n < 0");
   if (n == 0) return CTR_OK;
   CTR_REQUIRE(p && g && m && v, "ctr_adam_dense: null pointer");
@@ -527,13 +592,15 @@ extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int6
                            eps, weight_decay);
   hipStream_t st = as_stream(stream);
   const bool al = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
+  CTR_REQUIRE(pv.n == 0 || (al && n % 4 == 0),
+              "ctr_adam_dense_planes: needs 16-B aligned vectors and n %% 4 == 0");
   int64_t done = 0;
   if (al && n >= 4) {
     const int64_t n4 = n / 4;
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 4096);
     hipLaunchKernelGGL(adam_dense_vec, grid, 256, 0, st, reinterpret_cast<float4*>(p),
                        reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m),
-                       reinterpret_cast<float4*>(v), n4, h, step_table, step_ptr);
+                       reinterpret_cast<float4*>(v), n4, h, step_table, step_ptr, pv);
     CTR_LAUNCH_CHECK("adam_dense_vec");
     done = n4 * 4;
   }
@@ -544,6 +611,44 @@ extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int6
     CTR_LAUNCH_CHECK("adam_dense_scalar");
   }
   return CTR_OK;
+}
+
+extern "C" int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n,
+                              double step_size, double bc2_sqrt, const float* step_table,
+                              const int32_t* step_ptr, double beta1, double beta2, double eps,
+                              double weight_decay, ctr_stream_t stream) {
+  PlaneViews pv{};
+  return adam_dense_impl(p, g, m, v, n, step_size, bc2_sqrt, step_table, step_ptr, beta1, beta2,
+                         eps, weight_decay, pv, stream);
+}
+
+extern "C" int ctr_adam_dense_planes(float* p, const float* g, float* m, float* v, int64_t n,
+                                     double step_size, double bc2_sqrt, const float* step_table,
+                                     const int32_t* step_ptr, double beta1, double beta2,
+                                     double eps, double weight_decay, const ctr_plane_view* views,
+                                     int n_views, ctr_stream_t stream) {
+  CTR_REQUIRE(n_views >= 0 && n_views <= kMaxPlaneViews && (n_views == 0 || views),
+              "ctr_adam_dense_planes: 0..%d plane views", kMaxPlaneViews);
+  PlaneViews pv{};
+  pv.n = n_views;
+  for (int j = 0; j < n_views; ++j) {
+    const ctr_plane_view& w = views[j];
+    const ctr_planes& q = w.planes;
+    CTR_REQUIRE(w.offset >= 0 && w.offset % 4 == 0 && w.rows > 0 && w.cols > 0 &&
+                    w.cols % 4 == 0 && w.offset + w.rows * w.cols <= n,
+                "ctr_adam_dense_planes: view %d outside the vector or not float4-aligned", j);
+    CTR_REQUIRE(q.data && (uintptr_t)q.data % 16 == 0 && q.ld % 4 == 0 && q.ld >= w.cols &&
+                    q.rows >= w.rows && q.plane_stride >= q.rows * q.ld,
+                "ctr_adam_dense_planes: view %d: bad plane layout", j);
+    pv.off[j] = w.offset;
+    pv.len[j] = w.rows * w.cols;
+    pv.cols[j] = w.cols;
+    pv.ld[j] = q.ld;
+    pv.ps[j] = q.plane_stride;
+    pv.d[j] = static_cast<uint16_t*>(q.data);
+  }
+  return adam_dense_impl(p, g, m, v, n, step_size, bc2_sqrt, step_table, step_ptr, beta1, beta2,
+                         eps, weight_decay, pv, stream);
 }
 
 extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,

@@ -6,12 +6,14 @@ an error, never a silent fallback.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import torch
 
 from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
-                   EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, SparsePlan, lib)
+                   EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, PlaneViewDesc, SparsePlan,
+                   lib)
 
 __all__ = [
     "embedding_gather", "fm_forward", "fm_forward_planes", "bce_sigmoid", "deepfm_head", "gemm", "linear",
@@ -499,15 +501,22 @@ def adam_scalars(step: int, lr: float, betas=(0.9, 0.999)) -> tuple[float, float
 
 
 def adam_dense(p, g, m, v, step: int, lr: float, betas=(0.9, 0.999), eps=1e-8,
-               weight_decay=0.0, step_dev=None, table=None) -> None:
-    """One Adam step; with step_dev/table the step index is read on the device (graphs)."""
+               weight_decay=0.0, step_dev=None, table=None, planes=None) -> None:
+    """One Adam step; with step_dev/table the step index is read on the device (graphs).
+    planes: [(offset, Planes)] — sub-matrices p[offset : offset + rows*cols] (row-major,
+    the Planes' shape) whose planes are rewritten with the updated values (ctr_adam_dense_planes)."""
     for t, n in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
         _f32(t, n)
     ss, bc2s = adam_scalars(max(step, 1), lr, betas)
     tab = table.ensure(step) if table is not None else None
-    lib.ctr_adam_dense(_p(p), _p(g), _p(m), _p(v), p.numel(), ss, bc2s, _p(tab), _p(step_dev),
-                       float(betas[0]), float(betas[1]), float(eps), float(weight_decay),
-                       _stream())
+    args = (_p(p), _p(g), _p(m), _p(v), p.numel(), ss, bc2s, _p(tab), _p(step_dev),
+            float(betas[0]), float(betas[1]), float(eps), float(weight_decay))
+    if not planes:
+        lib.ctr_adam_dense(*args, _stream())
+        return
+    views = (PlaneViewDesc * len(planes))(
+        *[PlaneViewDesc(int(off), pl.rows, pl.cols, pl.desc) for off, pl in planes])
+    lib.ctr_adam_dense_planes(*args, ctypes.cast(views, ctypes.c_void_p), len(planes), _stream())
 
 
 def adam_embedding(emb, m_emb, v_emb, lin, m_lin, v_lin, rowmap, grad_rows, grad_lin, step: int,

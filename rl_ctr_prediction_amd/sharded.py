@@ -84,7 +84,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         y = y.contiguous()
         bias, gv = self.views["bias"], self.grad_views
 
-        hip_ops.step_begin(self.step_ctr)
+        self._sync_weight_planes()
         # 1. plan of the local batch, per-owner counts of its unique rows
         t = self._mark("plan")
         b.plan.build(x, self.V, err_flag=self.err)
@@ -126,6 +126,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
                                   grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
         self._span("scatter", t)
+        if self.kind != "FM":  # the dense-parameter gradients, on the weight-gradient stream
+            self._weight_grads(b, gz)
         if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream (joined below)
             hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         # 5. gradients to the owners, summed per row in (source rank, position) order
@@ -150,9 +152,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                    grad_rows=b.g_rows, grad_lin=b.g_lin, step_dev=self.step_cur)
         self._span("adam", t)
         self._dirty = True
-        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, self.step_count,
-                           self.lr, self.betas, self.eps, self.weight_decay,
-                           step_dev=self.step_cur, table=self.step_table)
+        self._adam_dense(self.step_count)
         self._join_sweep()
         hip_ops.step_end(self.step_ctr)
         return b.loss

@@ -143,7 +143,8 @@ class FusedCTRTrainer:
         self.rowmap = torch.full((self.V_tab,), -1, dtype=torch.int32, device=self.device)
         self.last = torch.zeros(self.V_tab, dtype=torch.int32, device=self.device)
         # device step counters: [0] completed steps, [1] the step in flight (ctr_step_begin/end)
-        self.step_ctr = torch.zeros(2, dtype=torch.int32, device=self.device)
+        # initialised to {0, 1}: ctr_step_end advances both, so no step-begin launch is needed
+        self.step_ctr = torch.tensor([0, 1], dtype=torch.int32, device=self.device)
         self.step_done, self.step_cur = self.step_ctr[0:1], self.step_ctr[1:2]
         # optional background sweep: each step brings 1/sweep_slices of the rows up to date on
         # its own stream. Off by default: measured on MI355X (C3) it slows the concurrent
@@ -151,11 +152,19 @@ class FusedCTRTrainer:
         self.sweep_slices = 0
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
-        self._wgrad_stream = (torch.cuda.Stream(device=self.device) if self.kind in _MLP_KINDS
-                              else None)
-        # the MLP weights' planes, re-split from the fp32 parameters at the start of every step
-        # (the parameters stay the source of truth: state_dict / load_state_dict see fp32)
+        # the weight-gradient work shares the plan's side stream (it starts after the head,
+        # long after the plan is built): the captured graph then has exactly two parallel
+        # lists — the critical path and one side list — and the HIP graph executor cannot
+        # map two independent side lists onto one hardware queue in the wrong order (seen
+        # with three: the plan queued behind the weight gradients, +100 us per step)
+        self._wgrad_stream = None
+        if self.kind in _MLP_KINDS:
+            self._wgrad_stream = self._side if self._side is not None else torch.cuda.Stream(device=self.device)
+        # the MLP weights' planes: rewritten by the dense Adam with every update
+        # (ctr_adam_dense_planes), re-split from the fp32 parameters (the source of truth:
+        # state_dict / load_state_dict see fp32) whenever those changed outside the trainer
         self._wplanes = None
+        self._wver = None
         if self.kind in _MLP_KINDS:
             w0, w1 = self.views["mlp.0.weight"], self.views["mlp.3.weight"]
             self._wplanes = (hip_ops.Planes(*w0.shape, self.device),
@@ -249,7 +258,7 @@ class FusedCTRTrainer:
             if t is not None:
                 t.zero_()
         self.last.zero_()
-        self.step_ctr.zero_()
+        self.step_ctr.copy_(torch.tensor([0, 1], dtype=torch.int32))
         self.step_count = 0
 
     def optimizer_state_dict(self) -> dict:
@@ -328,6 +337,7 @@ class FusedCTRTrainer:
         B, F = x.shape
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
+        self._sync_weight_planes()
         if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
                 and y.dtype == torch.float32 and y.is_contiguous()):
             return self._graph_step(x, y, mean_div)
@@ -335,6 +345,25 @@ class FusedCTRTrainer:
         loss = self._launch(x, y, mean_div)
         self._after_step()
         return loss
+
+    def _weights_version(self):
+        mlp = self.model.mlp
+        return (mlp[0].weight._version, mlp[3].weight._version)
+
+    def _sync_weight_planes(self, force: bool = False) -> None:
+        """Re-split the MLP weights' planes if the fp32 weights changed outside the trainer
+        (load_state_dict, in-place ops on the Parameters: their version counters move).
+        Writes through ``.data`` bypass the counters: call sync_weights() after those."""
+        if self._wplanes is None:
+            return
+        ver = self._weights_version()
+        if force or ver != self._wver:
+            self._split_weights()
+            self._wver = ver
+
+    def sync_weights(self) -> None:
+        """Tell the trainer the MLP weights were modified through ``.data``."""
+        self._sync_weight_planes(force=True)
 
     def _after_step(self) -> None:
         """Host mirrors of what a step did on the device."""
@@ -376,7 +405,6 @@ class FusedCTRTrainer:
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
-        hip_ops.step_begin(self.step_ctr)
         y = y.reshape(-1)
         if y.dtype != torch.float32:
             y = y.float()
@@ -386,23 +414,30 @@ class FusedCTRTrainer:
         w = m.linear.weight.data if self.kind != "IPNN" else None
         gv = self.grad_views
         step_hint = self.step_count + 1
+        self._ev_wplanes = None
         if self._side is not None:
             # the sparse plan is only needed from the scatter on: build it on a side stream
-            # while the catch-up (plan-free, from the ids) and the forward run here
+            # while the catch-up (plan-free, from the ids) and the forward run here.
+            # Capture order: in a HIP graph the first captured successor of a node continues
+            # that node's hardware queue and the others start new queues; every fork / join
+            # on the step's critical path costs ~5-12 us (rocprofv3 timelines) — so the
+            # critical path is always enqueued before the branch that forks off it.
             main = torch.cuda.current_stream()
-            self._side.wait_stream(main)  # x ready; previous step's plan users done
-            if not torch.cuda.is_current_stream_capturing():
-                x.record_stream(self._side)
-            with torch.cuda.stream(self._side):
-                t_plan = self._mark("plan")
-                b.plan.build(x, self.V)
-                self._span("plan", t_plan)
+            ev0 = torch.cuda.Event()
+            ev0.record(main)  # x ready; previous step's plan users and Adam done
             t = self._mark("adam")
             hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
                                               self.last, x, self.rowmap, self.step_done,
                                               self.step_table, step_hint, self.betas,
                                               self.eps, self.weight_decay)
             self._span("adam", t)
+            self._side.wait_event(ev0)
+            if not torch.cuda.is_current_stream_capturing():
+                x.record_stream(self._side)
+            with torch.cuda.stream(self._side):
+                t_plan = self._mark("plan")
+                b.plan.build(x, self.V)
+                self._span("plan", t_plan)
             self._fork_sweep()
         else:
             t_plan = self._mark("plan")
@@ -434,6 +469,8 @@ class FusedCTRTrainer:
             hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
                                       grad_rows=b.grad_rows, grad_lin=b.grad_lin)
         self._span("scatter", t)
+        if self.kind in _MLP_KINDS:  # captured after the scatter: see the capture-order note
+            self._weight_grads(b, gz)
         if self.kind == "FM":  # MLP kinds: on the weight-gradient stream, off this chain
             hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         grad_rows, grad_lin, plan = b.grad_rows, (b.grad_lin if w is not None else None), b.plan
@@ -453,13 +490,34 @@ class FusedCTRTrainer:
                                    self.eps, self.weight_decay, step_dev=self.step_cur,
                                    table=self.step_table)
         self._span("adam", t)
+        # the dense Adam where the dense gradient completes: on the weight-gradient stream
+        # at one process (beside the embedding apply), after the exchange otherwise
+        wg = self._wgrad_stream if ws == 1 else None
+        if wg is None:
+            self._join_wgrad()
+        with torch.cuda.stream(wg) if wg is not None else _nullctx():
+            self._adam_dense(step_hint)
         self._join_wgrad()
-        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, step_hint,
-                           self.lr, self.betas, self.eps, self.weight_decay,
-                           step_dev=self.step_cur, table=self.step_table)
         self._join_sweep()
         hip_ops.step_end(self.step_ctr)
         return b.loss
+
+    def _adam_dense(self, step_hint: int) -> None:
+        """The flat dense parameters' Adam step; the MLP weights' planes are rewritten with
+        the updated values (the next step's GEMM operands) — by the Adam kernel itself when
+        a weight's row length is a multiple of 4, by a split pass after it otherwise."""
+        planes, resplit = [], []
+        if self._wplanes is not None:
+            for name, pl in zip(("mlp.0.weight", "mlp.3.weight"), self._wplanes):
+                if pl.cols % 4 == 0 and self.offsets[name] % 4 == 0:
+                    planes.append((self.offsets[name], pl))
+                else:
+                    resplit.append((name, pl))
+        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, step_hint,
+                           self.lr, self.betas, self.eps, self.weight_decay,
+                           step_dev=self.step_cur, table=self.step_table, planes=planes or None)
+        for name, pl in resplit:
+            hip_ops.split_planes(self.views[name], out=pl)
 
     def _fork_sweep(self) -> None:
         """Start this step's background sweep (after the catch-up: the batch's rows are
@@ -498,8 +556,6 @@ class FusedCTRTrainer:
         rank, ws = world()
         off1 = rank * B * H1
         off2 = ws * B * H1 + rank * B * H2
-        hip_ops.split_planes(vw["mlp.0.weight"], out=w0p)
-        hip_ops.split_planes(vw["mlp.3.weight"], out=w1p)
         t = self._mark("gather")
         if self.kind == "IPNN":  # cat = flat(E[x]) ++ pairwise inner products
             X = hip_ops.ipnn_forward(x, E, out=b.fm.emb_out, err_flag=self.err)
@@ -526,23 +582,9 @@ class FusedCTRTrainer:
         head = hip_ops.deepfm_head(b.h2, vw["mlp.6.weight"], vw["mlp.6.bias"], z_fm, y,
                                    mean_div=mean_div, drop_scale=1.0 / (1.0 - p1), out=b.head,
                                    dh_planes=b.dh2p)
-        gz, dh2 = head["gz"], head["dh_pre"]
-        # the weight / bias gradients are needed only by the dense Adam at the end of the
-        # step: they run on one side stream, the small layers' from the head on (under the
-        # dH1 / dX GEMMs), dW0 from dX on (under the scatter and the embedding Adam)
-        side = self._wgrad_stream
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side) if side is not None else _nullctx():
-            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
-            if "bias" in gv:  # DeepFM's FM bias: sum gz
-                hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
-            # Linear(200,1): dW = gz^T H2, db = sum gz; Linear(300,200): db1 = colsum dH2
-            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
-                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
-                                  (dh2, None, gv["mlp.3.bias"])])
-            # Linear(300,200): dW1 = dH2^T H1 (both operands k-strided: transpose reads)
-            self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B, out=gv["mlp.3.weight"])
+        gz = head["gz"]
+        b.ev_head = torch.cuda.Event()
+        b.ev_head.record()
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm_planes(b.dh2p, w1p, False, True, B, H1, H2, out=b.dh1, out_planes=b.dh1p,
                           epi=hip_ops.EPI_GRAD_MASK, aux=b.h1, scale=1.0 / (1.0 - p0))
@@ -550,19 +592,43 @@ class FusedCTRTrainer:
         self._gemm_planes(b.dh1p, w0p, False, True, B, W, H1, out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
             hip_ops.ipnn_backward(x, E, b.dx, out=b.dslot)
-        self._dw0(side, b, gv)  # after dX: forking dW0 beside dX measured slower
+        b.ev_dx = torch.cuda.Event()
+        b.ev_dx.record()
         return gz
 
-    def _dw0(self, side, b: _Bufs, gv) -> None:
-        """mlp.0's weight / bias gradients on the weight-gradient stream, under the scatter
-        chain: db0 = colsum dH1, dW0 = dH1^T X (both operands k-strided planes)."""
+    def _split_weights(self) -> None:
+        """The MLP weights' bf16 planes, re-split from the fp32 parameters every step."""
+        w0p, w1p = self._wplanes
+        hip_ops.split_planes(self.views["mlp.0.weight"], out=w0p)
+        hip_ops.split_planes(self.views["mlp.3.weight"], out=w1p)
+
+    def _weight_grads(self, b: _Bufs, gz) -> None:
+        """The dense-parameter gradients, needed only by the dense Adam at the end of the
+        step, on one side stream: the small layers' from the head on (under dH1 / dX), dW0
+        from dX on (under the scatter and the embedding Adam). Enqueued after the scatter
+        so that, in the captured graph, the dH1 -> dX -> scatter chain keeps one queue."""
+        gv, B = self.grad_views, b.B
+        side = self._wgrad_stream
+        H1 = b.h1.shape[1]
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
+            side.wait_event(b.ev_head)
         with torch.cuda.stream(side) if side is not None else _nullctx():
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
+            if "bias" in gv:  # DeepFM's FM bias: sum gz
+                hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+            # Linear(200,1): dW = gz^T H2, db = sum gz; Linear(300,200): db1 = colsum dH2
+            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
+                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
+                                  (b.head["dh_pre"], None, gv["mlp.3.bias"])])
+            # Linear(300,200): dW1 = dH2^T H1 (both operands k-strided: transpose reads)
+            self._gemm_planes(b.dh2p, b.h1p, True, True, b.h2.shape[1], H1, B,
+                              out=gv["mlp.3.weight"])
+            if side is not None:
+                side.wait_event(b.ev_dx)
+            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X (both operands k-strided)
             hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
-            H1, W = b.dh1.shape[1], b.dx.shape[1]
-            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, b.dh1.shape[0],
-                              out=gv["mlp.0.weight"])
+            W = b.dx.shape[1]
+            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B, out=gv["mlp.0.weight"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""

@@ -1,6 +1,6 @@
 """Per-step kernel timeline from a rocprofv3 --kernel-trace csv.
 
-    python tools/timeline.py run_kernel_trace.csv [--step N] [--marker step_begin_kernel]
+    python tools/timeline.py run_kernel_trace.csv [--step N] [--marker step_end_kernel]
 
 Splits the trace at each launch of the marker kernel (one per training step), prints the
 kernels of step N (default: the median-length step) with start offset, duration and queue,
@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=None)
-    ap.add_argument("--marker", default="step_begin_kernel")
+    ap.add_argument("--marker", default="step_end_kernel")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
