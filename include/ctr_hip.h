@@ -172,6 +172,17 @@ int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
                     const int32_t* step_ptr, void* ws, int64_t ws_bytes, ctr_stream_t stream);
 int ctr_gemm_planes_config(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K, int* tile,
                            int* splits, int* bm, int* bn);
+/* ctr_gemm_planes_lastcol: ctr_gemm_planes whose result column N-1 is written to
+ * last_col[m] (m < M) instead of C, which then holds N-1 columns (ldc >= N-1). With a B
+ * operand whose column N-1 is all ones (a ones column in the planes' zero padding), a weight
+ * gradient dW = G^T X and its bias gradient db = colsum(G) come out of ONE GEMM.
+ * Replaces: the mlp.0 / mlp.3 weight AND bias gradients of p_model.py:276-293 backward. */
+int ctr_gemm_planes_lastcol(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                            const ctr_planes* A, const ctr_planes* B, float* C, int64_t ldc,
+                            const ctr_planes* Cp, int epi, const float* bias, const float* aux,
+                            int64_t ldaux, float scale, float drop_p, uint64_t seed,
+                            uint64_t offset, const int32_t* step_ptr, float* last_col, void* ws,
+                            int64_t ws_bytes, ctr_stream_t stream);
 
 /* The producers of the MLP's GEMM operands writing planes directly (no fp32 round trip):
  * ctr_fm_forward_planes: ctr_fm_forward (no BCE head; DeepFM's FM part) whose flattened

@@ -76,6 +76,9 @@ SIGNATURES = {
     "ctr_gemm_planes": (_i32, [_i32, _i32, _i64, _i64, _i64, _planes_p, _planes_p, _vp, _i64,
                                _planes_p, _i32, _vp, _vp, _i64, _f32, _f32, _u64, _u64, _vp, _vp,
                                _i64, _vp]),
+    "ctr_gemm_planes_lastcol": (_i32, [_i32, _i32, _i64, _i64, _i64, _planes_p, _planes_p, _vp,
+                                       _i64, _planes_p, _i32, _vp, _vp, _i64, _f32, _f32, _u64,
+                                       _u64, _vp, _vp, _vp, _i64, _vp]),
     "ctr_gemm_planes_config": (_i32, [_i32, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "ctr_fm_forward_planes": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp,
                                      _planes_p, _vp, _vp]),

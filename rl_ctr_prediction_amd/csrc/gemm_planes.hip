@@ -54,6 +54,7 @@ struct PlanesArgs {
   GemmArgs g;           // M, N, C, ldc, epilogue, split-K slab stride
   uint16_t* cpl;        // output planes (nullptr: none)
   int64_t cpl_ld, cpl_ps;
+  float* last_col;      // non-null: result column N-1 goes to last_col[m], C has N-1 columns
 };
 
 // ---- LDS image swizzles ----------------------------------------------------------------
@@ -155,6 +156,7 @@ __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[
   GemmArgs ge = g;
   if (epi == CTR_EPI_BIAS_RELU_DROP && ge.step_ptr) ge.offset += (uint64_t)(*ge.step_ptr) << 32;
   const bool planes = a.cpl && !slab;
+  float* const lastc = slab ? nullptr : a.last_col;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -176,13 +178,16 @@ __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[
       o.w = n + 3 < g.N ? apply_epi(ge, epi, v.w, m, n + 3) : 0.f;
       if (C) {
         float* crow = C + m * g.ldc;
-        if (g.vec_c && n + 3 < g.N) {
+        const int64_t nc = lastc ? g.N - 1 : g.N;  // columns that go to C
+        if (g.vec_c && n + 3 < nc) {
           *reinterpret_cast<float4*>(crow + n) = o;
         } else {
-          crow[n] = o.x;
-          if (n + 1 < g.N) crow[n + 1] = o.y;
-          if (n + 2 < g.N) crow[n + 2] = o.z;
-          if (n + 3 < g.N) crow[n + 3] = o.w;
+          const float e[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (n + j < nc) crow[n + j] = e[j];
+            else if (lastc && n + j == nc) lastc[m] = e[j];
+          }
         }
       }
       if (planes) store_planes4(a, m, n, o);
@@ -356,18 +361,20 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
 
 // split-K: sum the fp32 slabs in split order (4 independent loads in flight per step of
 // the chain), then the epilogue (fp32 out and/or planes); one thread per 4 columns
+// slabs: [splits][M][sld], sld = align_up(N, 4) (the padding columns are never read as
+// results), so every row starts 16-B aligned and the float4 path always applies
 __global__ __launch_bounds__(64) void planes_reduce_kernel(PlanesArgs a, const float* __restrict__ slabs,
-                                                           int splits) {
+                                                           int splits, int64_t sld) {
   GemmArgs g = a.g;
   if (g.epi == CTR_EPI_BIAS_RELU_DROP && g.step_ptr) g.offset += (uint64_t)(*g.step_ptr) << 32;
   const int64_t n4 = (g.N + 3) / 4;
   const int64_t total = g.M * n4;
-  const int64_t slab = g.M * g.N;
-  const bool vec = g.N % 4 == 0;
+  const int64_t slab = g.M * sld;
+  const bool vec = true;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = t / n4, n = 4 * (t - m * n4);
-    const int64_t o = m * g.N + n;
+    const int64_t o = m * sld + n;
     float e[4];
     if (vec) {
       float4 s = *reinterpret_cast<const float4*>(slabs + o);
@@ -402,7 +409,11 @@ __global__ __launch_bounds__(64) void planes_reduce_kernel(PlanesArgs a, const f
       if (n + j < g.N) e[j] = apply_epi(g, g.epi, e[j], m, n + j);
     if (g.C) {
       float* crow = g.C + m * g.ldc;
-      for (int j = 0; j < 4 && n + j < g.N; ++j) crow[n + j] = e[j];
+      const int64_t nc = a.last_col ? g.N - 1 : g.N;
+      for (int j = 0; j < 4 && n + j < g.N; ++j) {
+        if (n + j < nc) crow[n + j] = e[j];
+        else a.last_col[m] = e[j];
+      }
     }
     if (a.cpl) store_planes4(a, m, n, make_float4(e[0], e[1], e[2], e[3]));
   }
@@ -583,7 +594,7 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
 #undef CTR_PL_K
 
 static int64_t pl_ws_bytes(const PlCfg& c, int64_t M, int64_t N) {
-  return c.splits > 1 ? (int64_t)c.splits * M * N * 4 : 0;
+  return c.splits > 1 ? (int64_t)c.splits * M * align_up(N, 4) * 4 : 0;
 }
 
 }  // namespace ctr
@@ -619,19 +630,22 @@ extern "C" int64_t ctr_gemm_planes_workspace_bytes(int a_rc, int b_rc, int64_t M
   return pl_ws_bytes(c, M, N);
 }
 
-extern "C" int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
-                               const ctr_planes* A, const ctr_planes* B, float* C, int64_t ldc,
-                               const ctr_planes* Cp, int epi, const float* bias, const float* aux,
-                               int64_t ldaux, float scale, float drop_p, uint64_t seed,
-                               uint64_t offset, const int32_t* step_ptr, void* ws,
-                               int64_t ws_bytes, ctr_stream_t stream) {
+extern "C" int ctr_gemm_planes_lastcol(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                                       const ctr_planes* A, const ctr_planes* B, float* C,
+                                       int64_t ldc, const ctr_planes* Cp, int epi,
+                                       const float* bias, const float* aux, int64_t ldaux,
+                                       float scale, float drop_p, uint64_t seed, uint64_t offset,
+                                       const int32_t* step_ptr, float* last_col, void* ws,
+                                       int64_t ws_bytes, ctr_stream_t stream) {
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "ctr_gemm_planes: negative size");
   if (M == 0 || N == 0) return CTR_OK;
   CTR_REQUIRE(C || Cp, "ctr_gemm_planes: no output");
+  CTR_REQUIRE(!last_col || (C && !Cp && N >= 2),
+              "ctr_gemm_planes: last_col needs an fp32 output C of N-1 >= 1 columns, no planes");
   CTR_REQUIRE(plane_src_ok(A) && plane_src_ok(B), "ctr_gemm_planes: bad operand plane layout");
   CTR_REQUIRE(!Cp || (plane_src_ok(Cp) && Cp->rows >= M && Cp->cols >= N),
               "ctr_gemm_planes: bad output plane layout");
-  CTR_REQUIRE(!C || ldc >= N, "ctr_gemm_planes: ldc < N");
+  CTR_REQUIRE(!C || ldc >= (last_col ? N - 1 : N), "ctr_gemm_planes: ldc < N");
   const int64_t Kp = align_up(std::max<int64_t>(K, 1), kPBK);
   // KC operand: storage [rows >= extent][cols >= Kp]; RC: storage [rows >= Kp][cols >= extent]
   CTR_REQUIRE(a_rc ? (A->rows >= Kp && A->cols >= M && A->cols % 16 == 0)
@@ -683,29 +697,44 @@ extern "C" int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t
     a.cpl_ld = Cp->ld;
     a.cpl_ps = Cp->plane_stride;
   }
+  a.last_col = last_col;
+  if (last_col) g.vec_c = g.vec_c && (N - 1) % 4 == 0;
   hipStream_t st = as_stream(stream);
   const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
   CTR_REQUIRE(tiles <= INT32_MAX && c.splits <= 65535, "ctr_gemm_planes: grid too large");
   const dim3 grid((unsigned)tiles, 1, (unsigned)c.splits);
   if (c.splits > 1) {
     PlanesArgs s = a;
+    const int64_t sld = align_up(N, 4);
     s.g.C = static_cast<float*>(ws);
-    s.g.ldc = N;
-    s.g.slab_stride = M * N;
-    s.g.vec_c = N % 4 == 0;
+    s.g.ldc = sld;
+    s.g.slab_stride = M * sld;
+    s.g.vec_c = (uintptr_t)ws % 16 == 0;
     s.cpl = nullptr;
+    s.last_col = nullptr;
     pl_launch(c, s, arc, brc, grid, st);
     CTR_LAUNCH_CHECK("gemm_planes_kernel (split-K)");
     const int64_t total = M * ceil_div(N, 4);
     const unsigned g2 = (unsigned)std::min<int64_t>(ceil_div(total, 64), 16384);
     hipLaunchKernelGGL(planes_reduce_kernel, g2, 64, 0, st, a, static_cast<const float*>(ws),
-                       c.splits);
+                       c.splits, sld);
     CTR_LAUNCH_CHECK("planes_reduce_kernel");
     return CTR_OK;
   }
   pl_launch(c, a, arc, brc, grid, st);
   CTR_LAUNCH_CHECK("gemm_planes_kernel");
   return CTR_OK;
+}
+
+extern "C" int ctr_gemm_planes(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
+                               const ctr_planes* A, const ctr_planes* B, float* C, int64_t ldc,
+                               const ctr_planes* Cp, int epi, const float* bias, const float* aux,
+                               int64_t ldaux, float scale, float drop_p, uint64_t seed,
+                               uint64_t offset, const int32_t* step_ptr, void* ws,
+                               int64_t ws_bytes, ctr_stream_t stream) {
+  return ctr_gemm_planes_lastcol(a_rc, b_rc, M, N, K, A, B, C, ldc, Cp, epi, bias, aux, ldaux,
+                                 scale, drop_p, seed, offset, step_ptr, nullptr, ws, ws_bytes,
+                                 stream);
 }
 
 extern "C" int ctr_gemm_planes_config(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,

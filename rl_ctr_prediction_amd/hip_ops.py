@@ -237,11 +237,17 @@ class Planes:
     zeros (allocated zeroed; producers write only the valid region, so the pad stays zero).
     x = x0 + (x1 + x2) recovers every fp32 element exactly (to_float)."""
 
-    def __init__(self, rows: int, cols: int, device, pad: int = 32):
+    def __init__(self, rows: int, cols: int, device, pad: int = 32, ones_col: bool = False):
         self.rows, self.cols = int(rows), int(cols)
         self.rows_pad = -(-max(self.rows, 1) // pad) * pad
-        self.cols_pad = -(-max(self.cols, 1) // pad) * pad
+        self.cols_pad = -(-max(self.cols + int(ones_col), 1) // pad) * pad
         self.t = torch.zeros(3, self.rows_pad, self.cols_pad, dtype=torch.bfloat16, device=device)
+        # ones_col: column `cols` (in the padding) holds 1.0 — exact in plane 0, zero in the
+        # others — so a GEMM reading this matrix as B with N = cols + 1 also returns the
+        # column sums of A (gemm_planes(last_col=...)); GEMMs with K = cols never read it.
+        self.ones_col = bool(ones_col)
+        if ones_col:
+            self.t[0, :self.rows, self.cols] = 1.0
         self.desc = PlanesDesc(self.t.data_ptr(), self.cols_pad, self.rows_pad * self.cols_pad,
                                self.rows_pad, self.cols_pad)
 
@@ -272,14 +278,33 @@ def split_planes(src: torch.Tensor, out: Planes | None = None) -> Planes:
 def gemm_planes(a: Planes, b: Planes, a_rc: bool, b_rc: bool, *, out: torch.Tensor | None = None,
                 out_planes: Planes | None = None, epi: int = EPI_NONE, bias=None, aux=None,
                 scale: float = 1.0, drop_p: float = 0.0, seed: int = 0, offset: int = 0,
-                step_dev: torch.Tensor | None = None) -> torch.Tensor | None:
+                step_dev: torch.Tensor | None = None,
+                last_col: torch.Tensor | None = None) -> torch.Tensor | None:
     """C = A.B on pre-split planes (ctr_gemm_planes). a_rc: A holds A^T ([K, M]); b_rc: B holds
     B itself ([K, N]) rather than the nn.Linear form [N, K]. Writes `out` (fp32 [M, N]) and/or
-    `out_planes` (the planes of the epilogue's result)."""
+    `out_planes` (the planes of the epilogue's result).
+    last_col ([M]): B (b_rc, built with ones_col) gets its ones column appended, and the
+    extra result column — the row sums of A^T's rows, i.e. colsum of the stored A — lands
+    here (ctr_gemm_planes_lastcol)."""
     M, K = (a.cols, a.rows) if a_rc else (a.rows, a.cols)
     N, Kb = (b.cols, b.rows) if b_rc else (b.rows, b.cols)
     if K != Kb:
         raise ValueError(f"gemm_planes: inner dims differ ({K} vs {Kb})")
+    if last_col is not None:
+        _f32(last_col, "last_col")
+        if not (b_rc and b.ones_col) or out is None or out_planes is not None:
+            raise ValueError("gemm_planes: last_col needs b_rc planes with ones_col and an fp32 out")
+        if last_col.numel() != M or not last_col.is_contiguous():
+            raise ValueError(f"gemm_planes: last_col must be {M} contiguous floats")
+        if tuple(out.shape) != (M, N) or (out.numel() and out.stride(1) != 1):
+            raise ValueError(f"gemm_planes: out must be [{M}, {N}]")
+        nbytes = lib.ctr_gemm_planes_workspace_bytes(int(a_rc), 1, M, N + 1, K)
+        ws = Workspace.get(nbytes, a.device)
+        lib.ctr_gemm_planes_lastcol(int(a_rc), 1, M, N + 1, K, a.desc, b.desc, _p(out),
+                                    out.stride(0), None, int(epi), _p(bias), None, 0,
+                                    float(scale), 0.0, 0, 0, None, _p(last_col), _p(ws),
+                                    0 if ws is None else ws.numel(), _stream())
+        return out
     if out is None and out_planes is None:
         out = torch.empty(M, N, dtype=torch.float32, device=a.device)
     if out is not None:
@@ -329,15 +354,17 @@ def tensor_sum(x: torch.Tensor, scale: float = 1.0, out=None) -> torch.Tensor:
 
 
 def colsum_multi(jobs) -> None:
-    """Several colsum() calls in one launch pair: jobs = [(X [M,N], row_w or None, out [N])];
-    each out is bitwise what colsum(X, row_w, out=out) writes."""
+    """Several colsum() calls in one launch pair: jobs = [(X [M,N], row_w or None, out [N]
+    [, scale])]; each out is bitwise what colsum(X, row_w, scale, out=out) writes."""
     from ._lib import ColsumJob
     arr = (ColsumJob * len(jobs))()
-    for i, (X, row_w, out) in enumerate(jobs):
+    for i, job in enumerate(jobs):
+        X, row_w, out = job[:3]
+        scale = float(job[3]) if len(job) > 3 else 1.0
         _f32(X, "X")
         if X.dim() != 2 or out.numel() != X.shape[1]:
             raise ValueError("colsum_multi: X must be [M, N] and out N elements")
-        arr[i] = ColsumJob(_p(X), X.shape[0], X.shape[1], X.stride(0), _p(row_w), 1.0, _p(out))
+        arr[i] = ColsumJob(_p(X), X.shape[0], X.shape[1], X.stride(0), _p(row_w), scale, _p(out))
     nbytes = lib.ctr_colsum_multi_workspace_bytes(len(jobs), arr)
     ws = Workspace.get(nbytes, jobs[0][0].device)
     lib.ctr_colsum_multi_f32(len(jobs), arr, _p(ws), ws.numel(), _stream())

@@ -308,7 +308,10 @@ class FusedCTRTrainer:
             H1, H2 = mlp[0].out_features, mlp[3].out_features
             b.h1, b.h2, b.dh1, b.dx = e(B, H1), e(B, H2), e(B, H1), e(B, W)
             P = hip_ops.Planes
-            b.xp, b.h1p, b.dh2p, b.dh1p = P(B, W, dev), P(B, H1, dev), P(B, H2, dev), P(B, H1, dev)
+            # H1 carries a ones column in its padding: dW1 then returns the bias gradient
+            # db1 = colsum dH2 as one more output column
+            b.xp, b.h1p = P(B, W, dev), P(B, H1, dev, ones_col=True)
+            b.dh2p, b.dh1p = P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
                 b.dslot = e(S, K)
                 b.zero = torch.zeros(B, dtype=torch.float32, device=dev)
@@ -604,30 +607,33 @@ class FusedCTRTrainer:
 
     def _weight_grads(self, b: _Bufs, gz) -> None:
         """The dense-parameter gradients, needed only by the dense Adam at the end of the
-        step, on one side stream: the small layers' from the head on (under dH1 / dX), dW0
-        from dX on (under the scatter and the embedding Adam). Enqueued after the scatter
-        so that, in the captured graph, the dH1 -> dX -> scatter chain keeps one queue."""
+        step, on the side stream: from the head on (under dH1 / dX) one launch pair of
+        column sums (batch loss, FM bias, mlp.6) and dW1 with db1 (ones-column GEMM), from
+        dX on (under the scatter and the embedding Adam) db0 and dW0. Enqueued after the
+        scatter so that, in the captured graph, the dH1 -> dX -> scatter chain keeps one
+        queue. Measured alternatives (rocprofv3 timelines, C3): forking everything from dH1
+        (side kernels dispatched after dX has filled the CUs: +40 us), dW0 from dH1 (it then
+        takes the CUs ahead of the scatter chain: +25 us)."""
         gv, B = self.grad_views, b.B
         side = self._wgrad_stream
-        H1 = b.h1.shape[1]
+        H1, H2, W = b.h1.shape[1], b.h2.shape[1], b.dx.shape[1]
         if side is not None:
             side.wait_event(b.ev_head)
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)  # batch mean BCE
+            jobs = [(b.fm.loss_elem.view(B, 1), None, b.loss, 1.0 / B)]  # batch mean BCE
             if "bias" in gv:  # DeepFM's FM bias: sum gz
-                hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
-            # Linear(200,1): dW = gz^T H2, db = sum gz; Linear(300,200): db1 = colsum dH2
-            hip_ops.colsum_multi([(b.h2, gz, gv["mlp.6.weight"].view(-1)),
-                                  (gz.view(-1, 1), None, gv["mlp.6.bias"].view(1)),
-                                  (b.head["dh_pre"], None, gv["mlp.3.bias"])])
-            # Linear(300,200): dW1 = dH2^T H1 (both operands k-strided: transpose reads)
-            self._gemm_planes(b.dh2p, b.h1p, True, True, b.h2.shape[1], H1, B,
-                              out=gv["mlp.3.weight"])
-            if side is not None:
+                jobs.append((gz.view(B, 1), None, gv["bias"].view(1)))
+            # Linear(200,1): dW = gz^T H2, db = sum gz
+            jobs += [(b.h2, gz, gv["mlp.6.weight"].view(-1)),
+                     (gz.view(B, 1), None, gv["mlp.6.bias"].view(1))]
+            hip_ops.colsum_multi(jobs)
+            # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2 (H1's ones column)
+            self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B,
+                              out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
+            if side is not None:  # from dX on
                 side.wait_event(b.ev_dx)
-            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X (both operands k-strided)
+            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X
             hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
-            W = b.dx.shape[1]
             self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B, out=gv["mlp.0.weight"])
 
     def _join_wgrad(self) -> None:

@@ -211,3 +211,30 @@ def test_trainer_weight_planes_follow_updates(cuda):
     tr.step(x, y)
     torch.cuda.synchronize()
     check()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 1664, 8192), (200, 300, 8192), (37, 45, 100)])
+def test_gemm_planes_last_col(cuda, M, N, K):
+    """dW = G^T X and db = colsum(G) from one GEMM: X planes with a ones column, N + 1
+    output columns, the last routed to last_col (split-K and single-pass tilings)."""
+    H = _H()
+    g = torch.Generator().manual_seed(2)
+    G, X = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
+    pg = H.split_planes(G.to(cuda))
+    px = H.Planes(K, N, cuda, ones_col=True)
+    H.split_planes(X.to(cuda), out=px)
+    assert float(px.t[0, :K, N].float().min()) == 1.0 and float(px.t[1:, :, N].abs().max()) == 0
+    out = torch.full((M, N), float("nan"), device=cuda)
+    db = torch.full((M,), float("nan"), device=cuda)
+    H.gemm_planes(pg, px, True, True, out=out, last_col=db)
+    ref = G.double().t() @ X.double()
+    bound = G.double().abs().t() @ X.double().abs()
+    assert ((out.cpu().double() - ref).abs() <= 2e-6 * bound + 1e-30).all()
+    dref = G.double().sum(0)
+    dbound = G.double().abs().sum(0)
+    assert ((db.cpu().double() - dref).abs() <= 2e-6 * dbound + 1e-30).all()
+    # the same planes still serve GEMMs that contract over their K = N columns (fwd0 / fwd1)
+    Y = torch.randn(N, 17, generator=g)
+    y = H.gemm_planes(px, H.split_planes(Y.t().contiguous().to(cuda)), False, False)
+    yref = X.double() @ Y.double()
+    assert ((y.cpu().double() - yref).abs() <= 2e-6 * (X.double().abs() @ Y.double().abs()) + 1e-30).all()

@@ -1,0 +1,16 @@
+#!/bin/bash
+# MFMA / LDS / wait counters of the six C3 MLP GEMMs (tools/gemm_planes_pmc.py), one
+# rocprofv3 --pmc pass per counter set, then a per-shape summary.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/gemm_pmc
+rm -rf $OUT; mkdir -p $OUT
+i=0
+for P in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU" \
+         "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+         "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- \
+    python3 tools/gemm_planes_pmc.py run 10 > $OUT/p$i.log 2>&1 || { tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 tools/gemm_planes_pmc.py summary $OUT 10 | tee $OUT/summary.txt
