@@ -371,6 +371,36 @@ int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float*
                                   const int32_t* step_ptr, const float* step_table, double beta1,
                                   double beta2, double eps, double weight_decay,
                                   ctr_stream_t stream);
+/* Fused scatter + deferred Adam (ws == 1, deferred mode): the segmented row sums of
+ * ctr_fm_embedding_grad / ctr_segment_sum_rows with ctr_adam_deferred_rows(the sums,
+ * step = *step_ptr) folded into the pass that finishes the rows spanning several chunks —
+ * bitwise the same tables, one launch fewer, and the spanning rows' sums never round-trip
+ * through memory. grad_rows / grad_lin (out / out_lin) are required scratch; with
+ * keep_sums != 0 they hold every row's sum afterwards (else only the rows inside one
+ * chunk). Needs K % 4 == 0, K <= 256.
+ * Replaces: embedding_dense_backward + optimizer.step of all_main/pretrain_main.py:77-78. */
+typedef struct ctr_deferred_table {
+  float* emb;
+  float* m_emb;
+  float* v_emb;
+  float* lin;    /* the linear table w[V] and its moments, or all NULL */
+  float* m_lin;
+  float* v_lin;
+  int32_t* last; /* step each row is current to */
+} ctr_deferred_table;
+int ctr_fm_embedding_grad_adam(const ctr_sparse_plan* plan, int F, int K, const float* gz,
+                               const float* sum_e, const float* dx,
+                               const ctr_deferred_table* table, const int32_t* step_ptr,
+                               const float* step_table, double beta1, double beta2, double eps,
+                               double weight_decay, float* grad_rows, float* grad_lin,
+                               int keep_sums, void* ws, int64_t ws_bytes, ctr_stream_t stream);
+int ctr_segment_sum_rows_adam(const ctr_sparse_plan* plan, int K, const float* vals,
+                              const float* vals_lin, const ctr_deferred_table* table,
+                              const int32_t* step_ptr, const float* step_table, double beta1,
+                              double beta2, double eps, double weight_decay, float* out,
+                              float* out_lin, int keep_sums, void* ws, int64_t ws_bytes,
+                              ctr_stream_t stream);
+
 /* Device step counters (int32[2]): ctr[0] = completed steps, ctr[1] = the step in flight.
  * ctr_step_begin: ctr[1] = ctr[0] + 1;  ctr_step_end: ctr[0] = ctr[1], ctr[1] += 1. A
  * counter initialised to {0, 1} therefore needs no ctr_step_begin (one launch less per

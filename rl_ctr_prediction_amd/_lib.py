@@ -47,6 +47,15 @@ class PlanesDesc(C.Structure):
 _planes_p = C.POINTER(PlanesDesc)
 
 
+class DeferredTable(C.Structure):
+    """Mirror of ``ctr_deferred_table`` (include/ctr_hip.h)."""
+    _fields_ = [("emb", _vp), ("m_emb", _vp), ("v_emb", _vp), ("lin", _vp), ("m_lin", _vp),
+                ("v_lin", _vp), ("last", _vp)]
+
+
+_table_p = C.POINTER(DeferredTable)
+
+
 class PlaneViewDesc(C.Structure):
     """Mirror of ``ctr_plane_view`` (include/ctr_hip.h)."""
     _fields_ = [("offset", _i64), ("rows", _i64), ("cols", _i64), ("planes", PlanesDesc)]
@@ -102,6 +111,10 @@ SIGNATURES = {
     "ctr_rows_to_dense": (_i32, [_plan_p, _i32, _vp, _vp, _vp, _vp, _vp]),
     "ctr_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp, _vp, _f64, _f64, _f64,
                               _f64, _vp]),
+    "ctr_fm_embedding_grad_adam": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _table_p, _vp, _vp,
+                                          _f64, _f64, _f64, _f64, _vp, _vp, _i32, _vp, _i64, _vp]),
+    "ctr_segment_sum_rows_adam": (_i32, [_plan_p, _i32, _vp, _vp, _table_p, _vp, _vp, _f64, _f64,
+                                         _f64, _f64, _vp, _vp, _i32, _vp, _i64, _vp]),
     "ctr_adam_dense_planes": (_i32, [_vp, _vp, _vp, _vp, _i64, _f64, _f64, _vp, _vp, _f64, _f64,
                                      _f64, _f64, _vp, _i32, _vp]),
     "ctr_adam_embedding": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _f64,

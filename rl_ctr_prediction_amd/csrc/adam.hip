@@ -19,48 +19,9 @@
 // receives every step's arithmetic, in order; only the HBM round trips of untouched rows
 // between two uses disappear. Results are bitwise identical to the dense pass
 // (tests/test_gpu_deferred.py).
-#include "ctr_common.h"
+#include "adam_common.h"
 
 namespace ctr {
-
-struct AdamHP {
-  float neg_step_size;  // -lr / (1 - beta1^t)
-  float inv_bc2_sqrt;   // 1 / sqrt(1 - beta2^t)
-  float w1;             // 1 - beta1   (lerp weight)
-  float beta2;
-  float w2;             // 1 - beta2   (addcmul value)
-  float eps;
-  float wd;
-};
-
-// One Adam element update. m and v use torch's own FMA forms (bit-identical to its CPU
-// single-tensor Adam, pinned by tests); the parameter step uses the hardware square root
-// and reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp) instead of IEEE-exact sequences: torch's
-// own CPU sqrt is not correctly rounded either, the step differs by a few ulps of the
-// step (~1e-10 absolute at lr 1e-3), and the replayed (deferred) path stays ~3x cheaper.
-// Every Adam kernel below calls this one function, so the dense and the deferred-exact
-// paths produce bitwise identical tables.
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
-                                          const AdamHP& h) {
-#pragma clang fp contract(off)
-  g = __builtin_fmaf(h.wd, p, g);                 // grad.add(param, alpha=wd)
-  m = __builtin_fmaf(h.w1, g - m, m);             // exp_avg.lerp_(grad, 1-beta1)
-  v = __builtin_fmaf(h.w2 * g, g, v * h.beta2);   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-  const float denom = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), h.inv_bc2_sqrt, h.eps);
-  p = __builtin_fmaf(h.neg_step_size * m, __builtin_amdgcn_rcpf(denom), p);  // addcdiv_
-}
-
-// Four elements (a float4 column). Scalar ops on purpose: a packed-fp32 form
-// (v_pk_fma_f32 / v_pk_mul_f32, bitwise the same results) measured slower on MI355X — the
-// apply pass 2-4x (deferred_rows_vec<APPLY>: 7.3 -> 32.6 us at C2, 33.5 -> 59.7 us at C3)
-// and no faster on the flush (3.54 vs 3.56 ms), which is not VALU-bound.
-__device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4& v,
-                                         const AdamHP& h) {
-  adam_elem(p.x, g.x, m.x, v.x, h);
-  adam_elem(p.y, g.y, m.y, v.y, h);
-  adam_elem(p.z, g.z, m.z, v.z, h);
-  adam_elem(p.w, g.w, m.w, v.w, h);
-}
 
 // The replay step of an absent row (g = 0 before weight decay) on four elements, in
 // packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 operations per
@@ -104,7 +65,6 @@ __device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v,
 
 // ------------------------------------------------------------------ dense -----------
 // step_ptr != NULL: the step's scalars come from the device step table (HIP-graph replay)
-__device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s);
 
 // Up to two row-major [rows, cols] sub-matrices of the flat parameter vector (the MLP
 // weights the GEMMs read as bf16 planes) whose planes are rewritten with the updated values,
@@ -247,12 +207,6 @@ __global__ __launch_bounds__(256) void adam_embedding_scalar(
 }
 
 // ------------------------------------------------------------ deferred-exact --------
-// step_tab[2t] = -lr/(1-beta1^t), step_tab[2t+1] = 1/sqrt(1-beta2^t)  (host doubles -> f32)
-__device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s) {
-  const float2 v = reinterpret_cast<const float2*>(tab)[s];
-  h.neg_step_size = v.x;
-  h.inv_bc2_sqrt = v.y;
-}
 
 // Rows of a sparse plan (unique rows of a batch). One lane group of K4 lanes per row
 // (float4 columns), 64/K4 rows per wave. APPLY=false: replay to `step` (catch-up before
@@ -560,20 +514,6 @@ __global__ __launch_bounds__(256) void deferred_scalar(
   }
 }
 
-// Hyper-parameters arrive as doubles, exactly as torch's python code holds them; each is
-// rounded to float once, where ATen casts the python scalar for the fp32 kernel.
-static AdamHP make_hp(double step_size, double bc2_sqrt, double beta1, double beta2, double eps,
-                      double wd) {
-  AdamHP h;
-  h.neg_step_size = (float)(-step_size);
-  h.inv_bc2_sqrt = (float)(1.0 / bc2_sqrt);
-  h.w1 = (float)(1.0 - beta1);
-  h.beta2 = (float)beta2;
-  h.w2 = (float)(1.0 - beta2);
-  h.eps = (float)eps;
-  h.wd = (float)wd;
-  return h;
-}
 
 }  // namespace ctr
 

@@ -9,7 +9,7 @@
 // 16-position chunks so every lane group does equal work; chunk partials of rows that
 // span chunks are added in chunk order by a second pass. No float atomics anywhere: the
 // result is bitwise reproducible, which is what keeps data-parallel replicas identical.
-#include "ctr_common.h"
+#include "adam_common.h"
 
 namespace ctr {
 
@@ -75,7 +75,28 @@ struct SegArgs {
   int32_t* rowmap;
   void* part;       // [n_chunks, 2, KV]  chunk partials: [0] run holding the chunk's first
   float* part_lin;  // [n_chunks, 2]      position, [1] the chunk's last (open) run
+  // fused deferred-Adam apply (float4 path, seg_combine_apply_kernel): every row's final
+  // sum is applied to the table by the pass that finishes the spanning rows
+  bool apply;
+  bool out_keep;  // apply mode: also write the spanning rows' sums to out / out_lin
+  float4 *E, *mE, *vE;
+  float *w, *mw, *vw;
+  int32_t* last;
+  const int32_t* step_ptr;
+  const float* tab;
+  AdamHP hp;
 };
+
+// a completed row sum: written out (and the rowmap entry of the dense-mode optimizer)
+template <typename VT>
+__device__ __forceinline__ void seg_emit(const SegArgs& a, int64_t u, int c, bool col,
+                                         const VT& acc, float accl) {
+  if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
+  if (c == 0) {
+    if (a.out_lin) a.out_lin[u] = accl;
+    if (a.rowmap) a.rowmap[a.unique_rows[u]] = (int32_t)u;
+  }
+}
 
 enum { MODE_FM = 0, MODE_VALS = 1 };
 
@@ -125,11 +146,7 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
     const int32_t off0 = a.seg_offsets[u];
     const int32_t off1 = a.seg_offsets[u + 1];
     if (off0 / kChunk == (off1 - 1) / kChunk) {  // whole row inside this chunk: final
-      if (col) static_cast<VT*>(a.out)[(int64_t)u * a.KV + c] = acc;
-      if (c == 0) {
-        if (a.out_lin) a.out_lin[u] = accl;
-        if (a.rowmap) a.rowmap[a.unique_rows[u]] = u;
-      }
+      seg_emit<VT>(a, u, c, col, acc, accl);
     } else {
       const int64_t k = gid * 2 + (first_run ? 0 : 1);
       if (col) static_cast<VT*>(a.part)[k * a.KV + c] = acc;
@@ -191,11 +208,64 @@ __global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
       VOps<VT>::add(acc, VOps<VT>::shfl_xor(acc, o));
       accl += __shfl_xor(accl, o, kWave);
     }
-    if (g == 0) {
-      if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
-      if (c == 0) {
-        if (a.out_lin) a.out_lin[u] = accl;
-        if (a.rowmap) a.rowmap[a.unique_rows[u]] = (int32_t)u;
+    if (g == 0) seg_emit<VT>(a, u, c, col, acc, accl);
+  }
+}
+
+// The combine pass with the deferred Adam apply fused in (float4): a wave takes G = 64/LPR
+// consecutive unique rows. Rows inside one chunk (their sum already in `out`, from
+// seg_chunk) are applied by their own lane group, all G at once; then each row of the G
+// that spans chunks is summed by the whole wave exactly as seg_combine_kernel sums it (same
+// partial order, same butterfly: bitwise the same sums) and applied by lane group 0. One
+// launch for what the combine and ctr_adam_deferred_rows did in two, and the spanning
+// rows' sums never make the round trip through `out`.
+template <int LPR>
+__global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
+  using VT = float4;
+  constexpr int kChunk = seg_chunk<LPR>();
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, c = lane % LPR;
+  const bool col = c < a.KV;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int U = *a.num_unique;
+  const int step = *a.step_ptr;
+  for (int64_t u0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave) * G; u0 < U;
+       u0 += waves * G) {
+    {  // rows inside one chunk: one lane group each
+      const int64_t u = u0 + g;
+      if (u < U) {
+        const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
+        if (off0 / kChunk == (off1 - 1) / kChunk) {
+          const VT gr = col ? static_cast<const VT*>(a.out)[u * a.KV + c] : VOps<VT>::zero();
+          const float gl = a.out_lin ? a.out_lin[u] : 0.f;
+          deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV,
+                             c, col, gr, gl, step, a.tab, a.hp);
+        }
+      }
+    }
+    for (int j = 0; j < G && u0 + j < U; ++j) {  // rows spanning chunks: the whole wave
+      const int64_t u = u0 + j;
+      const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
+      const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
+      if (fs == ls) continue;  // wave-uniform
+      const int64_t P = ls - fs + 1;
+      VT acc = VOps<VT>::zero();
+      float accl = 0.f;
+      for (int64_t i = g; i < P; i += G) {
+        const int64_t k = i == 0 ? fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1) : (fs + i) * 2;
+        if (col) VOps<VT>::add(acc, static_cast<const VT*>(a.part)[k * a.KV + c]);
+        accl += a.part_lin[k];
+      }
+#pragma unroll
+      for (int o = LPR; o < kWave; o <<= 1) {
+        VOps<VT>::add(acc, VOps<VT>::shfl_xor(acc, o));
+        accl += __shfl_xor(accl, o, kWave);
+      }
+      if (g == 0) {
+        if (a.out_keep) seg_emit<VT>(a, u, c, col, acc, accl);
+        deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV,
+                           c, col, acc, accl, step, a.tab, a.hp);
       }
     }
   }
@@ -213,6 +283,13 @@ static int launch_seg_lpr(SegArgs& a, int mode, hipStream_t st) {
   CTR_LAUNCH_CHECK("seg_chunk_kernel");
   // one wave per unique row (rows are at most S): up to 2048 blocks of 4 waves
   const unsigned g2 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(a.S, 4), 2048));
+  if constexpr (std::is_same<VT, float4>::value) {
+    if (a.apply) {
+      hipLaunchKernelGGL((seg_combine_apply_kernel<LPR>), g2, 256, 0, st, a);
+      CTR_LAUNCH_CHECK("seg_combine_apply_kernel");
+      return CTR_OK;
+    }
+  }
   hipLaunchKernelGGL((seg_combine_kernel<VT, LPR>), g2, 256, 0, st, a);
   CTR_LAUNCH_CHECK("seg_combine_kernel");
   return CTR_OK;
@@ -337,6 +414,82 @@ extern "C" int ctr_fm_embedding_grad(const ctr_sparse_plan* plan, int F, int K, 
   const bool al = ((uintptr_t)emb | (uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)grad_rows |
                    (uintptr_t)ws) % 16 == 0;
   return launch_seg(a, K, MODE_FM, as_stream(stream), al);
+}
+
+static int seg_set_apply(SegArgs& a, int K, const ctr_deferred_table* t, const int32_t* step_ptr,
+                         const float* step_table, double beta1, double beta2, double eps,
+                         double weight_decay) {
+  CTR_REQUIRE(t && t->emb && t->m_emb && t->v_emb && t->last && step_ptr && step_table,
+              "segment sum + Adam: null table / step pointer");
+  CTR_REQUIRE((t->lin && t->m_lin && t->v_lin) || (!t->lin && !t->m_lin && !t->v_lin),
+              "segment sum + Adam: linear table pointers must be all set or all NULL");
+  CTR_REQUIRE(K % 4 == 0 && K / 4 <= 64 &&
+                  ((uintptr_t)t->emb | (uintptr_t)t->m_emb | (uintptr_t)t->v_emb) % 16 == 0,
+              "segment sum + Adam: needs K %% 4 == 0, K <= 256 and 16-B aligned rows");
+  a.apply = true;
+  a.E = reinterpret_cast<float4*>(t->emb);
+  a.mE = reinterpret_cast<float4*>(t->m_emb);
+  a.vE = reinterpret_cast<float4*>(t->v_emb);
+  a.w = t->lin;
+  a.mw = t->m_lin;
+  a.vw = t->v_lin;
+  a.last = t->last;
+  a.step_ptr = step_ptr;
+  a.tab = step_table;
+  a.hp = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  return CTR_OK;
+}
+
+extern "C" int ctr_fm_embedding_grad_adam(const ctr_sparse_plan* plan, int F, int K,
+                                          const float* gz, const float* sum_e, const float* dx,
+                                          const ctr_deferred_table* table,
+                                          const int32_t* step_ptr, const float* step_table,
+                                          double beta1, double beta2, double eps,
+                                          double weight_decay, float* grad_rows,
+                                          float* grad_lin, int keep_sums, void* ws,
+                                          int64_t ws_bytes, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_fm_embedding_grad_adam: incomplete plan");
+  CTR_REQUIRE(F > 0 && K > 0 && gz && sum_e, "ctr_fm_embedding_grad_adam: bad arguments");
+  if (plan->S == 0) return CTR_OK;
+  CTR_REQUIRE(grad_rows && grad_lin, "ctr_fm_embedding_grad_adam: grad_rows / grad_lin needed");
+  SegArgs a;
+  int rc = seg_prepare(a, plan, K, grad_rows, grad_lin, nullptr, ws, ws_bytes);
+  if (rc != CTR_OK) return rc;
+  rc = seg_set_apply(a, K, table, step_ptr, step_table, beta1, beta2, eps, weight_decay);
+  if (rc != CTR_OK) return rc;
+  a.out_keep = keep_sums != 0;
+  a.F = F;
+  a.gz = gz;
+  a.sum_e = sum_e;
+  a.dx = dx;
+  a.emb = table->emb;
+  CTR_REQUIRE(((uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)grad_rows | (uintptr_t)ws) % 16 == 0,
+              "ctr_fm_embedding_grad_adam: 16-B aligned buffers required");
+  return launch_seg(a, K, MODE_FM, as_stream(stream), true);
+}
+
+extern "C" int ctr_segment_sum_rows_adam(const ctr_sparse_plan* plan, int K, const float* vals,
+                                         const float* vals_lin, const ctr_deferred_table* table,
+                                         const int32_t* step_ptr, const float* step_table,
+                                         double beta1, double beta2, double eps,
+                                         double weight_decay, float* out, float* out_lin,
+                                         int keep_sums, void* ws, int64_t ws_bytes,
+                                         ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_segment_sum_rows_adam: incomplete plan");
+  CTR_REQUIRE(K > 0 && vals, "ctr_segment_sum_rows_adam: bad arguments");
+  if (plan->S == 0) return CTR_OK;
+  CTR_REQUIRE(out && !vals_lin == !out_lin, "ctr_segment_sum_rows_adam: out (and out_lin) needed");
+  SegArgs a;
+  int rc = seg_prepare(a, plan, K, out, out_lin, nullptr, ws, ws_bytes);
+  if (rc != CTR_OK) return rc;
+  rc = seg_set_apply(a, K, table, step_ptr, step_table, beta1, beta2, eps, weight_decay);
+  if (rc != CTR_OK) return rc;
+  a.out_keep = keep_sums != 0;
+  a.vals = vals;
+  a.vals_lin = vals_lin;
+  CTR_REQUIRE(((uintptr_t)vals | (uintptr_t)out | (uintptr_t)ws) % 16 == 0,
+              "ctr_segment_sum_rows_adam: 16-B aligned buffers required");
+  return launch_seg(a, K, MODE_VALS, as_stream(stream), true);
 }
 
 extern "C" int ctr_segment_sum_rows(const ctr_sparse_plan* plan, int K, const float* vals,

@@ -18,6 +18,7 @@ from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS
 __all__ = [
     "embedding_gather", "fm_forward", "fm_forward_planes", "bce_sigmoid", "deepfm_head", "gemm", "linear",
     "tensor_sum", "colsum", "transpose", "Planes", "split_planes", "gemm_planes", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
+    "fm_embedding_grad_adam", "segment_sum_rows_adam",
     "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
     "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
@@ -505,6 +506,44 @@ def segment_sum_rows(plan: SparsePlanBuffers, vals, vals_lin=None, rowmap=None, 
     lib.ctr_segment_sum_rows(plan.struct(), int(K), _p(vals), _p(vals_lin), _p(out), _p(out_lin),
                              _p(rowmap), _p(ws), ws.numel(), _stream())
     return out, out_lin
+
+
+def _deferred_table(emb, m_emb, v_emb, lin, m_lin, v_lin, last):
+    from ._lib import DeferredTable
+    for t, n in ((emb, "emb"), (m_emb, "m_emb"), (v_emb, "v_emb")):
+        _f32(t, n)
+    return DeferredTable(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), _p(last))
+
+
+def fm_embedding_grad_adam(plan: SparsePlanBuffers, F: int, gz, sum_e, dx, table, step_dev,
+                           step_table: "AdamStepTable", step: int, betas=(0.9, 0.999), eps=1e-8,
+                           weight_decay=0.0, grad_rows=None, grad_lin=None,
+                           keep_sums: bool = False) -> None:
+    """fm_embedding_grad + adam_deferred_rows(sums, step = *step_dev) with the apply fused
+    into the combine pass (ctr_fm_embedding_grad_adam): table = (E, m_E, v_E, w, m_w, v_w,
+    last); grad_rows / grad_lin are scratch, holding every row's sum with keep_sums."""
+    K = table[0].shape[1]
+    ws = _seg_ws(plan, K)
+    tab = step_table.ensure(step)
+    lib.ctr_fm_embedding_grad_adam(plan.struct(), int(F), int(K), _p(gz), _p(sum_e), _p(dx),
+                                   _deferred_table(*table), _p(step_dev), _p(tab),
+                                   float(betas[0]), float(betas[1]), float(eps),
+                                   float(weight_decay), _p(grad_rows), _p(grad_lin),
+                                   int(keep_sums), _p(ws), ws.numel(), _stream())
+
+
+def segment_sum_rows_adam(plan: SparsePlanBuffers, vals, vals_lin, table, step_dev,
+                          step_table: "AdamStepTable", step: int, betas=(0.9, 0.999), eps=1e-8,
+                          weight_decay=0.0, out=None, out_lin=None, keep_sums: bool = False) -> None:
+    """segment_sum_rows + adam_deferred_rows in one pass (ctr_segment_sum_rows_adam)."""
+    K = vals.shape[1]
+    ws = _seg_ws(plan, K)
+    tab = step_table.ensure(step)
+    lib.ctr_segment_sum_rows_adam(plan.struct(), int(K), _p(vals), _p(vals_lin),
+                                  _deferred_table(*table), _p(step_dev), _p(tab),
+                                  float(betas[0]), float(betas[1]), float(eps),
+                                  float(weight_decay), _p(out), _p(out_lin), int(keep_sums),
+                                  _p(ws), ws.numel(), _stream())
 
 
 def rows_to_dense(plan: SparsePlanBuffers, V: int, grad_rows, grad_lin=None):

@@ -150,6 +150,10 @@ class FusedCTRTrainer:
         # its own stream. Off by default: measured on MI355X (C3) it slows the concurrent
         # GEMMs by more than it saves at flush() (8.6 vs 9.9 M ex/s at K=30)
         self.sweep_slices = 0
+        # fused scatter + Adam apply (one process, deferred mode); keep_grads keeps every
+        # row's gradient sum in b.grad_rows / b.grad_lin (tests read them)
+        self.fuse_apply = True
+        self.keep_grads = False
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -466,8 +470,21 @@ class FusedCTRTrainer:
             torch.cuda.current_stream().wait_stream(self._side)  # the plan
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
+        # one process, deferred Adam: the row sums are applied where they complete
+        fused = ws == 1 and self.deferred and self._vec_ok and self.fuse_apply
+        table = (E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last)
+        apply_kw = dict(step_dev=self.step_cur, step_table=self.step_table, step=step_hint,
+                        betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
         if self.kind == "IPNN":
-            hip_ops.segment_sum_rows(b.plan, b.dslot, rowmap=sparse_rowmap, out=b.grad_rows)
+            if fused:
+                hip_ops.segment_sum_rows_adam(b.plan, b.dslot, None, table, **apply_kw,
+                                              out=b.grad_rows, keep_sums=self.keep_grads)
+            else:
+                hip_ops.segment_sum_rows(b.plan, b.dslot, rowmap=sparse_rowmap, out=b.grad_rows)
+        elif fused:
+            hip_ops.fm_embedding_grad_adam(b.plan, F, gz, b.fm.sum_e, b.dx, table, **apply_kw,
+                                           grad_rows=b.grad_rows, grad_lin=b.grad_lin,
+                                           keep_sums=self.keep_grads)
         else:
             hip_ops.fm_embedding_grad(b.plan, F, E, gz, b.fm.sum_e, b.dx, sparse_rowmap,
                                       grad_rows=b.grad_rows, grad_lin=b.grad_lin)
@@ -482,7 +499,9 @@ class FusedCTRTrainer:
             grad_rows, grad_lin = self._exchange(b)
             plan = b.gplan
         t = self._mark("adam")
-        if self.deferred:
+        if fused:
+            pass  # applied inside the segmented sums above
+        elif self.deferred:
             hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                        plan, step_hint, self.step_table, self.betas,
                                        self.eps, self.weight_decay, grad_rows=grad_rows,

@@ -166,6 +166,7 @@ def fused_grads(tr):
     """A FusedCTRTrainer's last-step gradients, densified on the host:
     (E grad [V,K], w grad [V,1] or None, {dense name: grad})."""
     import torch
+    assert getattr(tr, "keep_grads", True), "set tr.keep_grads = True before stepping"
     b = tr._bufs
     U = b.plan.num_unique_host()
     rows = b.plan.unique_rows[:U].long()

@@ -41,6 +41,7 @@ def test_fused_fm_two_steps_vs_reference(cuda, golden, tag):
     g = golden("g_fm.npz")
     m = _fm_from_golden(g, tag, cuda)
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
+    tr.keep_grads = True  # fused_grads reads the per-row sums
     bd = {n: AdamBound(g[f"{tag}_{n}0"], 1e-3, 1e-5) for n in ("E", "w", "b")}
     for s in range(2):
         x = torch.tensor(g[f"{tag}_x{s}"], device=cuda)
@@ -98,6 +99,7 @@ def test_fused_deepfm_two_steps_vs_reference(cuda, golden):
     g = golden("g_deepfm.npz")
     m = _deepfm_from_golden(g, cuda)
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
+    tr.keep_grads = True  # fused_grads reads the per-row sums
     bd = {k: AdamBound(g[f"init/{k}"], 1e-3, 1e-5) for k in O.DEEPFM_KEYS}
     for s in range(2):
         loss = tr.step(torch.tensor(g[f"x{s}"], device=cuda), torch.tensor(g[f"y{s}"], device=cuda))
@@ -415,6 +417,7 @@ def test_fused_ipnn_two_steps_vs_reference(cuda, golden):
     g = golden("g_ipnn.npz")
     m = _ipnn_from_golden(g, cuda)
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
+    tr.keep_grads = True  # fused_grads reads the per-row sums
     bd = {k: AdamBound(g[f"init/{k}"], 1e-3, 1e-5) for k in O.IPNN_KEYS}
     for s in range(2):
         loss = tr.step(torch.tensor(g[f"x{s}"], device=cuda), torch.tensor(g[f"y{s}"], device=cuda))
@@ -507,6 +510,7 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B, F):
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     cond = O.grad_condition(kind, params_cpu, torch.tensor(x), torch.tensor(y))
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5)
+    tr.keep_grads = True  # fused_grads reads the per-row sums
     loss = tr.step(torch.tensor(x, device=cuda), torch.tensor(y, device=cuda)).item()
     opt = O.make_optimizer(params_cpu, 1e-3, 1e-5)
     lref = O.train_step(kind, params_cpu, opt, torch.tensor(x), torch.tensor(y), drop_p=0.0)

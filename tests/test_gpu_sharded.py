@@ -139,6 +139,7 @@ def test_sharded_world2_matches_global_batch(cuda, kind, drop, V, F, K, B):
     from oracle import ctr_oracle as O
     m = _model(kind, V, F, K, drop=drop)
     tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3)
+    tr.keep_grads = True  # fused_grads reads the per-row sums
     sd = m.state_dict()
     bd = {k: AdamBound(v.cpu().numpy(), 1e-3, 1e-5) for k, v in sd.items()}
     ref_losses = []
