@@ -305,6 +305,92 @@ __global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
   }
 }
 
+// The same catch-up with one LANE per slot for the ownership / staleness test and the
+// replay done by lane groups over a compacted per-wave list: the test for all 64 slots of a
+// wave issues together (idx -> owner -> last, three dependent loads for 64 slots at once
+// instead of for one slot per K4-lane group), then the wave's stale owned rows — a fraction
+// of its slots — are dealt to its 64/K4 lane groups, UNR rows per group at a time with
+// every load of the batch issued before the replay. Same adam_elem chain: bitwise the
+// per-slot kernel above.
+template <typename IdxT, int K4, int UNR>
+__global__ __launch_bounds__(256) void deferred_catchup_wave(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
+    int32_t* __restrict__ last, const IdxT* __restrict__ idx, int64_t S, int64_t V,
+    const int32_t* __restrict__ owner, const int32_t* __restrict__ step_ptr,
+    const float* __restrict__ tab, AdamHP h) {
+  constexpr int RPI = kWave / K4;  // lane groups (rows in flight per batch step) per wave
+  __shared__ int32_t s_row[4][kWave];
+  __shared__ int32_t s_from[4][kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = threadIdx.x / kWave;
+  const int g = lane / K4, c = lane % K4;
+  const int step = *step_ptr;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x / kWave) + wib) * kWave; base < S;
+       base += nwaves * kWave) {
+    const int64_t s = base + lane;
+    bool need = false;
+    int32_t r = 0, from = 0;
+    if (s < S) {
+      r = (int32_t)load_row(idx, s, V, nullptr);
+      if (owner[r] == (int32_t)s) {
+        from = last[r];
+        need = from < step;
+      }
+    }
+    const uint64_t mask = __ballot(need);
+    const int n = __popcll(mask);
+    if (need) {
+      const int pos = __popcll(mask & ((1ull << lane) - 1));
+      s_row[wib][pos] = r;
+      s_from[wib][pos] = from;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int j0 = 0; j0 < n; j0 += RPI * UNR) {
+      float4 pp[UNR], mm[UNR], vv[UNR];
+      int32_t rr[UNR], ff[UNR];
+      int fmin = step;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int j = j0 + u * RPI + g;
+        rr[u] = j < n ? s_row[wib][j] : -1;
+        ff[u] = j < n ? s_from[wib][j] : step;
+        fmin = min(fmin, ff[u]);
+        if (rr[u] >= 0) {
+          const int64_t e = (int64_t)rr[u] * K4 + c;
+          pp[u] = E[e]; mm[u] = mE[e]; vv[u] = vE[e];
+        }
+      }
+      for (int t = fmin + 1; t <= step; ++t) {
+        load_step(h, tab, t);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (t > ff[u]) adam_vec(pp[u], z4, mm[u], vv[u], h);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (rr[u] < 0) continue;
+        const int64_t e = (int64_t)rr[u] * K4 + c;
+        E[e] = pp[u]; mE[e] = mm[u]; vE[e] = vv[u];
+        if (c == 0) {
+          if (w) {
+            float pw = w[rr[u]], mws = mw[rr[u]], vws = vw[rr[u]];
+            for (int t = ff[u] + 1; t <= step; ++t) {
+              load_step(h, tab, t);
+              adam_elem(pw, 0.f, mws, vws, h);
+            }
+            w[rr[u]] = pw; mw[rr[u]] = mws; vw[rr[u]] = vws;
+          }
+          last[rr[u]] = step;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the list is re-filled by the next iteration
+  }
+}
+
 // Device step counters of a trainer: ctr[0] = completed steps, ctr[1] = the step in flight.
 // Within a step, ctr[0] stays at t-1 (catch-up, sweep and dropout read it) and ctr[1] = t
 // (the Adam apply reads it), so work on several streams never sees the counter move.
@@ -783,9 +869,10 @@ extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_
                        static_cast<const int32_t*>(idx), S, V, owner);
   CTR_LAUNCH_CHECK("deferred_mark_kernel");
   const int K4 = K / 4;
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(S * K4, 256), 8192);
+  // one lane per slot: S / 256 blocks of 4 waves (a wave re-loops when S exceeds the grid)
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(S, 256), 8192));
 #define CTR_CATCHUP(IT, K4_)                                                                   \
-  hipLaunchKernelGGL((deferred_catchup_ids_vec<IT, K4_>), grid, 256, 0, st,                    \
+  hipLaunchKernelGGL((deferred_catchup_wave<IT, K4_, 2>), grid, 256, 0, st,                    \
                      reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \
                      reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                \
                      static_cast<const IT*>(idx), S, V, owner, step_ptr, step_table, h)
@@ -806,7 +893,7 @@ extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_
   }
 #undef CTR_CATCHUP_K
 #undef CTR_CATCHUP
-  CTR_LAUNCH_CHECK("deferred_catchup_ids_vec");
+  CTR_LAUNCH_CHECK("deferred_catchup_wave");
   return CTR_OK;
 }
 

@@ -506,13 +506,15 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
         pl_valid(ti, a_rc, b_rc))
       return mk(ti, sp);
   }
-  // measured on MI355X (tools/gemm_planes_bench.py --sweep, profiles/r02_gemm_planes_sweep.jsonl):
+  // measured on MI355X (tools/gemm_planes_bench.py --sweep, profiles/r02_gemm_planes_sweep.jsonl;
+  // fwd1 (N = 200) 14.6 us on 17 vs 16.2 on 8, dX (N = 1664) 70.7 on 19 vs 74.3 on 7):
   // large-M products with a narrow N (the forward) on the 8-wave 64x160 tiling, large-M
   // products with a k-strided B (the dH1 / dX backward) on 64x64 x3 blocks per CU, the
   // transposed weight gradients (both operands k-strided, long K) on 64x64 with split-K
   // sized to ~2 blocks per CU
-  if (!a_rc && !b_rc && M >= 2048 && N > 192 && N <= 320) return mk(8, 1);
-  if (!a_rc && !b_rc && M >= 2048 && N <= 192) return mk(17, 1);
+  if (!a_rc && !b_rc && M >= 2048 && N > 256 && N <= 320) return mk(8, 1);
+  if (!a_rc && !b_rc && M >= 2048 && N <= 256) return mk(17, 1);
+  if (!a_rc && b_rc && M >= 2048 && N >= 1024) return mk(19, 1);
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
   if (a_rc && b_rc && Kp >= 2048) {
     const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
