@@ -529,6 +529,32 @@ def test_full_size_step_vs_oracle(cuda, kind, V, K, B, F):
     for k, v in dense.items():
         tol[k] = assert_grad_close(v, params_cpu[k].grad.numpy(), err_msg=f"grad {k}")
     sd = m.state_dict()
+    # untouched rows: the oracle's gradient is exactly 0, Adam sees g = wd * p — m and v
+    # must be bit-identical to torch's; p within one ulp of p plus 8 ulps of the Adam step
+    # (the step uses the ~1-ulp hardware sqrt / rcp and a reciprocal-multiply where torch
+    # divides: a few ulps of the step, csrc/adam_common.h adam_elem)
+    untouched = np.setdiff1d(sample, np.unique(x))
+    ui = torch.tensor(untouched)
+    st = {n: opt.state[params_cpu[n]] for n in ("feature_embedding.weight", "linear.weight")
+          if n in tol}
+    ours_mv = {"feature_embedding.weight": (tr.m_E, tr.v_E), "linear.weight": (tr.m_w, tr.v_w)}
+    for n, sn in st.items():
+        mo, vo = ours_mv[n]
+        mo = mo[ui.to(cuda)].cpu().reshape(sn["exp_avg"][ui].shape)
+        vo = vo[ui.to(cuda)].cpu().reshape(sn["exp_avg_sq"][ui].shape)
+        assert torch.equal(mo, sn["exp_avg"][ui]), f"{n}: m of untouched rows"
+        assert torch.equal(vo, sn["exp_avg_sq"][ui]), f"{n}: v of untouched rows"
+        po = sd[n][ui.to(cuda)].cpu()
+        pr = params_cpu[n].detach()[ui]
+        p00 = torch.tensor(p0[n] if n not in ("feature_embedding.weight", "linear.weight")
+                           else p0[n])[np.searchsorted(sample, untouched)]
+        inf = torch.tensor(float("inf"))
+        ulp = lambda t: torch.nextafter(t.abs(), inf) - t.abs()  # noqa: E731
+        stp = (pr - p00).abs()
+        bound = ulp(pr) + 8 * ulp(stp)
+        excess = ((po - pr).abs() / bound).max().item()
+        print(f"[parity] {n} untouched p: max |dp| / (ulp(p) + 8 ulp(step)) = {excess:.3g}")
+        assert excess <= 1.0, f"{n}: p of untouched rows beyond ulp(p) + 8 ulp(step)"
     for k in tol:
         row = k in ("feature_embedding.weight", "linear.weight")
         ours = (sd[k][idx.to(cuda)] if row else sd[k]).cpu().numpy()
