@@ -86,11 +86,14 @@ def gather_bytes(S, K, B, deep):
     return S * (8 + 4 * K + 4) + B * 4 * K + (S * 4 * K if deep else 0) + B * 16
 
 
-def scatter_bytes(S, K, U, deep):
+def scatter_bytes(S, K, U, deep, apply=False):
     """fm_embedding_grad: per slot its plan entries (12 B) and example terms (4 B gz +
     4K B sum_e), for DeepFM the MLP-input gradient row (4K B); per unique row the table
-    row read, the gradient row written (4K B each) and the linear grad (4 B)."""
-    return S * (12 + 4 + 4 * K + (4 * K if deep else 0)) + U * (8 * K + 8)
+    row read, the gradient row written (4K B each) and the linear grad (4 B). apply (the
+    fused deferred-Adam apply of N = 1, ctr_fm_embedding_grad_adam): per unique row also
+    read + write p, m, v of the row and of its linear weight (24 (K + 1) B) and last[]."""
+    return (S * (12 + 4 + 4 * K + (4 * K if deep else 0)) + U * (8 * K + 8)
+            + (U * (24 * (K + 1) + 8) if apply else 0))
 
 
 def plan_bytes(S, U):
@@ -302,6 +305,36 @@ def bench_pg(args, cfg, world, rank, dev):
         dist.destroy_process_group()
 
 
+def load_mfma_busy():
+    """Matrix-pipe busy fraction of the six MLP GEMMs (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES
+    over the SIMD-cycles of each launch, standalone; profiles/*gemm_mfma_busy.json from
+    tools/gemm_planes_pmc.sh), weighted by each launch's cycles."""
+    for p in sorted((ROOT / "profiles").glob("*gemm_mfma_busy.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())["shapes"]
+            busy = sum(v["mfma_busy_cycles"] for v in d.values())
+            simd = sum(1024 * v["grbm_gui_active"] / 8 for v in d.values())
+            return busy / simd, f"profiles/{p.name}"
+        except Exception:
+            continue
+    return None
+
+
+def load_crosscal(config: str):
+    """The oracle's CPU step time over the reference's own, measured side by side in the
+    build container (tools/cpu_crosscal.py -> profiles/*cpu_crosscal.json)."""
+    for p in sorted((ROOT / "profiles").glob("*cpu_crosscal.json"), reverse=True):
+        try:
+            d = json.loads(p.read_text())
+            c = d["configs"][config]
+            return {"oracle_over_reference": c["oracle_over_reference"],
+                    "within_10pct": c["within_10pct"], "threads": d["threads"],
+                    "host": d["cpu_model"], "source": f"profiles/{p.name}"}
+        except Exception:
+            continue
+    return None
+
+
 def load_traffic(config: str, kernel: str):
     """HBM bytes per launch of the dominant kernel from the committed PMC summary (rocprofv3
     FETCH_SIZE/WRITE_SIZE passes with the gfx950 corrections, profiles/)."""
@@ -404,6 +437,10 @@ def main():
     torch.cuda.synchronize()
     bd, trainer.timing = trainer.timing, None
     per_step = {k: total_ms(v) / n_bd for k, v in bd.items()}
+    # N = 1 deferred: the embedding Adam apply runs inside the scatter's combine pass
+    fused_apply = (world == 1 and args.optimizer == "deferred" and isinstance(
+        trainer, FusedCTRTrainer) and not isinstance(trainer, ShardedCTRTrainer)
+        and trainer.fuse_apply and trainer._vec_ok)
     dominant = max(("adam", "gather", "plan", "scatter", "gemm", "flush"),
                    key=lambda k: per_step[k])
 
@@ -477,6 +514,9 @@ def main():
                                  "2500 TF bf16 dense",
                     "bf16_mfma_frac": 6.0 * achieved / MFMA_BF16_PEAK_TFS,
                     "algorithmic_flops_per_launch": flops}
+        busy = load_mfma_busy()
+        if busy is not None:
+            roofline["mfma_busy"], roofline["mfma_busy_source"] = busy
         traffic, src = load_traffic(args.config, "gemm")
     else:
         if dominant == "adam":
@@ -493,8 +533,10 @@ def main():
         elif dominant == "gather":
             nbytes, kname = gather_bytes(S, K, B, deep), "fm_forward_vec (embedding gather + FM)"
         elif dominant == "scatter":
-            nbytes = scatter_bytes(S, K, U, deep)
-            kname = "seg_chunk_kernel + seg_combine_kernel (per-row gradient sums)"
+            nbytes = scatter_bytes(S, K, U, deep, apply=fused_apply)
+            kname = ("seg_chunk_kernel + seg_combine_apply_kernel (per-row gradient sums with "
+                     "the deferred Adam apply fused)" if fused_apply else
+                     "seg_chunk_kernel + seg_combine_kernel (per-row gradient sums)")
         else:
             nbytes = plan_bytes(S, U)
             kname = "sparse plan (keys + radix sort + scan + scatter)"
@@ -531,16 +573,23 @@ def main():
         "gather_scatter": {
             "gather_kernel": "fm_forward_vec", "gather_ms": gather_ms,
             "gather_GBps": gather_bytes(S, K, B, deep) / (gather_ms * 1e-3) / 1e9,
-            "scatter_kernels": "seg_chunk_kernel + seg_combine_kernel (per-row sums; the "
-                               "sparse plan is timed separately under kernels)",
+            "scatter_kernels": ("seg_chunk_kernel + seg_combine_apply_kernel (per-row sums "
+                                "and the fused deferred-Adam apply of the batch's rows"
+                                if fused_apply else
+                                "seg_chunk_kernel + seg_combine_kernel (per-row sums") +
+                               "; the sparse plan is timed separately under kernels)",
             "scatter_ms": scatter_ms,
-            "scatter_GBps": scatter_bytes(S, K, U, deep) / (scatter_ms * 1e-3) / 1e9,
+            "scatter_GBps": scatter_bytes(S, K, U, deep, apply=fused_apply)
+            / (scatter_ms * 1e-3) / 1e9,
             "unique_rows_per_batch": U, "slots_per_batch": S},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(cfg, host_batches)
+        cc = load_crosscal(args.config)
+        if cc is not None:  # how the port's CPU time compares with the reference's own
+            result["cpu_baseline"]["cross_calibration"] = cc
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
