@@ -42,9 +42,6 @@ class ShardedCTRTrainer(FusedCTRTrainer):
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None):
-        if not hasattr(model, "linear"):
-            raise NotImplementedError("row sharding drives FM / DeepFM; train InnerPNN with "
-                                      "FusedCTRTrainer (replicated tables)")
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:
@@ -82,7 +79,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if y.dtype != torch.float32:
             y = y.float()
         y = y.contiguous()
-        bias, gv = self.views["bias"], self.grad_views
+        bias, gv = self.views.get("bias"), self.grad_views
+        has_lin = self.w_tab is not None  # InnerPNN: no linear table
 
         self._sync_weight_planes()
         # 1. plan of the local batch, per-owner counts of its unique rows
@@ -106,9 +104,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._fork_sweep()
         t = self._mark("exchange")
         rows = hip_ops.embedding_gather(self.E_tab, req)
-        lin = hip_ops.embedding_gather(self.w_tab, req)
         T = alltoallv(rows, recv_c, send_c, self.group)
-        T_lin = alltoallv(lin, recv_c, send_c, self.group).view(-1)
+        T_lin = None
+        if has_lin:
+            lin = hip_ops.embedding_gather(self.w_tab, req)
+            T_lin = alltoallv(lin, recv_c, send_c, self.group).view(-1)
         self._span("exchange", t)
         # 4. forward + backward over the compact table
         ids = b.plan.slot_to_unique(out=self._slot2u)[:B * F].view(B, F)
@@ -123,8 +123,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         t = self._mark("scatter")
-        hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
-                                  grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
+        if self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
+            hip_ops.segment_sum_rows(b.plan, b.dslot, out=b.grad_rows)
+        else:
+            hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
+                                      grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
         self._span("scatter", t)
         if self.kind != "FM":  # the dense-parameter gradients, on the weight-gradient stream
             self._weight_grads(b, gz)
@@ -133,7 +136,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 5. gradients to the owners, summed per row in (source rank, position) order
         t = self._mark("exchange")
         G = alltoallv(b.grad_rows, send_c, recv_c, self.group)
-        G_lin = alltoallv(b.grad_lin, send_c, recv_c, self.group)
+        G_lin = alltoallv(b.grad_lin, send_c, recv_c, self.group) if has_lin else None
         self._join_wgrad()
         allreduce_sum_(self.flat_grad, self.group)
         if ws > 1:
@@ -142,14 +145,16 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("exchange", t)
         t = self._mark("scatter")
         b.gplan.build(req, self.V_tab)
-        hip_ops.segment_sum_rows(b.gplan, G, G_lin, rowmap=None, out=b.g_rows, out_lin=b.g_lin)
+        hip_ops.segment_sum_rows(b.gplan, G, G_lin, rowmap=None, out=b.g_rows,
+                                 out_lin=b.g_lin if has_lin else None)
         self._span("scatter", t)
         self.step_count += 1
         t = self._mark("adam")
         hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
                                    self.v_w, self.last, b.gplan, self.step_count,
                                    self.step_table, self.betas, self.eps, self.weight_decay,
-                                   grad_rows=b.g_rows, grad_lin=b.g_lin, step_dev=self.step_cur)
+                                   grad_rows=b.g_rows, grad_lin=b.g_lin if has_lin else None,
+                                   step_dev=self.step_cur)
         self._span("adam", t)
         self._dirty = True
         self._adam_dense(self.step_count)
@@ -157,27 +162,26 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.step_end(self.step_ctr)
         return b.loss
 
-    def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor]:
-        """Full (E [V,K], w [V,1]) assembled from every rank's shard (after a flush)."""
+    def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor | None]:
+        """Full (E [V,K], w [V,1] or None for InnerPNN) assembled from every rank's shard
+        (after a flush)."""
         self.flush()
         E = self.model.feature_embedding.weight.data
-        w = self.model.linear.weight.data
+        w = self.model.linear.weight.data if self.w_tab is not None else None
         if self.world_size == 1:
-            return E.clone(), w.clone()
-        pad = self.shard_rows * self.world_size
-        outE = torch.empty(pad, self.K, dtype=E.dtype, device=E.device)
-        outw = torch.empty(pad, 1, dtype=w.dtype, device=w.device)
-        sendE = torch.zeros(self.shard_rows, self.K, dtype=E.dtype, device=E.device)
-        sendw = torch.zeros(self.shard_rows, 1, dtype=w.dtype, device=w.device)
-        sendE[:self.V_tab] = self.E_tab
-        sendw[:self.V_tab] = self.w_tab
-        if E.is_cuda and dist.get_backend(self.group) == "gloo":
-            oE, ow = outE.cpu(), outw.cpu()
-            dist.all_gather_into_tensor(oE, sendE.cpu(), group=self.group)
-            dist.all_gather_into_tensor(ow, sendw.cpu(), group=self.group)
-            outE.copy_(oE)
-            outw.copy_(ow)
-        else:
-            dist.all_gather_into_tensor(outE, sendE, group=self.group)
-            dist.all_gather_into_tensor(outw, sendw, group=self.group)
-        return outE[:self.V], outw[:self.V]
+            return E.clone(), (w.clone() if w is not None else None)
+
+        def gather(tab, width):
+            out = torch.empty(self.shard_rows * self.world_size, width, dtype=tab.dtype,
+                              device=tab.device)
+            send = torch.zeros(self.shard_rows, width, dtype=tab.dtype, device=tab.device)
+            send[:self.V_tab] = tab.view(self.V_tab, width)
+            if tab.is_cuda and dist.get_backend(self.group) == "gloo":
+                o = out.cpu()
+                dist.all_gather_into_tensor(o, send.cpu(), group=self.group)
+                out.copy_(o)
+            else:
+                dist.all_gather_into_tensor(out, send, group=self.group)
+            return out[:self.V]
+
+        return gather(self.E_tab, self.K), (gather(self.w_tab, 1) if w is not None else None)

@@ -65,8 +65,8 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sparse_exchange_world2_gloo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_sparse_exchange_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -94,10 +94,11 @@ def test_sparse_exchange_world2_gloo():
         np.testing.assert_array_equal(u, gu)
         np.testing.assert_allclose(s, gs, rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(l_, gl, rtol=1e-5, atol=1e-5)
-        assert flat0 == 3.0  # 1 + 2
-    # both ranks received the same concatenation (rank order), so their re-sums agree bitwise
-    np.testing.assert_array_equal(res[0][3], res[1][3])
-    np.testing.assert_array_equal(res[0][1], res[1][1])
+        assert flat0 == world * (world + 1) / 2  # sum of rank + 1
+    # every rank received the same concatenation (rank order), so the re-sums agree bitwise
+    for rank in range(1, world):
+        np.testing.assert_array_equal(res[0][3], res[rank][3])
+        np.testing.assert_array_equal(res[0][1], res[rank][1])
 
 
 # ------------------------------------------------------------ row-sharded exchange ----
@@ -137,8 +138,9 @@ def _shard_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_row_sharded_exchange_world3_gloo():
-    world = 3
+@pytest.mark.parametrize("world", [3, 8])
+def test_row_sharded_exchange_gloo(world):
+    """The row-sharded protocol at world sizes 3 and 8 (the target node: 8 x MI355X)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -31,17 +31,20 @@ def _model(kind, V, F, K, seed=4, drop=0.0):
     import rl_ctr_prediction_amd as P
     torch.manual_seed(seed)
     with torch.device("cuda:0"):
-        m = P.FM(V, K) if kind == "FM" else P.DeepFM(V, F, K)
+        m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
+             "IPNN": lambda: P.InnerPNN(V, F, K)}[kind]()
     for mod in m.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = drop
     with torch.no_grad():
         m.feature_embedding.weight.mul_(0.05)
-        m.linear.weight.mul_(0.05)
+        if kind != "IPNN":
+            m.linear.weight.mul_(0.05)
     return m
 
 
-@pytest.mark.parametrize("kind,V,K,B", [("FM", 40_000, 16, 1024), ("DeepFM", 200_000, 32, 2048)])
+@pytest.mark.parametrize("kind,V,K,B", [("FM", 40_000, 16, 1024), ("DeepFM", 200_000, 32, 2048),
+                                        ("IPNN", 200_000, 32, 2048)])
 def test_sharded_world1_equals_fused_bitwise(cuda, kind, V, K, B):
     import rl_ctr_prediction_amd as P
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
@@ -95,14 +98,14 @@ def _rank_main(rank, world, port, kind, V, F, K, B, steps, q, drop=0.0):
                  if k not in ("feature_embedding.weight", "linear.weight")}
         # numpy, pickled by value: a torch tensor would travel as a shared-memory fd that the
         # parent can only open while this process is still alive
-        q.put((rank, losses, E.cpu().numpy(), w.cpu().numpy(), dense))
+        q.put((rank, losses, E.cpu().numpy(), None if w is None else w.cpu().numpy(), dense))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("kind,drop,V,F,K,B", [
     ("FM", 0.0, 30_000, 26, 16, 512), ("DeepFM", 0.0, 30_000, 26, 16, 512),
-    ("DeepFM", 0.2, 30_000, 26, 16, 512),
+    ("DeepFM", 0.2, 30_000, 26, 16, 512), ("IPNN", 0.0, 30_000, 26, 16, 512),
     # C5's row shape (Avazu 22 fields, dim 128): both shards own hot rows
     ("FM", 0.0, 200_000, 22, 128, 1024)])
 def test_sharded_world2_matches_global_batch(cuda, kind, drop, V, F, K, B):
@@ -150,7 +153,9 @@ def test_sharded_world2_matches_global_batch(cuda, kind, drop, V, F, K, B):
                                   torch.tensor(y, device=cuda)).item())
         gE, gw, dense = fused_grads(tr)
         n = np.bincount(np.asarray(x).reshape(-1), minlength=V)
-        grads = dict(dense, **{"feature_embedding.weight": gE, "linear.weight": gw})
+        grads = dict(dense, **{"feature_embedding.weight": gE})
+        if gw is not None:
+            grads["linear.weight"] = gw
         for k, g in grads.items():
             c = cond.get(k)
             bd[k].step(g, grad_bound(g, cond=None if c is None else c.numpy(),
@@ -162,7 +167,9 @@ def test_sharded_world2_matches_global_batch(cuda, kind, drop, V, F, K, B):
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
         bd["feature_embedding.weight"].check(E, sd["feature_embedding.weight"].cpu().numpy(),
                                              err_msg=f"E rank {rank}")
-        bd["linear.weight"].check(w, sd["linear.weight"].cpu().numpy(), err_msg=f"w rank {rank}")
+        if w is not None:
+            bd["linear.weight"].check(w, sd["linear.weight"].cpu().numpy(),
+                                      err_msg=f"w rank {rank}")
         for k, v in dense.items():
             bd[k].check(v, sd[k].cpu().numpy(), err_msg=f"{k} rank {rank}")
     # the replicated dense parameters are bitwise identical across ranks
