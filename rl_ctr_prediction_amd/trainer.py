@@ -153,6 +153,11 @@ class FusedCTRTrainer:
         # fused scatter + Adam apply (one process, deferred mode); keep_grads keeps every
         # row's gradient sum in b.grad_rows / b.grad_lin (tests read them)
         self.fuse_apply = True
+        # capture order of the step's first fork: the plan first where it is the critical
+        # path (FM: the forward / backward are short; C2 31.6 vs 28.4 M ex/s), the catch-up
+        # and forward first where they are (MLP kinds; C3 12.39 vs 11.67 M ex/s)
+        env = os.environ.get("CTR_PLAN_FIRST")
+        self.plan_first = (env == "1") if env in ("0", "1") else self.kind == "FM"
         self.keep_grads = False
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
@@ -432,19 +437,26 @@ class FusedCTRTrainer:
             main = torch.cuda.current_stream()
             ev0 = torch.cuda.Event()
             ev0.record(main)  # x ready; previous step's plan users and Adam done
+
+            def plan():
+                self._side.wait_event(ev0)
+                if not torch.cuda.is_current_stream_capturing():
+                    x.record_stream(self._side)
+                with torch.cuda.stream(self._side):
+                    t_plan = self._mark("plan")
+                    b.plan.build(x, self.V)
+                    self._span("plan", t_plan)
+
+            if self.plan_first:
+                plan()
             t = self._mark("adam")
             hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
                                               self.last, x, self.rowmap, self.step_done,
                                               self.step_table, step_hint, self.betas,
                                               self.eps, self.weight_decay)
             self._span("adam", t)
-            self._side.wait_event(ev0)
-            if not torch.cuda.is_current_stream_capturing():
-                x.record_stream(self._side)
-            with torch.cuda.stream(self._side):
-                t_plan = self._mark("plan")
-                b.plan.build(x, self.V)
-                self._span("plan", t_plan)
+            if not self.plan_first:
+                plan()
             self._fork_sweep()
         else:
             t_plan = self._mark("plan")
