@@ -440,7 +440,7 @@ def main():
     # N = 1 deferred: the embedding Adam apply runs inside the scatter's combine pass
     fused_apply = (world == 1 and args.optimizer == "deferred" and isinstance(
         trainer, FusedCTRTrainer) and not isinstance(trainer, ShardedCTRTrainer)
-        and trainer.fuse_apply and trainer._vec_ok)
+        and trainer.fuse_apply and trainer._vec_ok and trainer.K >= 32)
     dominant = max(("adam", "gather", "plan", "scatter", "gemm", "flush"),
                    key=lambda k: per_step[k])
 

@@ -213,10 +213,11 @@ __global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
 }
 
 // The combine pass with the deferred Adam apply fused in (float4): a wave takes G = 64/LPR
-// consecutive unique rows. Rows inside one chunk (their sum already in `out`, from
-// seg_chunk) are applied by their own lane group, all G at once; then each row of the G
-// that spans chunks is summed by the whole wave exactly as seg_combine_kernel sums it (same
-// partial order, same butterfly: bitwise the same sums) and applied by lane group 0. One
+// consecutive unique rows. Each of the G rows that spans chunks is first summed by the
+// whole wave exactly as seg_combine_kernel sums it (same partial order, same butterfly:
+// bitwise the same sums) into a wave-private LDS slot; then every lane group applies its
+// own row — the sum from seg_chunk's `out` for a row inside one chunk, from the LDS slot
+// for a spanning one — so the G applies (the memory-heavy part) run side by side. One
 // launch for what the combine and ctr_adam_deferred_rows did in two, and the spanning
 // rows' sums never make the round trip through `out`.
 template <int LPR>
@@ -224,7 +225,10 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
   using VT = float4;
   constexpr int kChunk = seg_chunk<LPR>();
   constexpr int G = kWave / LPR;
+  __shared__ VT s_sum[4][kWave];      // [wave][row of the G * lane group column]
+  __shared__ float s_lin[4][G];
   const int lane = threadIdx.x & (kWave - 1);
+  const int wib = threadIdx.x / kWave;
   const int g = lane / LPR, c = lane % LPR;
   const bool col = c < a.KV;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
@@ -232,18 +236,6 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
   const int step = *a.step_ptr;
   for (int64_t u0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave) * G; u0 < U;
        u0 += waves * G) {
-    {  // rows inside one chunk: one lane group each
-      const int64_t u = u0 + g;
-      if (u < U) {
-        const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
-        if (off0 / kChunk == (off1 - 1) / kChunk) {
-          const VT gr = col ? static_cast<const VT*>(a.out)[u * a.KV + c] : VOps<VT>::zero();
-          const float gl = a.out_lin ? a.out_lin[u] : 0.f;
-          deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV,
-                             c, col, gr, gl, step, a.tab, a.hp);
-        }
-      }
-    }
     for (int j = 0; j < G && u0 + j < U; ++j) {  // rows spanning chunks: the whole wave
       const int64_t u = u0 + j;
       const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
@@ -264,10 +256,29 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
       }
       if (g == 0) {
         if (a.out_keep) seg_emit<VT>(a, u, c, col, acc, accl);
-        deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV,
-                           c, col, acc, accl, step, a.tab, a.hp);
+        s_sum[wib][j * LPR + c] = acc;
+        if (c == 0) s_lin[wib][j] = accl;
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave-private slots are written
+    __builtin_amdgcn_wave_barrier();
+    const int64_t u = u0 + g;  // every lane group applies its own row
+    if (u < U) {
+      const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
+      const bool inside = off0 / kChunk == (off1 - 1) / kChunk;
+      VT gr;
+      float gl;
+      if (inside) {
+        gr = col ? static_cast<const VT*>(a.out)[u * a.KV + c] : VOps<VT>::zero();
+        gl = a.out_lin ? a.out_lin[u] : 0.f;
+      } else {
+        gr = s_sum[wib][g * LPR + c];
+        gl = s_lin[wib][g];
+      }
+      deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV, c,
+                         col, gr, gl, step, a.tab, a.hp);
+    }
+    __builtin_amdgcn_wave_barrier();  // the slots are re-filled by the next iteration
   }
 }
 

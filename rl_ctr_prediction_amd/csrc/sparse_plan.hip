@@ -4,7 +4,7 @@
 // rows in ascending order and their segment offsets — bit-identical to numpy's stable
 // argsort + unique (tests/test_gpu_kernels.py).
 //
-// LSD radix sort, 8-bit digits, ceil(log2 V / 8) passes, two launches per pass and no
+// LSD radix sort, 8- or 11-bit digits (plan_bits), two launches per pass and no
 // inter-workgroup hand-off inside a launch (a cross-XCD look-back chain costs ~1 us per hop
 // on gfx950; a kernel boundary ~1.5 us):
 //   radix_hist:    per tile (256 threads x IPT keys) the 256-bin digit histogram, LDS
@@ -22,10 +22,17 @@
 
 namespace ctr {
 
-constexpr int kRadixBits = 8;
-constexpr int kRadix = 1 << kRadixBits;
 constexpr int kSortThreads = 256;
 constexpr int kSortWaves = kSortThreads / kWave;
+
+// Digit width: 8 bits (256 bins) or 11 bits (2048 bins). The plan picks the width that
+// needs fewer passes for the key range (V = 1M: 20 bits = 3 x 8 or 2 x 11; V = 10M: 24 bits
+// = 3 x 8 = 3 x 11, so 8): one pass less is two launches less on a latency-bound path.
+template <int BITS>
+struct Radix {
+  static constexpr int kBins = 1 << BITS;
+  static constexpr int kDPT = kBins / kSortThreads;  // digits owned per thread (1 or 8)
+};
 
 struct RadixPass {
   const void* idx;     // pass 0: feature ids
@@ -35,7 +42,7 @@ struct RadixPass {
   const int32_t* vals_in;
   uint32_t* keys_out;
   int32_t* vals_out;
-  int32_t* hist;       // [n_tiles][256]
+  int32_t* hist;       // [n_tiles][bins]
   int64_t S;
   int n_tiles;
   int shift;
@@ -52,20 +59,21 @@ __device__ __forceinline__ uint32_t radix_key(const RadixPass& a, int64_t i, int
   return a.keys_in[i];
 }
 
-template <int IPT, bool FIRST>
+template <int IPT, bool FIRST, int BITS>
 __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(RadixPass a) {
-  __shared__ int32_t h[kRadix];
+  constexpr int R = Radix<BITS>::kBins;
+  __shared__ int32_t h[R];
   const int t = threadIdx.x;
-  h[t] = 0;
+  for (int d = t; d < R; d += kSortThreads) h[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * (kSortThreads * IPT);
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const int64_t e = base + i * kSortThreads + t;
-    if (e < a.S) atomicAdd(&h[(radix_key<FIRST>(a, e, a.err) >> a.shift) & (kRadix - 1)], 1);
+    if (e < a.S) atomicAdd(&h[(radix_key<FIRST>(a, e, a.err) >> a.shift) & (R - 1)], 1);
   }
   __syncthreads();
-  a.hist[(int64_t)blockIdx.x * kRadix + t] = h[t];
+  for (int d = t; d < R; d += kSortThreads) a.hist[(int64_t)blockIdx.x * R + d] = h[d];
 }
 
 // Exclusive scan of one value per thread over the 256-thread block (4 waves).
@@ -86,11 +94,19 @@ __device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t* wave
   return off + x - v;
 }
 
-template <int IPT, bool FIRST, bool LAST>
+// One pass of the stable LSD sort over one tile: the block scans the per-tile digit
+// histograms for its global digit bases (thread t owns the DPT consecutive digits
+// [t*DPT, (t+1)*DPT)), ranks its keys stably with wave ballots (BITS ballots give the
+// lanes holding the same digit; popcount below the lane = rank within the wave; the waves
+// before it and the item rows before it come from per-wave counts and a running count in
+// LDS; measured: the per-digit update below beats one LDS atomic per (wave, digit) group,
+// 13-16 vs 10-12 us per pass at C2), and scatters (key, value).
+template <int IPT, bool FIRST, bool LAST, int BITS>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a) {
-  __shared__ int32_t s_base[kRadix];               // global base of each digit for this tile
-  __shared__ int32_t s_run[kRadix];                // digits ranked so far in this tile
-  __shared__ int32_t s_wcnt[kSortWaves][kRadix];   // per-wave digit counts of one item row
+  constexpr int R = Radix<BITS>::kBins, DPT = Radix<BITS>::kDPT;
+  __shared__ int32_t s_base[R];               // global base of each digit for this tile
+  __shared__ int32_t s_run[R];                // digits ranked so far in this tile
+  __shared__ int32_t s_wcnt[kSortWaves][R];   // per-wave digit counts of one item row
   __shared__ int32_t s_wtot[kSortWaves];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
@@ -111,29 +127,44 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
     }
   }
 
-  // thread t owns digit t: total over all tiles and the part of the tiles before this one
-  int32_t tot = 0, before = 0;
+  // digits [t*DPT, (t+1)*DPT): totals over all tiles and the part of the tiles before this one
+  int32_t tot[DPT], before[DPT];
+#pragma unroll
+  for (int k = 0; k < DPT; ++k) tot[k] = before[k] = 0;
   {
-    const int32_t* hcol = a.hist + t;
-    int j = 0;
-    for (; j + 4 <= a.n_tiles; j += 4) {
-      const int32_t h0 = hcol[(int64_t)(j + 0) * kRadix], h1 = hcol[(int64_t)(j + 1) * kRadix];
-      const int32_t h2 = hcol[(int64_t)(j + 2) * kRadix], h3 = hcol[(int64_t)(j + 3) * kRadix];
-      tot += (h0 + h1) + (h2 + h3);
-      before += (j + 0 < tile ? h0 : 0) + (j + 1 < tile ? h1 : 0) + (j + 2 < tile ? h2 : 0) +
-                (j + 3 < tile ? h3 : 0);
-    }
-    for (; j < a.n_tiles; ++j) {
-      const int32_t h0 = hcol[(int64_t)j * kRadix];
-      tot += h0;
-      before += j < tile ? h0 : 0;
+    const int32_t* hcol = a.hist + t * DPT;
+    for (int j = 0; j < a.n_tiles; ++j) {
+      int32_t hv[DPT];
+      if constexpr (DPT % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < DPT; k += 4) {
+          const int4 q = *reinterpret_cast<const int4*>(hcol + (int64_t)j * R + k);
+          hv[k] = q.x; hv[k + 1] = q.y; hv[k + 2] = q.z; hv[k + 3] = q.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) hv[k] = hcol[(int64_t)j * R + k];
+      }
+#pragma unroll
+      for (int k = 0; k < DPT; ++k) {
+        tot[k] += hv[k];
+        before[k] += j < tile ? hv[k] : 0;
+      }
     }
   }
-  const int32_t digit_start = block_exclusive_scan(tot, s_wtot);
-  s_base[t] = digit_start + before;
-  s_run[t] = 0;
+  int32_t mine = 0;
 #pragma unroll
-  for (int j = 0; j < kSortWaves; ++j) s_wcnt[j][t] = 0;
+  for (int k = 0; k < DPT; ++k) mine += tot[k];
+  int32_t start = block_exclusive_scan(mine, s_wtot);
+#pragma unroll
+  for (int k = 0; k < DPT; ++k) {
+    s_base[t * DPT + k] = start + before[k];
+    s_run[t * DPT + k] = 0;
+    start += tot[k];
+  }
+  for (int d = t; d < R; d += kSortThreads)
+#pragma unroll
+    for (int j = 0; j < kSortWaves; ++j) s_wcnt[j][d] = 0;
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
@@ -142,10 +173,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
   for (int i = 0; i < IPT; ++i) {
     const int64_t e = base + i * kSortThreads + t;
     const bool ok = e < a.S;
-    const uint32_t d = (key[i] >> a.shift) & (kRadix - 1);
+    const uint32_t d = (key[i] >> a.shift) & (R - 1);
     uint64_t peers = __ballot(ok);
 #pragma unroll
-    for (int b = 0; b < kRadixBits; ++b) {
+    for (int b = 0; b < BITS; ++b) {
       const uint64_t m = __ballot((d >> b) & 1u);
       peers &= ((d >> b) & 1u) ? m : ~m;
     }
@@ -157,13 +188,18 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
     for (int j = 0; j < kSortWaves; ++j) off += j < w ? s_wcnt[j][d] : 0;
     pos[i] = ok ? s_base[d] + off : -1;
     __syncthreads();
-    int32_t add = 0;
+    // the running counts of this item row's digits (thread t owns digits t*DPT ...)
 #pragma unroll
-    for (int j = 0; j < kSortWaves; ++j) {
-      add += s_wcnt[j][t];
-      s_wcnt[j][t] = 0;
+    for (int k = 0; k < DPT; ++k) {
+      const int dd = t * DPT + k;
+      int32_t add = 0;
+#pragma unroll
+      for (int j = 0; j < kSortWaves; ++j) {
+        add += s_wcnt[j][dd];
+        s_wcnt[j][dd] = 0;
+      }
+      s_run[dd] += add;
     }
-    s_run[t] += add;
     __syncthreads();
   }
 #pragma unroll
@@ -295,7 +331,26 @@ static int key_bits(int64_t V) {
 
 // Items per thread: 8 (2048-key tiles) while that keeps the per-block histogram scan short
 // (<= 256 tiles); larger batches (data-parallel gathered plans) use 32 (8192-key tiles).
-static int plan_ipt(int64_t S) { return S <= 256 * 2048 ? 8 : 32; }
+static int plan_ipt(int64_t S) {
+  if (const char* env = getenv("CTR_PLAN_IPT")) {  // A/B runs
+    const int v = atoi(env);
+    if (v == 4 || v == 8 || v == 32) return v;
+  }
+  return S <= 256 * 2048 ? 8 : 32;
+}
+
+// digit width for a key range: 11 bits where that takes fewer passes than 8
+static int plan_bits(int64_t V) {
+  if (const char* env = getenv("CTR_PLAN_BITS")) {  // A/B runs
+    const int b = atoi(env);
+    if (b == 8 || b == 11) return b;
+  }
+  // measured on MI355X (C2: S = 106k, V = 1M): two 11-bit passes lose to three 8-bit ones —
+  // the 2048-bin scatter takes 22-25 us against 13-16 (tools/plan_ab.sh), more than the
+  // launch it saves; 11 bits stay available for A/B runs
+  (void)V;
+  return 8;
+}
 
 struct PlanLayout {
   uint32_t* keys[2];
@@ -319,36 +374,37 @@ static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
     L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
     L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
   }
-  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * kRadix * n_tiles));
+  // histograms sized for the widest digit (the plan's buffers do not know V)
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles));
   L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
   L->total = off;
   return off;
 }
 
-template <int IPT>
+template <int IPT, int BITS>
 static int run_passes(RadixPass a, int passes, const ctr_sparse_plan* plan, PlanLayout& L,
                       hipStream_t st) {
   const unsigned grid = (unsigned)a.n_tiles;
   for (int p = 0; p < passes; ++p) {
     const bool first = p == 0, last = p == passes - 1;
-    a.shift = p * kRadixBits;
+    a.shift = p * BITS;
     a.keys_in = first ? nullptr : L.keys[(p - 1) & 1];
     a.vals_in = first ? nullptr : L.vals[(p - 1) & 1];
     a.keys_out = last ? reinterpret_cast<uint32_t*>(plan->sorted_rows) : L.keys[p & 1];
     a.vals_out = last ? plan->sorted_slots : L.vals[p & 1];
     if (first)
-      hipLaunchKernelGGL((radix_hist_kernel<IPT, true>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_hist_kernel<IPT, true, BITS>), grid, kSortThreads, 0, st, a);
     else
-      hipLaunchKernelGGL((radix_hist_kernel<IPT, false>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_hist_kernel<IPT, false, BITS>), grid, kSortThreads, 0, st, a);
     CTR_LAUNCH_CHECK("radix_hist_kernel");
     if (first && last)
-      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, true>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, true, BITS>), grid, kSortThreads, 0, st, a);
     else if (first)
-      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, false>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, true, false, BITS>), grid, kSortThreads, 0, st, a);
     else if (last)
-      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, true>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, true, BITS>), grid, kSortThreads, 0, st, a);
     else
-      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, false>), grid, kSortThreads, 0, st, a);
+      hipLaunchKernelGGL((radix_scatter_kernel<IPT, false, false, BITS>), grid, kSortThreads, 0, st, a);
     CTR_LAUNCH_CHECK("radix_scatter_kernel");
   }
   return CTR_OK;
@@ -404,9 +460,17 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   a.S = S;
   a.n_tiles = (int)ceil_div(S, kSortThreads * ipt);
   a.err = err_flag;
-  const int passes = (int)ceil_div(key_bits(V), kRadixBits);
-  const int rc = ipt == 8 ? run_passes<8>(a, passes, plan, L, st)
-                          : run_passes<32>(a, passes, plan, L, st);
+  const int bits = plan_bits(V);
+  const int passes = (int)ceil_div(key_bits(V), bits);
+  int rc;
+  if (bits == 11)
+    rc = ipt == 4 ? run_passes<4, 11>(a, passes, plan, L, st)
+       : ipt == 8 ? run_passes<8, 11>(a, passes, plan, L, st)
+                  : run_passes<32, 11>(a, passes, plan, L, st);
+  else
+    rc = ipt == 4 ? run_passes<4, 8>(a, passes, plan, L, st)
+       : ipt == 8 ? run_passes<8, 8>(a, passes, plan, L, st)
+                  : run_passes<32, 8>(a, passes, plan, L, st);
   if (rc != CTR_OK) return rc;
   const unsigned gs = (unsigned)ceil_div(S, kSegTile);
   hipLaunchKernelGGL(seg_count_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,
