@@ -202,7 +202,9 @@ __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[
 // NS-deep LDS ring of 32-deep k stages; one barrier per stage; the DMA of stage t+NS-1 is
 // issued right after the barrier of stage t and stays in flight (counted vmcnt) under the
 // MFMAs of stages t .. t+NS-2.
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool A_RC, bool B_RC, int NS>
+// KS: 32-deep MFMA k-steps per ring stage (1 or 2): KS = 2 halves the barriers per k
+// (the guide's BK 32 -> 64) at twice the LDS per stage.
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool A_RC, bool B_RC, int NS, int KS = 1>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(PlanesArgs a) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -211,9 +213,12 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   static_assert(!A_RC || BM == 64 || BM == 128, "RC operand tiles of 64 or 128");
   static_assert(!B_RC || BN == 64 || BN == 128, "RC operand tiles of 64 or 128");
   static_assert(NS >= 2 && NS <= 7, "2- to 7-deep LDS ring");
+  static_assert(KS == 1 || KS == 2, "1 or 2 MFMA k-steps per stage");
   constexpr int A_PL = BM * kPBK * 2, B_PL = BN * kPBK * 2;  // bytes per plane image
-  constexpr int STAGE = 3 * (A_PL + B_PL);
-  constexpr int NIA = 3 * BM / 16, NIB = 3 * BN / 16;  // 1 KiB pieces per stage
+  constexpr int SUB = 3 * (A_PL + B_PL);                     // one 32-deep k-step's images
+  constexpr int STAGE = KS * SUB;
+  constexpr int NIA1 = 3 * BM / 16, NIB1 = 3 * BN / 16;  // 1 KiB pieces per k-step
+  constexpr int NIA = KS * NIA1, NIB = KS * NIB1;        // ... per stage
   constexpr int EPI = NW * 16 * (WN + 4) * 4;
   constexpr int LDS = NS * STAGE > EPI ? NS * STAGE : EPI;
   // ONE shared object: a second one can make hipcc wait vmcnt(0) before LDS reads
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   const int64_t n0 = (tix % gn) * BN;
   const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
   const int64_t ke = min(a.Kp, kb + a.k_per_split);
-  const int nt = kb < ke ? (int)((ke - kb) / kPBK) : 0;
+  const int nt = kb < ke ? (int)((ke - kb) / (kPBK * KS)) : 0;  // stages
 
   pf32x4 acc[TM][TN], lo[TM][TN];
 #pragma unroll
@@ -251,23 +256,27 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
 #pragma unroll
   for (int j = 0; j < IPWA; ++j) {
     const int ins = min(wave + NW * j, NIA - 1);
-    const int plane = ins / (BM / 16), c = ins % (BM / 16);
-    ldsA[j] = plane * A_PL + c * 1024;
-    const uint16_t* p = A_RC ? piece_rc<A_RC ? BM : 64>(SA, plane, c, m0, kb, lane)
-                             : piece_kc(SA, plane, c, m0, kb, lane);
+    const int ks = ins / NIA1, r = ins % NIA1;
+    const int plane = r / (BM / 16), c = r % (BM / 16);
+    ldsA[j] = ks * SUB + plane * A_PL + c * 1024;
+    const int64_t k0 = kb + ks * kPBK;
+    const uint16_t* p = A_RC ? piece_rc<A_RC ? BM : 64>(SA, plane, c, m0, k0, lane)
+                             : piece_kc(SA, plane, c, m0, k0, lane);
     offA[j] = (uint32_t)((const char*)p - (const char*)SA.p);
   }
 #pragma unroll
   for (int j = 0; j < IPWB; ++j) {
     const int ins = min(wave + NW * j, NIB - 1);
-    const int plane = ins / (BN / 16), c = ins % (BN / 16);
-    ldsB[j] = 3 * A_PL + plane * B_PL + c * 1024;
-    const uint16_t* p = B_RC ? piece_rc<B_RC ? BN : 64>(SB, plane, c, n0, kb, lane)
-                             : piece_kc(SB, plane, c, n0, kb, lane);
+    const int ks = ins / NIB1, r = ins % NIB1;
+    const int plane = r / (BN / 16), c = r % (BN / 16);
+    ldsB[j] = ks * SUB + 3 * A_PL + plane * B_PL + c * 1024;
+    const int64_t k0 = kb + ks * kPBK;
+    const uint16_t* p = B_RC ? piece_rc<B_RC ? BN : 64>(SB, plane, c, n0, k0, lane)
+                             : piece_kc(SB, plane, c, n0, k0, lane);
     offB[j] = (uint32_t)((const char*)p - (const char*)SB.p);
   }
-  const int64_t stepA = 2 * (A_RC ? kPBK * SA.ld : kPBK);  // bytes per stage along k
-  const int64_t stepB = 2 * (B_RC ? kPBK * SB.ld : kPBK);
+  const int64_t stepA = 2 * (A_RC ? kPBK * KS * SA.ld : kPBK * KS);  // bytes per stage along k
+  const int64_t stepB = 2 * (B_RC ? kPBK * KS * SB.ld : kPBK * KS);
   // (the source is passed as `const void*`: with a type-dependent `const char*` argument the
   // host-side pass of hipcc 7.2 fails substitution on this builtin and silently drops the
   // kernel's launch stub)
@@ -294,8 +303,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     boff[i][1] = B_RC ? frag_rc_off<B_RC ? BN : 64>(wn0 + 16 * i, lane, 1) : 0;
   }
 
-  auto compute = [&](int slot) {
-    const char* st = smem + slot * STAGE;
+  auto compute_sub = [&](const char* st) {
     pbf16x8 af[TM][3];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -326,6 +334,10 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
         acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[0], acc[i][tn], 0, 0, 0);
       }
     }
+  };
+  auto compute = [&](int slot) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) compute_sub(smem + slot * STAGE + ks * SUB);
   };
 
   // prologue: stages 0 .. NS-2 in flight
@@ -454,6 +466,7 @@ struct PlDef {
   int bm, bn, wm, wn, ns;
   int occ;     // blocks resident per CU (LDS bound)
   double eff;  // sustained fraction of the per-CU bf16 MFMA peak (model only)
+  int ks = 1;  // 32-deep k-steps per ring stage
 };
 static const PlDef kPl[] = {
     {64, 160, 2, 2, 3, 1, 0.60},   // 0: fwd0 / dH1-shaped (N = 300 -> 320), 256 blocks at B = 8192
@@ -478,6 +491,12 @@ static const PlDef kPl[] = {
     {128, 64, 4, 2, 4, 1, 0.68},   // 17
     {64, 64, 4, 2, 4, 1, 0.60},    // 18
     {64, 64, 4, 2, 2, 3, 0.55},    // 19: 8 waves, 3 blocks per CU
+    // 64-deep stages (KS = 2): one barrier per two MFMA k-steps
+    {64, 64, 2, 2, 3, 1, 0.60, 2},   // 20: 144 KB
+    {64, 64, 4, 2, 2, 1, 0.60, 2},   // 21: 96 KB
+    {128, 64, 4, 2, 2, 1, 0.65, 2},  // 22: 144 KB
+    {64, 128, 4, 2, 2, 1, 0.65, 2},  // 23: 144 KB
+    {64, 64, 2, 2, 2, 1, 0.55, 2},   // 24: 96 KB, 4 waves
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -491,11 +510,16 @@ static bool pl_valid(int ti, bool a_rc, bool b_rc) {
   return (!a_rc || d.bm == 64 || d.bm == 128) && (!b_rc || d.bn == 64 || d.bn == 128);
 }
 
+// a KS = 2 tiling needs every split's k range in whole 64-deep stages
+static bool pl_ks_ok(const PlDef& d, int64_t Kp, int64_t kps) {
+  return d.ks == 1 || (Kp % 64 == 0 && kps % 64 == 0);
+}
+
 static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   auto mk = [&](int ti, int s) {
     PlCfg c{ti, 1, Kp};
     if (s > 1) {
-      c.kps = align_up(ceil_div(Kp, s), kPBK);
+      c.kps = align_up(ceil_div(Kp, s), kPBK * kPl[ti].ks);
       c.splits = (int)ceil_div(Kp, c.kps);
     }
     return c;
@@ -503,8 +527,10 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   if (const char* env = getenv("CTR_GEMM_PLANES_CFG")) {
     int ti = -1, sp = 1;
     if (sscanf(env, "%d,%d", &ti, &sp) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
-        pl_valid(ti, a_rc, b_rc))
-      return mk(ti, sp);
+        pl_valid(ti, a_rc, b_rc)) {
+      const PlCfg c = mk(ti, sp);
+      if (pl_ks_ok(kPl[ti], Kp, c.kps)) return c;
+    }
   }
   // measured on MI355X (tools/gemm_planes_bench.py --sweep, profiles/r02_gemm_planes_sweep.jsonl;
   // fwd1 (N = 200) 14.6 us on 17 vs 16.2 on 8, dX (N = 1664) 70.7 on 19 vs 74.3 on 7):
@@ -529,7 +555,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   PlCfg best = mk(0, 1);
   double best_t = 1e30;
   for (int ti = 0; ti < kNumPl; ++ti) {
-    if (!pl_valid(ti, a_rc, b_rc)) continue;
+    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1) continue;  // the model: KS = 1 only
     const PlDef& d = kPl[ti];
     const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
     for (int s = 1; s <= 32; ++s) {
@@ -554,17 +580,18 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
 
 // every (tiling, orientation) pair is instantiated explicitly (RC operands only on 64- or
 // 128-wide tiles; pl_valid keeps the chooser inside this list)
-#define CTR_PL_K(BM, BN, WMW, WNW, NS, AR, BR)                                          \
-  hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WMW, WNW, AR, BR, NS>), grid, 64 * WMW * WNW, \
-                     0, st, a)
-#define CTR_PL_ALL4(BM, BN, WMW, WNW, NS)                          \
-  if (!a_rc && !b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false); \
-  else if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, true);      \
-  else if (!b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, true, false);      \
-  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, true);
+#define CTR_PL_K(BM, BN, WMW, WNW, NS, AR, BR, KS)                                        \
+  hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WMW, WNW, AR, BR, NS, KS>), grid,             \
+                     64 * WMW * WNW, 0, st, a)
+#define CTR_PL_ALL4K(BM, BN, WMW, WNW, NS, KS)                          \
+  if (!a_rc && !b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false, KS); \
+  else if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, true, KS);      \
+  else if (!b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, true, false, KS);      \
+  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, true, KS);
+#define CTR_PL_ALL4(BM, BN, WMW, WNW, NS) CTR_PL_ALL4K(BM, BN, WMW, WNW, NS, 1)
 #define CTR_PL_AONLY(BM, BN, WMW, WNW, NS)                          \
-  if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false);          \
-  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, false);
+  if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false, 1);       \
+  else CTR_PL_K(BM, BN, WMW, WNW, NS, true, false, 1);
 
 static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc, dim3 grid,
                       hipStream_t st) {
@@ -589,10 +616,16 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 17: CTR_PL_ALL4(128, 64, 4, 2, 4) break;
     case 18: CTR_PL_ALL4(64, 64, 4, 2, 4) break;
     case 19: CTR_PL_ALL4(64, 64, 4, 2, 2) break;
+    case 20: CTR_PL_ALL4K(64, 64, 2, 2, 3, 2) break;
+    case 21: CTR_PL_ALL4K(64, 64, 4, 2, 2, 2) break;
+    case 22: CTR_PL_ALL4K(128, 64, 4, 2, 2, 2) break;
+    case 23: CTR_PL_ALL4K(64, 128, 4, 2, 2, 2) break;
+    case 24: CTR_PL_ALL4K(64, 64, 2, 2, 2, 2) break;
   }
 }
 #undef CTR_PL_AONLY
 #undef CTR_PL_ALL4
+#undef CTR_PL_ALL4K
 #undef CTR_PL_K
 
 static int64_t pl_ws_bytes(const PlCfg& c, int64_t M, int64_t N) {

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="every tiling x split-K in {1,2,4,8}")
     ap.add_argument("--B", type=int, default=8192)
     ap.add_argument("--W", type=int, default=1664)
+    ap.add_argument("--tiles", type=int, default=25, help="sweep tilings 0 .. tiles-1")
+    ap.add_argument("--only", default="", help="comma-separated tiling indices to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -63,7 +65,8 @@ def main():
         out = torch.empty(M, N, device=dev)
         cfgs = ["auto"]
         if args.sweep:
-            cfgs += [f"{t},{s}" for t in range(20) for s in (1, 2, 4, 8)
+            tiles = [int(t) for t in args.only.split(",")] if args.only else range(args.tiles)
+            cfgs += [f"{t},{s}" for t in tiles for s in (1, 2, 4, 8)
                      if not (b_rc and t in (0, 6, 8, 9))]
         best = None
         for cfg in cfgs:
@@ -72,6 +75,8 @@ def main():
             else:
                 os.environ["CTR_GEMM_PLANES_CFG"] = cfg
             chosen = H.gemm_planes_config(a_rc, b_rc, M, N, K)
+            if cfg != "auto" and chosen["tile"] != int(cfg.split(",")[0]):
+                continue  # not valid for this shape (the library fell back to its choice)
             us = time_one(pa, pb, a_rc, b_rc, out, args.reps)
             tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
             print(json.dumps({"shape": name, "cfg": cfg, "chosen": chosen, "us": round(us, 2),
