@@ -466,6 +466,10 @@ int ctr_ffm_forward(const void* idx, int idx_type, int64_t B, int F, int K, int6
 int ctr_ffm_backward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
                      const float* const* tables, const float* gz, int32_t* keys, float* vals,
                      ctr_stream_t stream);
+/* ctr_ffm_keys: the keys of ctr_ffm_backward alone (same positions): the table rows an FFM
+ * step reads and updates, for the fused trainer's catch-up before the forward. */
+int ctr_ffm_keys(const void* idx, int idx_type, int64_t B, int F, int64_t V, int32_t* keys,
+                 int32_t* err_flag, ctr_stream_t stream);
 
 /* ------------------------------------------------ §8f: IPNN (InnerPNN) --------------
  * ctr_ipnn_forward: cat[b] = flat(E[x_b]) (F*K) ++ [ <E[x_bi],E[x_bj]> for i<j, row-major ]

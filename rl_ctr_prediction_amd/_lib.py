@@ -136,6 +136,7 @@ SIGNATURES = {
                                   _vp, _vp, _vp]),
     "ctr_ffm_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _f32,
                                _vp, _vp, _vp, _vp, _vp]),
+    "ctr_ffm_keys": (_i32, [_vp, _i32, _i64, _i32, _i64, _vp, _vp, _vp]),
     "ctr_ffm_backward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "ctr_csv_to_bin": (_i32, [C.c_char_p, C.c_char_p, _vp, _vp, _vp]),
     "ctr_bin_info": (_i32, [C.c_char_p, _vp, _vp, _vp, _vp]),

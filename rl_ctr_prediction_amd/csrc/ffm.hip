@@ -105,6 +105,24 @@ __global__ __launch_bounds__(256) void ffm_backward_kernel(
   }
 }
 
+// the keys alone (the fused trainer's catch-up runs before the forward): same positions
+template <typename IdxT>
+__global__ __launch_bounds__(256) void ffm_keys_kernel(const IdxT* __restrict__ idx, int64_t B,
+                                                       int F, int64_t V,
+                                                       int32_t* __restrict__ keys,
+                                                       int32_t* err) {
+  const int64_t per_ex = (int64_t)F * (F - 1);
+  const int64_t total = B * per_ex;
+  for (int64_t pos = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; pos < total;
+       pos += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = pos / per_ex;
+    const int r = (int)(pos - b * per_ex);
+    const int f = r / (F - 1), tp = r - f * (F - 1);
+    const int t = tp < f ? tp : tp + 1;
+    keys[pos] = (int32_t)(t * V + load_row(idx, b * F + f, V, err));
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
@@ -161,5 +179,24 @@ extern "C" int ctr_ffm_backward(const void* idx, int idx_type, int64_t B, int F,
     hipLaunchKernelGGL(ffm_backward_kernel<int32_t>, grid, 256, 0, st,
                        static_cast<const int32_t*>(idx), B, F, K, V, tables, gz, keys, vals);
   CTR_LAUNCH_CHECK("ctr_ffm_backward");
+  return CTR_OK;
+}
+
+extern "C" int ctr_ffm_keys(const void* idx, int idx_type, int64_t B, int F, int64_t V,
+                            int32_t* keys, int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(idx && keys && B >= 0 && F > 1 && V > 0, "ctr_ffm_keys: bad arguments");
+  CTR_REQUIRE((int64_t)F * V < (int64_t(1) << 31), "ctr_ffm_keys: F*V must fit int32 keys");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  if (B == 0) return CTR_OK;
+  const int64_t total = B * F * (int64_t)(F - 1);
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(total, 256), 16384);
+  hipStream_t st = as_stream(stream);
+  if (idx_type == CTR_IDX_I64)
+    hipLaunchKernelGGL(ffm_keys_kernel<int64_t>, grid, 256, 0, st,
+                       static_cast<const int64_t*>(idx), B, F, V, keys, err_flag);
+  else
+    hipLaunchKernelGGL(ffm_keys_kernel<int32_t>, grid, 256, 0, st,
+                       static_cast<const int32_t*>(idx), B, F, V, keys, err_flag);
+  CTR_LAUNCH_CHECK("ctr_ffm_keys");
   return CTR_OK;
 }

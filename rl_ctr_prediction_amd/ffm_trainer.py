@@ -1,0 +1,263 @@
+"""The fused FFM training step: the reference's per-batch body
+(all_main/pretrain_main.py:72-79: ``y = model(x); loss = BCELoss(y, labels);
+model.zero_grad(); loss.backward(); optimizer.step()``) for FFM (p_model.py:59-100) with
+torch.optim.Adam(lr, weight_decay) — dense Adam semantics (every row of every field table
+moves every step), computed deferred-exact like FusedCTRTrainer's default mode.
+
+The F field tables ``field_feature_embeddings.t.weight`` [V, K] are re-pointed into one
+contiguous [F*V, K] buffer (same Parameter objects, same state_dict), so the F*V
+(table, row) key space of ctr_ffm_backward is one deferred-Adam table:
+
+  ffm_keys(x)                      keys t*V + x[b,f] of every (example, field, table) slot
+  sparse plans over keys and x     (the field tables' and the linear table's rows)
+  deferred catch-up of those rows  (they replay the g = wd*p steps they missed)
+  ffm_forward(+BCE head)           z, p, per-example loss, dL/dz
+  ffm_backward                     per-slot table-row gradients [B*F*(F-1), K]
+  segmented sums (+ Adam apply)    per (table, row), in slot order, applied at step t
+  linear: per-row sums of dL/dz    + its deferred Adam; bias: sum(dL/dz) + dense Adam
+
+No dense [F*V, K] gradient is materialised (the AutogradTrainer path writes F dense [V, K]
+gradients and streams F*V*K*24 B of Adam traffic per step). Single-process steps are
+captured into HIP graphs and replayed, as in FusedCTRTrainer.step.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from . import hip_ops
+from .p_model import FFM
+
+
+@dataclass
+class _FFMBufs:
+    B: int
+    keys: torch.Tensor                 # int32 [S2]  S2 = B*F*(F-1)
+    vals: torch.Tensor                 # [S2, K]     per-slot table-row gradients
+    plan: hip_ops.SparsePlanBuffers    # over keys (F*V rows)
+    plan_x: hip_ops.SparsePlanBuffers  # over x (V rows of the linear table)
+    grad_rows: torch.Tensor            # [S2, K]     per-row sums (scratch)
+    slot_g: torch.Tensor               # [B*F, 1]    dL/dz of each slot's example
+    grad_w: torch.Tensor               # [B*F, 1]    per-row sums of the linear table
+    fwd: dict                          # z, p, loss_elem, gz [B]
+    loss: torch.Tensor                 # [1]
+
+
+class FusedFFMTrainer:
+    """Fused forward + BCE + backward + deferred-exact dense Adam for FFM.
+
+    Args mirror ``torch.optim.Adam(model.parameters(), lr, betas, eps, weight_decay)``;
+    the interface is FusedCTRTrainer's (step / flush / reset_optimizer /
+    optimizer_state_dict / check_errors)."""
+
+    def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 0.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, seed: int | None = None):
+        if not isinstance(model, FFM):
+            raise TypeError("FusedFFMTrainer drives FFM")
+        tabs = [e.weight for e in model.field_feature_embeddings]
+        self.model = model
+        self.kind = "FFM"
+        self.lr, self.weight_decay, self.betas, self.eps = float(lr), float(weight_decay), betas, eps
+        self.device = tabs[0].device
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedFFMTrainer needs the model on a ROCm device")
+        self.F = len(tabs)
+        self.V, self.K = tabs[0].shape
+        if self.F < 2:
+            raise ValueError("FusedFFMTrainer: FFM needs at least 2 fields")
+        if self.F * self.V >= 2**31:
+            raise ValueError("FusedFFMTrainer: F*V must fit int32 keys")
+        FV, K, dev = self.F * self.V, self.K, self.device
+        # the field tables as row blocks of one [F*V, K] table
+        self.T = torch.empty(FV, K, dtype=torch.float32, device=dev)
+        for t, p in enumerate(tabs):
+            blk = self.T[t * self.V:(t + 1) * self.V]
+            blk.copy_(p.data)
+            p.data = blk
+        self.m_T = torch.zeros_like(self.T)
+        self.v_T = torch.zeros_like(self.T)
+        self.last_T = torch.zeros(FV, dtype=torch.int32, device=dev)
+        # the linear table [V, 1] as a K = 1 deferred table; the bias through the dense Adam
+        self.w = model.linear.weight.data
+        self.m_w = torch.zeros_like(self.w)
+        self.v_w = torch.zeros_like(self.w)
+        self.last_w = torch.zeros(self.V, dtype=torch.int32, device=dev)
+        self.bias = model.bias.data
+        self.g_bias = torch.zeros_like(self.bias)
+        self.m_b = torch.zeros_like(self.bias)
+        self.v_b = torch.zeros_like(self.bias)
+        self.ptrs = model._ptrs.get(tabs)
+        self._vec_ok = K % 4 == 0 and 64 % (K // 4 or 1) == 0 and K <= 256
+        self.fuse_apply = os.environ.get("CTR_FUSE_APPLY", "1") != "0"
+        self.keep_grads = False  # fused apply: keep every row's sum in b.grad_rows (tests)
+        self.step_ctr = torch.tensor([0, 1], dtype=torch.int32, device=dev)
+        self.step_done, self.step_cur = self.step_ctr[0:1], self.step_ctr[1:2]
+        self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.step_count = 0
+        self._dirty = False
+        model.register_forward_pre_hook(lambda mod, inp: self.flush())
+        model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars: self.flush())
+        self._bufs: _FFMBufs | None = None
+        self._bufsets: dict = {}
+        self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
+        self.use_graphs = True
+        self.max_graphs = 8
+        self._graphs: dict = {}
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        self._graph_tab_version = self.step_table.version
+        self.timing = None  # FusedCTRTrainer's bench hook: not instrumented here
+
+    # ----------------------------------------------------------------- optimiser -----
+    def _table_args(self):
+        return (self.T, self.m_T, self.v_T, None, None, None, self.last_T)
+
+    def _w_args(self):
+        return (self.w, self.m_w, self.v_w, None, None, None, self.last_w)
+
+    def flush(self) -> None:
+        """Bring every row of every table up to the last completed step."""
+        if self._dirty and self.step_count > 0:
+            for tab in (self._table_args(), self._w_args()):
+                hip_ops.adam_deferred_flush(*tab, self.step_count, self.step_table, self.betas,
+                                            self.eps, self.weight_decay)
+        self._dirty = False
+
+    def reset_optimizer(self, lr: float | None = None) -> None:
+        """A re-created torch.optim.Adam (all_main/pretrain_main.py:153), optionally at a new
+        learning rate; captured graphs stay valid (the step table is rewritten in place)."""
+        self.flush()
+        if lr is not None:
+            self.lr = float(lr)
+            self.step_table.set_lr(self.lr)
+        for t in (self.m_T, self.v_T, self.m_w, self.v_w, self.m_b, self.v_b, self.last_T,
+                  self.last_w):
+            t.zero_()
+        self.step_ctr.copy_(torch.tensor([0, 1], dtype=torch.int32))
+        self.step_count = 0
+
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.Adam-compatible state_dict (parameter order = model.parameters():
+        linear.weight, bias, field_feature_embeddings.0..F-1.weight)."""
+        self.flush()
+        V = self.V
+        m = [self.m_w, self.m_b] + [self.m_T[t * V:(t + 1) * V] for t in range(self.F)]
+        v = [self.v_w, self.v_b] + [self.v_T[t * V:(t + 1) * V] for t in range(self.F)]
+        n = len(m)
+        state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": m[i].clone(),
+                     "exp_avg_sq": v[i].clone()} for i in range(n)}
+        return {"state": state if self.step_count else {},
+                "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                                  "weight_decay": self.weight_decay, "amsgrad": False,
+                                  "params": list(range(n))}]}
+
+    def check_errors(self) -> None:
+        hip_ops.check_index_error(self.err)
+
+    # --------------------------------------------------------------------- buffers ---
+    def _buffers(self, B: int, F: int) -> _FFMBufs:
+        b = self._bufsets.get((B, F))
+        if b is None:
+            dev, K = self.device, self.K
+            S2, S = B * F * (F - 1), B * F
+            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+            b = _FFMBufs(B=B, keys=torch.empty(max(S2, 1), dtype=torch.int32, device=dev),
+                         vals=e(max(S2, 1), K), plan=hip_ops.SparsePlanBuffers(S2, dev),
+                         plan_x=hip_ops.SparsePlanBuffers(S, dev), grad_rows=e(max(S2, 1), K),
+                         slot_g=e(max(S, 1), 1), grad_w=e(max(S, 1), 1),
+                         fwd=dict(z=e(B), p=e(B), loss_elem=e(B), gz=e(B)), loss=e(1))
+            self._bufsets[(B, F)] = b
+        self._bufs = b
+        return b
+
+    # ------------------------------------------------------------------------ step ----
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """One training step on batch (x [B,F] int64/int32, y [B] 0/1); returns the mean
+        BCE as the trainer's persistent 1-element loss buffer for this batch shape (valid
+        until the next step with the same shape; no host sync)."""
+        B, F = x.shape
+        if F != self.F:
+            raise ValueError(f"FusedFFMTrainer: batch has {F} fields, model {self.F}")
+        if self.use_graphs and x.is_cuda and y.dtype == torch.float32 and y.is_contiguous():
+            return self._graph_step(x, y)
+        self.step_table.ensure(self.step_count + 1)
+        loss = self._launch(x, y)
+        self._after_step()
+        return loss
+
+    def _after_step(self) -> None:
+        self.step_count += 1
+        self._dirty = True
+
+    def _graph_step(self, x, y):
+        if self.step_table.capacity < self.step_count + 2:
+            self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
+        if self._graph_tab_version != self.step_table.version:
+            self._graphs.clear()  # they hold the old table's address
+            self._graph_tab_version = self.step_table.version
+        key = (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
+               tuple(y.shape))
+        hit = self._graphs.get(key)
+        if hit is None:
+            loss = self._launch(x, y)  # the real step; also sizes every buffer
+            self._after_step()
+            if len(self._graphs) < self.max_graphs:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    self._launch(x, y)  # captured, not executed
+                self._graphs[key] = (g, self._bufs)
+            return loss
+        g, self._bufs = hit
+        g.replay()
+        self._after_step()
+        return self._bufs.loss
+
+    def _launch(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Enqueue one step; step-dependent values come from the device step counter."""
+        B, F = x.shape
+        V, K = self.V, self.K
+        b = self._buffers(B, F)
+        y = y.reshape(-1)
+        if y.dtype != torch.float32:
+            y = y.float()
+        y = y.contiguous()
+        tabs = [e.weight.data for e in self.model.field_feature_embeddings]
+        hint = self.step_count + 1
+        opt = dict(betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
+        # the batch's rows: plans over the (table, row) keys and over the ids
+        hip_ops.ffm_keys(x, V, out=b.keys, err_flag=self.err)
+        b.plan.build(b.keys[:b.plan.capacity], F * V)
+        b.plan_x.build(x, V, err_flag=self.err)
+        # catch-up: those rows replay the steps they missed (read the completed step)
+        hip_ops.adam_deferred_rows(*self._table_args(), b.plan, hint, self.step_table, **opt,
+                                   step_dev=self.step_done)
+        hip_ops.adam_deferred_rows(*self._w_args(), b.plan_x, hint, self.step_table, **opt,
+                                   step_dev=self.step_done)
+        fwd = hip_ops.ffm_forward(x, tabs, self.ptrs, self.w, self.bias, labels=y, mean_div=B,
+                                  err_flag=self.err, out=b.fwd)
+        gz = fwd["gz"]
+        hip_ops.ffm_backward(x, tabs, self.ptrs, gz, keys=b.keys, vals=b.vals)
+        S2 = b.plan.capacity
+        apply = dict(step_dev=self.step_cur, step_table=self.step_table, step=hint, **opt)
+        if self._vec_ok and self.fuse_apply and K >= 32:
+            hip_ops.segment_sum_rows_adam(b.plan, b.vals[:S2], None, self._table_args(), **apply,
+                                          out=b.grad_rows, keep_sums=self.keep_grads)
+        else:
+            hip_ops.segment_sum_rows(b.plan, b.vals[:S2], out=b.grad_rows)
+            hip_ops.adam_deferred_rows(*self._table_args(), b.plan, hint, self.step_table, **opt,
+                                       grad_rows=b.grad_rows, step_dev=self.step_cur)
+        # linear table: dL/dw[x_bf] = gz[b], summed per row in slot order
+        b.slot_g.view(B, F).copy_(gz.view(B, 1).expand(B, F))
+        hip_ops.segment_sum_rows(b.plan_x, b.slot_g[:B * F], out=b.grad_w)
+        hip_ops.adam_deferred_rows(*self._w_args(), b.plan_x, hint, self.step_table, **opt,
+                                   grad_rows=b.grad_w, step_dev=self.step_cur)
+        hip_ops.tensor_sum(gz, out=self.g_bias)
+        hip_ops.adam_dense(self.bias, self.g_bias, self.m_b, self.v_b, hint, self.lr,
+                           self.betas, self.eps, self.weight_decay, step_dev=self.step_cur,
+                           table=self.step_table)
+        hip_ops.tensor_sum(fwd["loss_elem"], scale=1.0 / B, out=b.loss)
+        hip_ops.step_end(self.step_ctr)
+        return b.loss

@@ -783,8 +783,9 @@ class FFMTables:
         return self.ptrs
 
 
-def ffm_forward(idx, tables, ptrs, lin, bias, labels=None, mean_div=None, err_flag=None):
-    """FFM logits z [B] (and with labels: p, per-example loss, dL/dz)."""
+def ffm_forward(idx, tables, ptrs, lin, bias, labels=None, mean_div=None, err_flag=None, out=None):
+    """FFM logits z [B] (and with labels: p, per-example loss, dL/dz). out: a dict of this
+    function's earlier result for the same B, written in place."""
     idx, it = _idx(idx)
     B, F = idx.shape
     V, K = tables[0].shape
@@ -792,27 +793,44 @@ def ffm_forward(idx, tables, ptrs, lin, bias, labels=None, mean_div=None, err_fl
         raise ValueError(f"ffm_forward: {len(tables)} tables for {F} fields")
     dev = tables[0].device
     e = lambda: torch.empty(B, dtype=torch.float32, device=dev)  # noqa: E731
-    z = e()
-    out = {"z": z}
-    if labels is not None:
-        out.update(p=e(), loss_elem=e(), gz=e())
+    if out is None:
+        out = {"z": e()}
+        if labels is not None:
+            out.update(p=e(), loss_elem=e(), gz=e())
+    z = out["z"]
     lib.ctr_ffm_forward(_p(idx), it, B, F, K, V, _p(ptrs), _p(lin), _p(bias), _p(z),
                         _p(labels), float(B if mean_div is None else mean_div), _p(out.get("p")),
                         _p(out.get("loss_elem")), _p(out.get("gz")), _p(err_flag), _stream())
     return out
 
 
-def ffm_backward(idx, tables, ptrs, gz):
-    """(keys int32 [B*F*(F-1)], vals [B*F*(F-1), K]): every example's table-row gradients."""
+def ffm_backward(idx, tables, ptrs, gz, keys=None, vals=None):
+    """(keys int32 [B*F*(F-1)], vals [B*F*(F-1), K]): every example's table-row gradients
+    (into keys / vals when given)."""
     idx, it = _idx(idx)
     B, F = idx.shape
     V, K = tables[0].shape
     n = B * F * (F - 1)
-    keys = torch.empty(max(n, 1), dtype=torch.int32, device=gz.device)
-    vals = torch.empty(max(n, 1), K, dtype=torch.float32, device=gz.device)
+    if keys is None:
+        keys = torch.empty(max(n, 1), dtype=torch.int32, device=gz.device)
+    if vals is None:
+        vals = torch.empty(max(n, 1), K, dtype=torch.float32, device=gz.device)
+    if keys.numel() < n or vals.shape[0] < n or vals.shape[1] != K:
+        raise ValueError("ffm_backward: keys / vals too small")
     lib.ctr_ffm_backward(_p(idx), it, B, F, K, V, _p(ptrs), _p(_f32(gz.contiguous(), "gz")),
                          _p(keys), _p(vals), _stream())
     return keys[:n], vals[:n]
+
+
+def ffm_keys(idx, V: int, out=None, err_flag=None) -> torch.Tensor:
+    """int32 [B*F*(F-1)]: the (table, row) keys t*V + x of ffm_backward, without values."""
+    idx, it = _idx(idx)
+    B, F = idx.shape
+    n = B * F * (F - 1)
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=idx.device)
+    lib.ctr_ffm_keys(_p(idx), it, B, F, int(V), _p(out), _p(err_flag), _stream())
+    return out[:n]
 
 
 # ----------------------------------------------------------------------- REINFORCE ----

@@ -31,7 +31,8 @@ import torch
 import torch.nn as nn
 
 from .. import creat_data as Data
-from ..pretrain_main import (AutogradTrainer, DeviceBatches, eva_stopping, get_model, setup_seed,
+from ..ffm_trainer import FusedFFMTrainer
+from ..pretrain_main import (DeviceBatches, eva_stopping, get_model, setup_seed,
                              submission, test, train)
 from ..trainer import FusedCTRTrainer
 
@@ -80,7 +81,7 @@ def main(data_path, dataset_name, campaign_id, valid_day, test_day, latent_dims,
         model.load_embedding(fm_params)
     loss = nn.BCELoss()
     if model_name == "FFM":
-        trainer = AutogradTrainer(model, learning_rate, weight_decay)
+        trainer = FusedFFMTrainer(model, lr=learning_rate, weight_decay=weight_decay)
     else:
         trainer = FusedCTRTrainer(model, lr=learning_rate, weight_decay=weight_decay)
 

@@ -9,8 +9,8 @@ AUC over the concatenated test predictions, loss-/AUC-based early stopping with 
 of the checkpoint four epochs back.
 
 Differences, all deliberate: the training step is the fused HIP step (FM, DeepFM and
-IPNN; FFM trains through autograd on its HIP kernels + torch.optim.Adam, AutogradTrainer;
-the other six model families are out of scope); the batches are
+IPNN; FFM: FusedFFMTrainer, the same deferred-exact Adam over its F*V field-table rows;
+AutogradTrainer keeps the autograd + torch.optim.Adam route for comparison; the other six model families are out of scope); the batches are
 sliced from one device-resident copy of the data instead of 8 DataLoader worker
 processes; the rotating-checkpoint cleanup skips files that were never written (the
 reference crashes there when epoch < 5, all_main/pretrain_main.py:201-202).
@@ -31,6 +31,7 @@ from sklearn.metrics import roc_auc_score
 from . import creat_data as Data
 from .binfmt import load_encoded
 from . import p_model as Model
+from .ffm_trainer import FusedFFMTrainer
 from .trainer import FusedCTRTrainer
 
 
@@ -58,7 +59,8 @@ def get_model(model_name, feature_nums, field_nums, latent_dims):
 
 class AutogradTrainer:
     """The reference's own step (all_main/pretrain_main.py:72-79: forward, BCELoss,
-    zero_grad, backward, torch.optim.Adam.step) for models without a fused step (FFM): the
+    zero_grad, backward, torch.optim.Adam.step) through autograd (tests compare it with the
+    fused trainers): the
     forward / backward run on the HIP kernels through autograd, the dense gradients go to
     an unchanged torch.optim.Adam, re-created every epoch like the reference (line 153)."""
 
@@ -190,7 +192,7 @@ def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, l
     model = get_model(model_name, feature_nums, field_nums, latent_dims).to(device)
     loss = nn.BCELoss()
     if model_name == "FFM":
-        trainer = AutogradTrainer(model, learning_rate, weight_decay)
+        trainer = FusedFFMTrainer(model, lr=learning_rate, weight_decay=weight_decay)
     else:
         trainer = FusedCTRTrainer(model, lr=learning_rate, weight_decay=weight_decay)
 

@@ -353,7 +353,12 @@ def test_pg_reference_shape_bug_kept_and_fixable(cuda):
     assert pg2.choose_action(x).shape == (8, 1)
 
 
-def test_pg_learn_matches_autograd(cuda):
+@pytest.mark.parametrize("V,F,K,A,T", [(200, 8, 2, 4, 300),
+                                       # C4 (BASELINE configs[3]): the C2 table's
+                                       # Feature_Embedding state (325 pairs + 416 = 741)
+                                       # -> 1024-512-256-128-5, a 4096-transition episode
+                                       (1_000_000, 26, 16, 5, 4096)])
+def test_pg_learn_matches_autograd(cuda, V, F, K, A, T):
     """The fused learn pass equals autograd through loss_func + torch.optim.Adam(wd=1e-5).
 
     The reference's own learn() feeds mean(vt) of STANDARDISED returns into the loss —
@@ -362,20 +367,21 @@ def test_pg_learn_matches_autograd(cuda):
     and discount_and_norm_rewards separately (vs the oracle and the golden vectors)."""
     P = _pkg()
     torch.manual_seed(21)
-    pg = P.PolicyGradient(200, 8, 2, "g", action_nums=4, device="cuda:0", fix_input_dims=True)
+    pg = P.PolicyGradient(V, F, K, "g", action_nums=A, device="cuda:0", fix_input_dims=True)
     for mod in pg.policy_net.modules():
         if isinstance(mod, torch.nn.Dropout):
             mod.p = 0.0
     rp = [p.detach().cpu().double().clone().requires_grad_(True) for p in pg.policy_net.mlp.parameters()]
-    x = torch.randint(0, 200, (300, 8), device=cuda)
-    a = torch.randint(1, 5, (300, 1), device=cuda)
-    r = torch.randn(300, 1, device=cuda)
-    pg.store_transition(x[:100], a[:100], r[:100])
-    pg.store_transition(x[100:], a[100:], r[100:])
+    x = torch.randint(0, V, (T, F), device=cuda)
+    a = torch.randint(1, A + 1, (T, 1), device=cuda)
+    r = torch.randn(T, 1, device=cuda)
+    h1 = T // 3
+    pg.store_transition(x[:h1], a[:h1], r[:h1])
+    pg.store_transition(x[h1:], a[h1:], r[h1:])
     vt = torch.tensor(O.pg_discount_and_norm(r.cpu().numpy(), 1.0), dtype=torch.float32).reshape(-1)
     np.testing.assert_allclose(pg.discount_and_norm_rewards().reshape(-1), vt.numpy(), rtol=1e-6,
                                atol=1e-6)
-    vt_raw = (torch.rand(300) + 0.5)
+    vt_raw = (torch.rand(T) + 0.5)
     loss = pg._fused_learn(x, a, vt_raw.to(cuda))
     s = O.feature_embedding(pg.policy_net.embedding_layer.feature_embedding.weight.detach().cpu().double(),
                             x.cpu())
