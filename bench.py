@@ -364,6 +364,9 @@ def main():
                          "with a sparse all-gather")
     ap.add_argument("--sweep-slices", type=int, default=0,
                     help="deferred mode: background sweep of 1/N of the rows per step (0 = off)")
+    ap.add_argument("--lookahead", type=int, default=2,
+                    help="sparse plans built this many batches ahead, concurrently with the "
+                         "step (FusedCTRTrainer next_x); 0 = every plan in its own step")
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
@@ -416,8 +419,18 @@ def main():
     trainer.sweep_slices = args.sweep_slices
     log(f"rank {rank}/{world}: {cfg['kind']} V={V} K={K} B={B} ready in {time.perf_counter() - t0:.1f}s")
 
+    # one running batch index over every loop below, so each step's lookahead batch is the
+    # batch the next step trains on (the graphs captured in the warm-up are the ones replayed)
+    seq = [0]
+
+    def step(_i):
+        i = seq[0]
+        seq[0] += 1
+        nxt = [xs[(i + j) % len(xs)] for j in range(1, args.lookahead + 1)]
+        return trainer.step(xs[i % len(xs)], ys[i % len(ys)], next_x=nxt)
+
     for i in range(args.warmup):
-        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+        step(i)
 
     def total_ms(spans):
         return float(sum(a.elapsed_time(b) for a, b, _ in spans))
@@ -432,7 +445,7 @@ def main():
     trainer.flush()
     trainer.timing = {k: [] for k in keys}
     for i in range(n_bd):
-        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+        step(i)
     trainer.flush()
     torch.cuda.synchronize()
     bd, trainer.timing = trainer.timing, None
@@ -451,7 +464,7 @@ def main():
     trainer.timing = None
     t_start = time.perf_counter()
     for i in range(args.steps):
-        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+        step(i)
     # deferred mode: every row is brought to the last step INSIDE the timed region, so the
     # measured work is the complete dense-Adam trajectory of K steps (nothing left owed)
     trainer.flush()
@@ -471,7 +484,7 @@ def main():
     # (profiles/) is the cross-check
     trainer.timing = {dominant: [], "flush": []}
     for i in range(args.steps):
-        trainer.step(xs[i % len(xs)], ys[i % len(ys)])
+        step(i)
     trainer.flush()
     torch.cuda.synchronize()
     timing = trainer.timing
@@ -567,7 +580,9 @@ def main():
                        "all-reduce)" if sharding == "rows" else
                        " (replicated tables, sparse row-grad all-gather)" if world > 1 else ""),
                    "optimizer": f"dense Adam lr=1e-3 wd=1e-5 (reference semantics), "
-                                f"{args.optimizer} mode"},
+                                f"{args.optimizer} mode",
+                   "plan_lookahead": (args.lookahead if world == 1 and args.optimizer == "deferred"
+                                      else 0)},
         "roofline": roofline,
         "kernels": kernels,
         "gather_scatter": {

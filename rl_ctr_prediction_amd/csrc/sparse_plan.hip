@@ -96,17 +96,22 @@ __device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t* wave
 
 // One pass of the stable LSD sort over one tile: the block scans the per-tile digit
 // histograms for its global digit bases (thread t owns the DPT consecutive digits
-// [t*DPT, (t+1)*DPT)), ranks its keys stably with wave ballots (BITS ballots give the
-// lanes holding the same digit; popcount below the lane = rank within the wave; the waves
-// before it and the item rows before it come from per-wave counts and a running count in
-// LDS; measured: the per-digit update below beats one LDS atomic per (wave, digit) group,
-// 13-16 vs 10-12 us per pass at C2), and scatters (key, value).
+// [t*DPT, (t+1)*DPT); the tile rows are read 8 at a time, independent loads in flight
+// together), ranks its keys stably with wave ballots (BITS ballots give the lanes holding
+// the same digit; popcount below the lane = rank within the wave) and scatters (key, value).
+// Ranking works on groups of G item rows: every (row, wave) leader records its digit
+// count, ONE barrier, each thread turns its digits' counts into exclusive prefixes over
+// (row, wave) order carried across groups, one barrier, and every key reads its offset —
+// 2 barriers per group instead of 3 per row (8-bit digits: G = 8 rows, 2 x 32 KB LDS).
 template <int IPT, bool FIRST, bool LAST, int BITS>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a) {
   constexpr int R = Radix<BITS>::kBins, DPT = Radix<BITS>::kDPT;
-  __shared__ int32_t s_base[R];               // global base of each digit for this tile
-  __shared__ int32_t s_run[R];                // digits ranked so far in this tile
-  __shared__ int32_t s_wcnt[kSortWaves][R];   // per-wave digit counts of one item row
+  constexpr int G = (R <= 256) ? (IPT < 8 ? IPT : 8) : 1;  // item rows ranked together
+  static_assert(IPT % G == 0, "IPT must be a multiple of the ranking group");
+  __shared__ int32_t s_base[R];                   // global base of each digit for this tile
+  __shared__ int32_t s_run[R];                    // digits ranked in earlier groups
+  __shared__ int32_t s_cnt[G][kSortWaves][R];     // (row, wave) digit counts of a group
+  __shared__ int32_t s_pre[G][kSortWaves][R];     // their exclusive prefixes (+ s_run)
   __shared__ int32_t s_wtot[kSortWaves];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
@@ -133,23 +138,31 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
   for (int k = 0; k < DPT; ++k) tot[k] = before[k] = 0;
   {
     const int32_t* hcol = a.hist + t * DPT;
-    for (int j = 0; j < a.n_tiles; ++j) {
-      int32_t hv[DPT];
-      if constexpr (DPT % 4 == 0) {
+    constexpr int U = 8;  // tile rows loaded together
+    for (int j0 = 0; j0 < a.n_tiles; j0 += U) {
+      int32_t hv[U][DPT];
 #pragma unroll
-        for (int k = 0; k < DPT; k += 4) {
-          const int4 q = *reinterpret_cast<const int4*>(hcol + (int64_t)j * R + k);
-          hv[k] = q.x; hv[k + 1] = q.y; hv[k + 2] = q.z; hv[k + 3] = q.w;
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u;
+        if constexpr (DPT % 4 == 0) {
+#pragma unroll
+          for (int k = 0; k < DPT; k += 4) {
+            int4 q = make_int4(0, 0, 0, 0);
+            if (j < a.n_tiles) q = *reinterpret_cast<const int4*>(hcol + (int64_t)j * R + k);
+            hv[u][k] = q.x; hv[u][k + 1] = q.y; hv[u][k + 2] = q.z; hv[u][k + 3] = q.w;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < DPT; ++k) hv[u][k] = j < a.n_tiles ? hcol[(int64_t)j * R + k] : 0;
         }
-      } else {
-#pragma unroll
-        for (int k = 0; k < DPT; ++k) hv[k] = hcol[(int64_t)j * R + k];
       }
 #pragma unroll
-      for (int k = 0; k < DPT; ++k) {
-        tot[k] += hv[k];
-        before[k] += j < tile ? hv[k] : 0;
-      }
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < DPT; ++k) {
+          tot[k] += hv[u][k];
+          before[k] += j0 + u < tile ? hv[u][k] : 0;
+        }
     }
   }
   int32_t mine = 0;
@@ -164,43 +177,54 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
   }
   for (int d = t; d < R; d += kSortThreads)
 #pragma unroll
-    for (int j = 0; j < kSortWaves; ++j) s_wcnt[j][d] = 0;
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int j = 0; j < kSortWaves; ++j) s_cnt[i][j][d] = 0;
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
   int32_t pos[IPT];
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const int64_t e = base + i * kSortThreads + t;
-    const bool ok = e < a.S;
-    const uint32_t d = (key[i] >> a.shift) & (R - 1);
-    uint64_t peers = __ballot(ok);
+  for (int g0 = 0; g0 < IPT; g0 += G) {
+    int rank[G];
 #pragma unroll
-    for (int b = 0; b < BITS; ++b) {
-      const uint64_t m = __ballot((d >> b) & 1u);
-      peers &= ((d >> b) & 1u) ? m : ~m;
+    for (int i = 0; i < G; ++i) {
+      const int64_t e = base + (g0 + i) * kSortThreads + t;
+      const bool ok = e < a.S;
+      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < BITS; ++b) {
+        const uint64_t m = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? m : ~m;
+      }
+      rank[i] = __popcll(peers & lt);
+      if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
     }
-    const int rank = __popcll(peers & lt);
-    if (ok && rank == 0) s_wcnt[w][d] = __popcll(peers);
     __syncthreads();
-    int32_t off = s_run[d] + rank;
-#pragma unroll
-    for (int j = 0; j < kSortWaves; ++j) off += j < w ? s_wcnt[j][d] : 0;
-    pos[i] = ok ? s_base[d] + off : -1;
-    __syncthreads();
-    // the running counts of this item row's digits (thread t owns digits t*DPT ...)
+    // per owned digit: exclusive prefix over (row, wave) of this group, after s_run
 #pragma unroll
     for (int k = 0; k < DPT; ++k) {
       const int dd = t * DPT + k;
-      int32_t add = 0;
+      int32_t run = s_run[dd];
 #pragma unroll
-      for (int j = 0; j < kSortWaves; ++j) {
-        add += s_wcnt[j][dd];
-        s_wcnt[j][dd] = 0;
-      }
-      s_run[dd] += add;
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int j = 0; j < kSortWaves; ++j) {
+          const int32_t c = s_cnt[i][j][dd];
+          s_pre[i][j][dd] = run;
+          s_cnt[i][j][dd] = 0;
+          run += c;
+        }
+      s_run[dd] = run;
     }
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int64_t e = base + (g0 + i) * kSortThreads + t;
+      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
+      pos[g0 + i] = e < a.S ? s_base[d] + s_pre[i][w][d] + rank[i] : -1;
+    }
   }
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
@@ -334,7 +358,7 @@ static int key_bits(int64_t V) {
 static int plan_ipt(int64_t S) {
   if (const char* env = getenv("CTR_PLAN_IPT")) {  // A/B runs
     const int v = atoi(env);
-    if (v == 4 || v == 8 || v == 32) return v;
+    if (v == 4 || v == 8 || v == 16 || v == 32) return v;
   }
   return S <= 256 * 2048 ? 8 : 32;
 }
@@ -466,10 +490,12 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   if (bits == 11)
     rc = ipt == 4 ? run_passes<4, 11>(a, passes, plan, L, st)
        : ipt == 8 ? run_passes<8, 11>(a, passes, plan, L, st)
+       : ipt == 16 ? run_passes<16, 11>(a, passes, plan, L, st)
                   : run_passes<32, 11>(a, passes, plan, L, st);
   else
     rc = ipt == 4 ? run_passes<4, 8>(a, passes, plan, L, st)
        : ipt == 8 ? run_passes<8, 8>(a, passes, plan, L, st)
+       : ipt == 16 ? run_passes<16, 8>(a, passes, plan, L, st)
                   : run_passes<32, 8>(a, passes, plan, L, st);
   if (rc != CTR_OK) return rc;
   const unsigned gs = (unsigned)ceil_div(S, kSegTile);

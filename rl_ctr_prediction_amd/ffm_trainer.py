@@ -111,6 +111,13 @@ class FusedFFMTrainer:
         self._graph_tab_version = self.step_table.version
         self.timing = None  # FusedCTRTrainer's bench hook: not instrumented here
 
+    def __del__(self):
+        try:  # a captured graph must not be destroyed while it still runs
+            if getattr(self, "_graphs", None):
+                torch.cuda.synchronize(self.device)
+        except Exception:  # interpreter shutdown
+            pass
+
     # ----------------------------------------------------------------- optimiser -----
     def _table_args(self):
         return (self.T, self.m_T, self.v_T, None, None, None, self.last_T)
@@ -196,6 +203,7 @@ class FusedFFMTrainer:
         if self.step_table.capacity < self.step_count + 2:
             self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
         if self._graph_tab_version != self.step_table.version:
+            torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
         key = (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),

@@ -68,7 +68,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         lo = min(self.rank * self.shard_rows, self.V)
         return lo, min(lo + self.shard_rows, self.V)
 
-    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
+    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
+             next_x: torch.Tensor | None = None) -> torch.Tensor:
+        """next_x: accepted for FusedCTRTrainer's interface; the sharded step builds its plan
+        in the step (its exchange sizes come from it)."""
         B, F = x.shape
         ws = self.world_size
         mean_div = float(global_batch if global_batch is not None else B * ws)

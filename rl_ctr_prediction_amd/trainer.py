@@ -55,7 +55,7 @@ _MLP_KINDS = ("DeepFM", "IPNN")
 class _Bufs:
     B: int
     fm: hip_ops.FMForward
-    plan: hip_ops.SparsePlanBuffers
+    plan: hip_ops.SparsePlanBuffers    # the plan of the step's batch
     grad_rows: torch.Tensor
     grad_lin: torch.Tensor
     h1: torch.Tensor | None = None
@@ -75,6 +75,7 @@ class _Bufs:
     g_lin: torch.Tensor | None = None
     dslot: torch.Tensor | None = None  # IPNN: per-slot embedding gradients [S, K]
     zero: torch.Tensor | None = None   # IPNN: the (absent) FM logit, zeros [B]
+    plan_own: hip_ops.SparsePlanBuffers | None = None  # the shape's plan without lookahead
 
 
 class FusedCTRTrainer:
@@ -159,6 +160,16 @@ class FusedCTRTrainer:
         env = os.environ.get("CTR_PLAN_FIRST")
         self.plan_first = (env == "1") if env in ("0", "1") else self.kind == "FM"
         self.keep_grads = False
+        # plan lookahead (step(..., next_x=)): the next batch's sparse plan is built on its
+        # own stream (own scratch workspace) concurrently with this step, OUTSIDE the step's
+        # graph (its own small graph), and the next step waits for it before it starts.
+        # Plans are kept per ids tensor (graphs hold their addresses), least recently used
+        # first out, never one a captured graph holds
+        self._plans: dict = {}
+        self._pinned_plans: set = set()
+        self._plan_graphs: dict = {}
+        self.max_plans = 16
+        self._pending: dict = {}  # ids key -> event of its plan built ahead, not yet used
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -178,7 +189,12 @@ class FusedCTRTrainer:
             w0, w1 = self.views["mlp.0.weight"], self.views["mlp.3.weight"]
             self._wplanes = (hip_ops.Planes(*w0.shape, self.device),
                              hip_ops.Planes(*w1.shape, self.device))
-        self._sweep_stream = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
+        # created on first use: every HIP stream takes one of the process's few hardware
+        # queues (GPU_MAX_HW_QUEUES = 4), and streams beyond that share queues in order
+        self._sweep_stream = None
+        self._plan_stream = None
+        if self._side is not None:
+            self._plan_stream = torch.cuda.Stream(device=self.device)
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -199,6 +215,15 @@ class FusedCTRTrainer:
         # recorded on the launch stream around those kernels; only the keys present in the
         # dict are instrumented (each event is a queue packet: keep the timed region lean)
         self.timing: dict | None = None
+
+    def __del__(self):
+        # a captured graph must not be destroyed while it still runs: plan-stream replays
+        # (lookahead) are not ordered before anything the caller synchronises with
+        try:
+            if getattr(self, "_graphs", None) or getattr(self, "_plan_graphs", None):
+                torch.cuda.synchronize(self.device)
+        except Exception:  # interpreter shutdown
+            pass
 
     def _table_rows(self) -> tuple[int, int]:
         return 0, self.V
@@ -312,6 +337,7 @@ class FusedCTRTrainer:
         S = B * F
         b = _Bufs(B=B, fm=fm, plan=hip_ops.SparsePlanBuffers(S, dev), grad_rows=e(S, K),
                   grad_lin=e(S), loss=e(1))
+        b.plan_own = b.plan
         if deep:
             mlp = self.model.mlp
             H1, H2 = mlp[0].out_features, mlp[3].out_features
@@ -334,9 +360,19 @@ class FusedCTRTrainer:
         return b
 
     # ------------------------------------------------------------------------ step ----
-    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None) -> torch.Tensor:
+    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
+             next_x=None) -> torch.Tensor:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
         batch's mean BCE as a 1-element device tensor (no host sync).
+
+        next_x (optional): the ids of the batch(es) the next step(s) will train on — one
+        tensor, or a sequence in step order. Their sparse plans (a pure function of the
+        ids) are built on a plan stream concurrently with this step (single process,
+        deferred mode), and the step that trains on one of them uses that plan instead of
+        building its own on its critical path. Two batches ahead hides the plan entirely:
+        its completion is then long past when the step waits for it (a cross-queue wait
+        that is still pending costs ~15 us). next_x must keep its contents until its step;
+        a step with other ids builds its plan as usual.
 
         The returned tensor is the trainer's persistent loss buffer for this batch shape
         (a captured HIP graph writes it in place): it is valid until the next step() with
@@ -350,13 +386,91 @@ class FusedCTRTrainer:
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
         self._sync_weight_planes()
+        xkey = self._xkey(x)
+        if next_x is None:
+            ahead = []
+        else:
+            ahead = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
+        if self._plan_stream is None or ws != 1:
+            ahead = []
+        ahead = [n for n in ahead if n.is_cuda and tuple(n.shape) == tuple(x.shape)
+                 and self._xkey(n) != xkey]
+        main = torch.cuda.current_stream()
+        ev = self._pending.pop(xkey, None)
+        have = ev is not None
+        if have:  # x's plan was built ahead
+            main.wait_event(ev)
+        keep = {self._xkey(n) for n in ahead}
+        for k in [k for k in self._pending if k not in keep]:
+            del self._pending[k]  # built for a batch that did not come next: unused
+        todo = [n for n in ahead if self._xkey(n) not in self._pending]
+        ev_start = None
+        if todo:
+            ev_start = torch.cuda.Event()
+            ev_start.record(main)  # everything before this step (earlier readers of the plans)
         if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
                 and y.dtype == torch.float32 and y.is_contiguous()):
-            return self._graph_step(x, y, mean_div)
-        self.step_table.ensure(self.step_count + 1)
-        loss = self._launch(x, y, mean_div)
-        self._after_step()
+            loss = self._graph_step(x, y, mean_div, have)
+        else:
+            self.step_table.ensure(self.step_count + 1)
+            loss = self._launch(x, y, mean_div, have)
+            self._after_step()
+        seen = set()
+        for n in todo:
+            k = self._xkey(n)
+            if k not in seen:
+                seen.add(k)
+                self._build_ahead(n, ev_start)
         return loss
+
+    def _build_ahead(self, nx: torch.Tensor, ev_start) -> None:
+        """The lookahead plan of ids nx on the plan stream, concurrent with the step just
+        enqueued (replayed from its own graph once captured)."""
+        ps = self._plan_stream
+        key = self._xkey(nx)
+        P = self._plan_for(nx)
+        ps.wait_event(ev_start)
+        nx.record_stream(ps)
+        with torch.cuda.stream(ps):
+            t = self._mark("plan")
+            g = self._plan_graphs.get(key)
+            if g is not None and self.timing is None:
+                g.replay()
+            else:
+                P.build(nx, self.V)
+                if (self.use_graphs and self.timing is None
+                        and len(self._plan_graphs) < self.max_plans):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self._graph_pool, stream=ps):
+                        P.build(nx, self.V)  # captured, not executed
+                    self._plan_graphs[key] = g
+                    self._pinned_plans.add(key)
+            self._span("plan", t)
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        self._pending[key] = ev
+
+    @staticmethod
+    def _xkey(x):
+        return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()))
+
+    def _plan_for(self, x) -> hip_ops.SparsePlanBuffers:
+        """The plan buffers of ids tensor x (lookahead); LRU, graph-held ones pinned."""
+        key = self._xkey(x)
+        p = self._plans.pop(key, None)
+        if p is None:
+            S = x.shape[0] * x.shape[1]
+            if len(self._plans) >= self.max_plans:
+                for k in list(self._plans):  # oldest first; reuse its buffers if big enough
+                    if k not in self._pinned_plans and k not in self._pending:
+                        old = self._plans.pop(k)
+                        if old.capacity >= S:
+                            p = old
+                        break
+            if p is None:
+                p = hip_ops.SparsePlanBuffers(S, self.device)
+        self._plans[key] = p  # most recently used last
+        return p
 
     def _weights_version(self):
         mlp = self.model.mlp
@@ -383,40 +497,53 @@ class FusedCTRTrainer:
         if self.deferred:
             self._dirty = True
 
-    def _graph_key(self, x, y, mean_div):
+    def _graph_key(self, x, y, mean_div, have=False):
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
         return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
-                tuple(y.shape), mean_div, self.model.training, drops)
+                tuple(y.shape), mean_div, self.model.training, drops,
+                self._xkey(x) if have else None)
 
-    def _graph_step(self, x, y, mean_div):
+    def _graph_step(self, x, y, mean_div, have=False):
         if self.step_table.capacity < self.step_count + 2:
             self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
         if self._graph_tab_version != self.step_table.version:
+            torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
-        key = self._graph_key(x, y, mean_div)
+        key = self._graph_key(x, y, mean_div, have)
         hit = self._graphs.get(key)
         if hit is None:
-            loss = self._launch(x, y, mean_div)  # the real step; also sizes every buffer
+            loss = self._launch(x, y, mean_div, have)  # the real step; sizes buffers
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self._graph_pool):
-                    self._launch(x, y, mean_div)  # captured, not executed
-                self._graphs[key] = (g, self._bufs)
+                    self._launch(x, y, mean_div, have)  # captured, not executed
+                if have:  # the graph reads x's lookahead plan buffers
+                    self._pinned_plans.add(self._xkey(x))
+                self._graphs[key] = (g, self._bufs, self._bufs.plan)
             return loss
-        g, self._bufs = hit  # the buffer set the graph was captured with
+        g, self._bufs, plan = hit  # the buffer set the graph was captured with
+        self._bufs.plan = plan
+        if have:
+            self._plan_for(x)  # LRU touch
         g.replay()
         self._after_step()
         return self._bufs.loss
 
-    def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float) -> torch.Tensor:
+    def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float,
+                have_plan: bool = False) -> torch.Tensor:
         """Enqueue one step. Changes no host state: step-dependent values come from
-        self.step_ctr (advanced on the device), so the launch sequence can be captured."""
+        self.step_ctr (advanced on the device), so the launch sequence can be captured.
+        have_plan: x's plan was built ahead (step(next_x=) of the previous step)."""
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
+        if have_plan:
+            b.plan = self._plan_for(x)
+        elif b.plan_own is not None:
+            b.plan = b.plan_own
         y = y.reshape(-1)
         if y.dtype != torch.float32:
             y = y.float()
@@ -437,8 +564,11 @@ class FusedCTRTrainer:
             main = torch.cuda.current_stream()
             ev0 = torch.cuda.Event()
             ev0.record(main)  # x ready; previous step's plan users and Adam done
+            ev_plan = torch.cuda.Event()
 
             def plan():
+                if have_plan:
+                    return  # built ahead: no fork
                 self._side.wait_event(ev0)
                 if not torch.cuda.is_current_stream_capturing():
                     x.record_stream(self._side)
@@ -446,6 +576,7 @@ class FusedCTRTrainer:
                     t_plan = self._mark("plan")
                     b.plan.build(x, self.V)
                     self._span("plan", t_plan)
+                    ev_plan.record()
 
             if self.plan_first:
                 plan()
@@ -478,8 +609,8 @@ class FusedCTRTrainer:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
         if self.kind == "FM":  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
-        if self._side is not None:
-            torch.cuda.current_stream().wait_stream(self._side)  # the plan
+        if self._side is not None and not have_plan:
+            torch.cuda.current_stream().wait_event(ev_plan)  # the plan
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         # one process, deferred Adam: the row sums are applied where they complete
@@ -557,8 +688,10 @@ class FusedCTRTrainer:
     def _fork_sweep(self) -> None:
         """Start this step's background sweep (after the catch-up: the batch's rows are
         current, so the sweep and the step touch disjoint rows)."""
-        if self._sweep_stream is None or not self.sweep_slices:
+        if not (self.deferred and self._vec_ok and self.sweep_slices):
             return
+        if self._sweep_stream is None:
+            self._sweep_stream = torch.cuda.Stream(device=self.device)
         self._sweep_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._sweep_stream):
             t = self._mark("sweep")
