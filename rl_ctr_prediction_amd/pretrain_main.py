@@ -127,8 +127,14 @@ def train(model, optimizer, data_loader, loss, device):
     model.train()
     total_loss = 0.0
     log_intervals = 0
-    for features, labels in data_loader:
-        train_loss = optimizer.step(features, labels)
+    batches = list(data_loader)  # views of the device-resident data: nothing is copied
+    lookahead = isinstance(optimizer, FusedCTRTrainer)
+    for i, (features, labels) in enumerate(batches):
+        if lookahead:  # the next two batches' sparse plans are built during this step
+            nxt = [b[0] for b in batches[i + 1:i + 3]]
+            train_loss = optimizer.step(features, labels, next_x=nxt)
+        else:
+            train_loss = optimizer.step(features, labels)
         total_loss += train_loss.item()
         log_intervals += 1
     optimizer.check_errors()

@@ -54,6 +54,17 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._side = None  # the exchange needs the plan before anything else
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+        # the plan and its per-owner counts are built on the plan stream (ahead of the step
+        # with next_x), and the counts all-to-all — the step's one host sync — runs there on
+        # a communicator of its own: the host then waits for the plan only, never for the
+        # previous step's kernels or collectives, and runs ahead of the GPU
+        if self._plan_stream is None:
+            self._plan_stream = torch.cuda.Stream(device=self.device)
+        self._count_group = None
+        if self.world_size > 1:
+            ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
+            self._count_group = dist.new_group(ranks=ranks)
+        self._ahead_counts: dict = {}
 
     def _buffers(self, B: int, F: int):
         b = super()._buffers(B, F)
@@ -69,9 +80,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         return lo, min(lo + self.shard_rows, self.V)
 
     def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-             next_x: torch.Tensor | None = None) -> torch.Tensor:
-        """next_x: accepted for FusedCTRTrainer's interface; the sharded step builds its plan
-        in the step (its exchange sizes come from it)."""
+             next_x=None) -> torch.Tensor:
+        """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches'
+        plans and per-owner counts are built on the plan stream during this step. Purely
+        local (no collective depends on it), so ranks may pass different next_x."""
         B, F = x.shape
         ws = self.world_size
         mean_div = float(global_batch if global_batch is not None else B * ws)
@@ -86,15 +98,39 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         has_lin = self.w_tab is not None  # InnerPNN: no linear table
 
         self._sync_weight_planes()
-        # 1. plan of the local batch, per-owner counts of its unique rows
+        main, ps = torch.cuda.current_stream(), self._plan_stream
+        xkey = self._xkey(x)
+        ahead = [] if next_x is None else (
+            [next_x] if isinstance(next_x, torch.Tensor) else list(next_x))
+        ahead = [n for n in ahead if n.is_cuda and n.dim() == 2 and n.shape[1] == F
+                 and self._xkey(n) != xkey]
+        ev_start = torch.cuda.Event()
+        ev_start.record(main)  # everything before this step (earlier readers of the plans)
+        # 1. plan of the local batch, per-owner counts of its unique rows (plan stream)
         t = self._mark("plan")
-        b.plan.build(x, self.V, err_flag=self.err)
-        b.plan.shard_counts(self.shard_rows, ws, out=self._counts)
+        keep = {self._xkey(n) for n in ahead} | {xkey}
+        for k in [k for k in self._pending if k not in keep]:
+            del self._pending[k]
+            self._ahead_counts.pop(k, None)
+        if self._pending.pop(xkey, None) is not None:  # built ahead (ps is in order)
+            plan, counts = self._plan_for(x), self._ahead_counts.pop(xkey)
+        else:
+            plan, counts = b.plan_own, self._counts
+            ps.wait_event(ev_start)
+            x.record_stream(ps)
+            with torch.cuda.stream(ps):
+                plan.build(x, self.V, err_flag=self.err)
+                plan.shard_counts(self.shard_rows, ws, out=counts)
+        b.plan = plan
+        with torch.cuda.stream(ps):
+            send_c, recv_c = exchange_counts(counts, self._count_group)
+            ev_plan = torch.cuda.Event()
+            ev_plan.record(ps)
+        main.wait_event(ev_plan)
         self._span("plan", t)
-        send_c, recv_c = exchange_counts(self._counts, self.group)
         # 2. unique row ids to their owners, as shard-local ids
         t = self._mark("exchange")
-        req = alltoallv(b.plan.unique_rows, send_c, recv_c, self.group)
+        req = alltoallv(plan.unique_rows, send_c, recv_c, self.group)
         hip_ops.ids_add_(req, -self.row_lo)
         self._span("exchange", t)
         # 3. owners: catch the rows up, send them back
@@ -114,7 +150,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             T_lin = alltoallv(lin, recv_c, send_c, self.group).view(-1)
         self._span("exchange", t)
         # 4. forward + backward over the compact table
-        ids = b.plan.slot_to_unique(out=self._slot2u)[:B * F].view(B, F)
+        ids = plan.slot_to_unique(out=self._slot2u)[:B * F].view(B, F)
         if self.kind == "FM":
             t = self._mark("gather")
             hip_ops.fm_forward(ids, T, T_lin, bias, want_sum=True, labels=y, mean_div=mean_div,
@@ -127,9 +163,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         t = self._mark("scatter")
         if self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
-            hip_ops.segment_sum_rows(b.plan, b.dslot, out=b.grad_rows)
+            hip_ops.segment_sum_rows(plan, b.dslot, out=b.grad_rows)
         else:
-            hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
+            hip_ops.fm_embedding_grad(plan, F, T, gz, b.fm.sum_e, b.dx, None,
                                       grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
         self._span("scatter", t)
         if self.kind != "FM":  # the dense-parameter gradients, on the weight-gradient stream
@@ -163,6 +199,21 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._adam_dense(self.step_count)
         self._join_sweep()
         hip_ops.step_end(self.step_ctr)
+        for n in ahead:  # the next batches' plans and counts, concurrent with this step
+            k = self._xkey(n)
+            if k in self._pending:
+                continue
+            P = self._plan_for(n)
+            c = torch.empty(ws, dtype=torch.int64, device=self.device)
+            ps.wait_event(ev_start)
+            n.record_stream(ps)
+            with torch.cuda.stream(ps):
+                P.build(n, self.V, err_flag=self.err)
+                P.shard_counts(self.shard_rows, ws, out=c)
+                ev = torch.cuda.Event()
+                ev.record(ps)
+            self._pending[k] = ev
+            self._ahead_counts[k] = c
         return b.loss
 
     def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor | None]:

@@ -55,8 +55,12 @@ def test_sharded_world1_equals_fused_bitwise(cuda, kind, V, K, B):
         m = _model(kind, V, F, K)
         kw = dict(optimizer_mode="deferred") if cls is P.FusedCTRTrainer else {}
         tr = cls(m, lr=1e-3, weight_decay=1e-5, seed=3, **kw)
-        losses = [tr.step(torch.tensor(x, device=cuda), torch.tensor(y, device=cuda)).item()
-                  for x, y in batches]
+        xs = [torch.tensor(x, device=cuda) for x, _ in batches]
+        ys = [torch.tensor(y, device=cuda) for _, y in batches]
+        # the sharded run builds its plans two batches ahead (next_x), the fused one in-step
+        losses = [tr.step(xs[i], ys[i], next_x=(xs[i + 1:i + 3] if cls is P.ShardedCTRTrainer
+                                                 else None)).item()
+                  for i in range(len(xs))]
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         st = tr.optimizer_state_dict()["state"]
         out[cls.__name__] = (losses, sd, st)
@@ -89,10 +93,13 @@ def _rank_main(rank, world, port, kind, V, F, K, B, steps, q, drop=0.0):
         m = _model(kind, V, F, K, drop=drop)
         tr = P.ShardedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3)
         losses = []
-        for x, y in CriteoSynth(V, F, seed=21).batches(steps, B * world):
-            xs = torch.tensor(x[rank * B:(rank + 1) * B], device="cuda:0")
-            ys = torch.tensor(y[rank * B:(rank + 1) * B], device="cuda:0")
-            losses.append(tr.step(xs, ys).item())
+        data = [(torch.tensor(x[rank * B:(rank + 1) * B], device="cuda:0"),
+                 torch.tensor(y[rank * B:(rank + 1) * B], device="cuda:0"))
+                for x, y in CriteoSynth(V, F, seed=21).batches(steps, B * world)]
+        for i, (xs, ys) in enumerate(data):
+            # rank 1 builds its plans ahead (next_x), rank 0 in-step: a local choice
+            nxt = [d[0] for d in data[i + 1:i + 3]] if rank == 1 else None
+            losses.append(tr.step(xs, ys, next_x=nxt).item())
         E, w = tr.gather_tables()
         dense = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()
                  if k not in ("feature_embedding.weight", "linear.weight")}
