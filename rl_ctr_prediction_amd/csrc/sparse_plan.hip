@@ -4,7 +4,7 @@
 // rows in ascending order and their segment offsets — bit-identical to numpy's stable
 // argsort + unique (tests/test_gpu_kernels.py).
 //
-// LSD radix sort, 8- or 11-bit digits (plan_bits), two launches per pass and no
+// LSD radix sort, 8- or 10-bit digits (plan_bits; 11 for A/B runs), two launches per pass and no
 // inter-workgroup hand-off inside a launch (a cross-XCD look-back chain costs ~1 us per hop
 // on gfx950; a kernel boundary ~1.5 us):
 //   radix_hist:    per tile (256 threads x IPT keys) the 256-bin digit histogram, LDS
@@ -106,7 +106,8 @@ __device__ __forceinline__ int32_t block_exclusive_scan(int32_t v, int32_t* wave
 template <int IPT, bool FIRST, bool LAST, int BITS>
 __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a) {
   constexpr int R = Radix<BITS>::kBins, DPT = Radix<BITS>::kDPT;
-  constexpr int G = (R <= 256) ? (IPT < 8 ? IPT : 8) : 1;  // item rows ranked together
+  // item rows ranked together (the two LDS count arrays stay <= 32 KB each)
+  constexpr int G = (R <= 256) ? (IPT < 8 ? IPT : 8) : (R <= 1024 ? 2 : 1);
   static_assert(IPT % G == 0, "IPT must be a multiple of the ranking group");
   __shared__ int32_t s_base[R];                   // global base of each digit for this tile
   __shared__ int32_t s_run[R];                    // digits ranked in earlier groups
@@ -367,11 +368,11 @@ static int plan_ipt(int64_t S) {
 static int plan_bits(int64_t V) {
   if (const char* env = getenv("CTR_PLAN_BITS")) {  // A/B runs
     const int b = atoi(env);
-    if (b == 8 || b == 11) return b;
+    if (b == 8 || b == 10 || b == 11) return b;
   }
-  // measured on MI355X (C2: S = 106k, V = 1M): two 11-bit passes lose to three 8-bit ones —
-  // the 2048-bin scatter takes 22-25 us against 13-16 (tools/plan_ab.sh), more than the
-  // launch it saves; 11 bits stay available for A/B runs
+  // 8 bits: measured on MI355X (tools/plan_ab2.sh, us per plan), wider digits save a pass
+  // but each pass costs more than the pass saved — 10 bits: C2 (V = 1M, 2 vs 3 passes)
+  // 53.7 vs 55.0, C5 (V = 40M, 3 vs 4 passes) 85.0 vs 75.6; 11 bits: C2 69
   (void)V;
   return 8;
 }
@@ -487,7 +488,12 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   const int bits = plan_bits(V);
   const int passes = (int)ceil_div(key_bits(V), bits);
   int rc;
-  if (bits == 11)
+  if (bits == 10)
+    rc = ipt == 4 ? run_passes<4, 10>(a, passes, plan, L, st)
+       : ipt == 8 ? run_passes<8, 10>(a, passes, plan, L, st)
+       : ipt == 16 ? run_passes<16, 10>(a, passes, plan, L, st)
+                  : run_passes<32, 10>(a, passes, plan, L, st);
+  else if (bits == 11)
     rc = ipt == 4 ? run_passes<4, 11>(a, passes, plan, L, st)
        : ipt == 8 ? run_passes<8, 11>(a, passes, plan, L, st)
        : ipt == 16 ? run_passes<16, 11>(a, passes, plan, L, st)
