@@ -30,6 +30,7 @@ import torch.nn as nn
 
 from . import hip_ops
 from .p_model import FFM
+from .trainer import flush_hooks, graph_capture
 
 
 @dataclass
@@ -99,8 +100,7 @@ class FusedFFMTrainer:
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_count = 0
         self._dirty = False
-        model.register_forward_pre_hook(lambda mod, inp: self.flush())
-        model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars: self.flush())
+        flush_hooks(model, self)
         self._bufs: _FFMBufs | None = None
         self._bufsets: dict = {}
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
@@ -214,7 +214,7 @@ class FusedFFMTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self._graph_pool):
+                with graph_capture(g, pool=self._graph_pool):
                     self._launch(x, y)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
             return loss

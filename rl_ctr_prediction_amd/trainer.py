@@ -26,7 +26,10 @@ Optimizer modes (identical results, bitwise — tests/test_gpu_deferred.py):
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -35,6 +38,35 @@ import torch.nn as nn
 from . import hip_ops
 from .distributed import allgather_sparse_rows, allreduce_sum_, world
 from .p_model import FM, DeepFM, InnerPNN
+
+
+@contextlib.contextmanager
+def graph_capture(g, **kw):
+    """torch.cuda.graph with Python's cyclic GC paused: a collection during the capture
+    could destroy another trainer's captured graphs (HIP calls that are illegal while a
+    stream captures -> abort)."""
+    gc.collect()  # dead cycles holding captured graphs die here, outside any capture
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()
+
+
+def flush_hooks(model: nn.Module, trainer) -> None:
+    """forward / state_dict pre-hooks that flush the trainer's deferred rows, holding the
+    trainer weakly (no model <-> trainer cycle: a dropped trainer is freed at once)."""
+    ref = weakref.ref(trainer)
+
+    def flush(*_):
+        t = ref()
+        if t is not None:
+            t.flush()
+    model.register_forward_pre_hook(flush)
+    model.register_state_dict_pre_hook(flush)
 
 
 class _nullctx:
@@ -198,8 +230,7 @@ class FusedCTRTrainer:
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
-            model.register_forward_pre_hook(lambda mod, inp: self.flush())
-            model.register_state_dict_pre_hook(lambda mod, prefix, keep_vars: self.flush())
+            flush_hooks(model, self)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.step_count = 0
         self._bufs: _Bufs | None = None
@@ -441,7 +472,7 @@ class FusedCTRTrainer:
                 if (self.use_graphs and self.timing is None
                         and len(self._plan_graphs) < self.max_plans):
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=self._graph_pool, stream=ps):
+                    with graph_capture(g, pool=self._graph_pool, stream=ps):
                         P.build(nx, self.V)  # captured, not executed
                     self._plan_graphs[key] = g
                     self._pinned_plans.add(key)
@@ -518,7 +549,7 @@ class FusedCTRTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self._graph_pool):
+                with graph_capture(g, pool=self._graph_pool):
                     self._launch(x, y, mean_div, have)  # captured, not executed
                 if have:  # the graph reads x's lookahead plan buffers
                     self._pinned_plans.add(self._xkey(x))
