@@ -581,8 +581,9 @@ def main():
                        " (replicated tables, sparse row-grad all-gather)" if world > 1 else ""),
                    "optimizer": f"dense Adam lr=1e-3 wd=1e-5 (reference semantics), "
                                 f"{args.optimizer} mode",
-                   "plan_lookahead": (args.lookahead if world == 1 and args.optimizer == "deferred"
-                                      else 0)},
+                   "plan_lookahead": (args.lookahead if isinstance(trainer, ShardedCTRTrainer)
+                                      or (getattr(trainer, "plan_lookahead", False)
+                                          and args.optimizer == "deferred") else 0)},
         "roofline": roofline,
         "kernels": kernels,
         "gather_scatter": {

@@ -202,6 +202,12 @@ class FusedCTRTrainer:
         self._plan_graphs: dict = {}
         self.max_plans = 16
         self._pending: dict = {}  # ids key -> event of its plan built ahead, not yet used
+        # lookahead pays where the plan is the step's critical path (FM: C2 35.5 -> 50.9 M
+        # ex/s); the MLP kinds build it on the graph's side list under the catch-up and the
+        # forward, where it finishes long before the scatter needs it, while a lookahead plan
+        # runs under dX / the scatter and slows them (C3 12.8 vs 12.7 M ex/s)
+        env = os.environ.get("CTR_PLAN_LOOKAHEAD")
+        self.plan_lookahead = (env == "1") if env in ("0", "1") else self.kind == "FM"
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -422,7 +428,7 @@ class FusedCTRTrainer:
             ahead = []
         else:
             ahead = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
-        if self._plan_stream is None or ws != 1:
+        if self._plan_stream is None or ws != 1 or not self.plan_lookahead:
             ahead = []
         ahead = [n for n in ahead if n.is_cuda and tuple(n.shape) == tuple(x.shape)
                  and self._xkey(n) != xkey]
@@ -828,7 +834,10 @@ class FusedCTRTrainer:
                               out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
             if side is not None:  # from dX on
                 side.wait_event(b.ev_dx)
-            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X
+            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X. The column sum stays here:
+            # it lets seg_chunk take the CUs before dW0 does (measured at C3 with db0 moved
+            # before the dX fork: dW0 and seg_chunk start together, seg_chunk 38 -> 106 us,
+            # the step +20 us)
             hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
             self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B, out=gv["mlp.0.weight"])
 

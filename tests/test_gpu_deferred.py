@@ -226,6 +226,7 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
             m.feature_embedding.weight.mul_(0.05)
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7)
         tr.use_graphs = graphs
+        tr.plan_lookahead = True  # default for FM only; exercised for every kind here
         losses = []
         for j, (i, n) in enumerate(order):
             nxt = xs[n] if (ahead and n is not None) else None
