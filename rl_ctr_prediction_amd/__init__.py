@@ -6,10 +6,11 @@ running on hand-written gfx950 HIP kernels behind the C ABI in include/ctr_hip.h
 """
 from .feature_embedding import Feature_Embedding
 from .ffm_trainer import FusedFFMTrainer
+from .optim import DenseAdam
 from .p_model import FFM, FM, DeepFM, InnerPNN
 from .pg_model import Net, PolicyGradient
 from .sharded import ShardedCTRTrainer
 from .trainer import FusedCTRTrainer
 
 __all__ = ["FM", "FFM", "DeepFM", "InnerPNN", "Feature_Embedding", "Net", "PolicyGradient", "FusedCTRTrainer",
-           "FusedFFMTrainer", "ShardedCTRTrainer"]
+           "FusedFFMTrainer", "ShardedCTRTrainer", "DenseAdam"]
