@@ -371,6 +371,23 @@ int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float*
                                   const int32_t* step_ptr, const float* step_table, double beta1,
                                   double beta2, double eps, double weight_decay,
                                   ctr_stream_t stream);
+/* Catch-up AHEAD of the next batch (FusedCTRTrainer.step(next_x=...)): while the current
+ * batch's step runs, the next batch's rows that the current batch does NOT touch are
+ * brought to *step_ptr (the step in flight: it gives them g = wd*p, which it would) — those
+ * rows are disjoint from everything the current step reads or writes, so the two run
+ * concurrently, and the next step needs no catch-up. `tag` is a caller-owned int32[V]
+ * scratch (no initialisation), `tag_value` a negative value never passed before with this
+ * tag array (the current batch's rows are tagged with it and skipped). Needs K % 4 == 0 and
+ * (K/4) | 64.
+ * Replaces: part of optimizer.step (all_main/pretrain_main.py:78) for the rows of the
+ * next batch, moved ahead in time (deferred-exact: same arithmetic, same order per row). */
+int ctr_adam_deferred_catchup_ahead(float* emb, float* m_emb, float* v_emb, float* lin,
+                                    float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
+                                    const void* idx_cur, int idx_type_cur, int64_t S_cur,
+                                    const void* idx_next, int idx_type_next, int64_t S_next,
+                                    int32_t* tag, int32_t tag_value, const int32_t* step_ptr,
+                                    const float* step_table, double beta1, double beta2,
+                                    double eps, double weight_decay, ctr_stream_t stream);
 /* Fused scatter + deferred Adam (ws == 1, deferred mode): the segmented row sums of
  * ctr_fm_embedding_grad / ctr_segment_sum_rows with ctr_adam_deferred_rows(the sums,
  * step = *step_ptr) folded into the pass that finishes the rows spanning several chunks —

@@ -124,6 +124,9 @@ SIGNATURES = {
     "ctr_adam_deferred_catchup_ids": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
                                              _i32, _i64, _vp, _vp, _vp, _f64, _f64, _f64, _f64,
                                              _vp]),
+    "ctr_adam_deferred_catchup_ahead": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp,
+                                               _vp, _i32, _i64, _vp, _i32, _i64, _vp, _i32, _vp,
+                                               _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_step_begin": (_i32, [_vp, _vp]),
     "ctr_step_end": (_i32, [_vp, _vp]),
     "ctr_adam_deferred_sweep": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32,

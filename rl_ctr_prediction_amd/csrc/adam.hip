@@ -269,6 +269,35 @@ __global__ __launch_bounds__(256) void deferred_mark_kernel(const IdxT* __restri
     owner[load_row(idx, s, V, nullptr)] = (int32_t)s;
 }
 
+// Catch-up AHEAD (ctr_adam_deferred_catchup_ahead): the next batch's rows that the current
+// batch does not touch, brought to the current step while it runs. `tag` (int32[V], caller
+// scratch, no initialisation) first gets a per-call negative value at the current batch's
+// rows, then every next-batch slot whose row does not carry it stores its index there (one
+// survives, as in deferred_mark_kernel); the surviving slot replays the row. Slot indices are
+// >= 0 and the tag value < 0, so rows of the current batch are never replayed here (they get
+// their gradient at this step), and stale tags of earlier calls never match.
+template <typename IdxT>
+__global__ __launch_bounds__(256) void deferred_tag_kernel(const IdxT* __restrict__ idx,
+                                                           int64_t S, int64_t V,
+                                                           int32_t* __restrict__ tag,
+                                                           int32_t value) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x)
+    tag[load_row(idx, s, V, nullptr)] = value;
+}
+
+template <typename IdxT>
+__global__ __launch_bounds__(256) void deferred_mark_excl_kernel(const IdxT* __restrict__ idx,
+                                                                 int64_t S, int64_t V,
+                                                                 int32_t* __restrict__ tag,
+                                                                 int32_t exclude) {
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = load_row(idx, s, V, nullptr);
+    if (tag[r] != exclude) tag[r] = (int32_t)s;
+  }
+}
+
 template <typename IdxT, int K4>
 __global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
     float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
@@ -841,6 +870,12 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
   return CTR_OK;
 }
 
+static int launch_catchup_wave(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                               float* v_lin, int64_t V, int K, int32_t* last, const void* idx,
+                               int idx_type, int64_t S, const int32_t* owner,
+                               const int32_t* step_ptr, const float* step_table, AdamHP h,
+                               hipStream_t st, int64_t max_blocks = 8192);
+
 extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float* lin,
                                              float* m_lin, float* v_lin, int64_t V, int K,
                                              int32_t* last, const void* idx, int idx_type,
@@ -868,9 +903,68 @@ extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_
     hipLaunchKernelGGL(deferred_mark_kernel<int32_t>, gm, 256, 0, st,
                        static_cast<const int32_t*>(idx), S, V, owner);
   CTR_LAUNCH_CHECK("deferred_mark_kernel");
+  return launch_catchup_wave(emb, m_emb, v_emb, lin, m_lin, v_lin, V, K, last, idx, idx_type, S,
+                             owner, step_ptr, step_table, h, st);
+}
+
+extern "C" int ctr_adam_deferred_catchup_ahead(
+    float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin, float* v_lin, int64_t V,
+    int K, int32_t* last, const void* idx_cur, int idx_type_cur, int64_t S_cur,
+    const void* idx_next, int idx_type_next, int64_t S_next, int32_t* tag, int32_t tag_value,
+    const int32_t* step_ptr, const float* step_table, double beta1, double beta2, double eps,
+    double weight_decay, ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && tag && step_ptr && step_table &&
+                  (idx_cur || S_cur == 0) && (idx_next || S_next == 0),
+              "ctr_adam_deferred_catchup_ahead: null pointer");
+  CTR_REQUIRE(tag_value < 0, "ctr_adam_deferred_catchup_ahead: tag_value must be negative");
+  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && K > 0 && S_cur >= 0 && S_next >= 0 &&
+                  S_cur < (int64_t(1) << 31) && S_next < (int64_t(1) << 31),
+              "ctr_adam_deferred_catchup_ahead: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_catchup_ahead: linear table pointers must be all set or all NULL");
+  CTR_REQUIRE((idx_type_cur == CTR_IDX_I32 || idx_type_cur == CTR_IDX_I64) &&
+                  (idx_type_next == CTR_IDX_I32 || idx_type_next == CTR_IDX_I64),
+              "ctr_adam_deferred_catchup_ahead: bad idx_type");
+  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, nullptr),
+              "ctr_adam_deferred_catchup_ahead: needs K %% 4 == 0, (K/4) | 64 and 16-B rows");
+  if (S_next == 0) return CTR_OK;
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipStream_t st = as_stream(stream);
+  if (S_cur > 0) {
+    const unsigned gc = (unsigned)std::min<int64_t>(ceil_div(S_cur, 256), 256);
+    if (idx_type_cur == CTR_IDX_I64)
+      hipLaunchKernelGGL(deferred_tag_kernel<int64_t>, gc, 256, 0, st,
+                         static_cast<const int64_t*>(idx_cur), S_cur, V, tag, tag_value);
+    else
+      hipLaunchKernelGGL(deferred_tag_kernel<int32_t>, gc, 256, 0, st,
+                         static_cast<const int32_t*>(idx_cur), S_cur, V, tag, tag_value);
+    CTR_LAUNCH_CHECK("deferred_tag_kernel");
+  }
+  const unsigned gn = (unsigned)std::min<int64_t>(ceil_div(S_next, 256), 256);
+  if (idx_type_next == CTR_IDX_I64)
+    hipLaunchKernelGGL(deferred_mark_excl_kernel<int64_t>, gn, 256, 0, st,
+                       static_cast<const int64_t*>(idx_next), S_next, V, tag, tag_value);
+  else
+    hipLaunchKernelGGL(deferred_mark_excl_kernel<int32_t>, gn, 256, 0, st,
+                       static_cast<const int32_t*>(idx_next), S_next, V, tag, tag_value);
+  CTR_LAUNCH_CHECK("deferred_mark_excl_kernel");
+  // a small grid: the replay trickles along beside the step's kernels instead of taking
+  // every CU ahead of them (CTR_CATCHUP_AHEAD_BLOCKS for A/B runs)
+  int64_t cap = 64;
+  if (const char* env = getenv("CTR_CATCHUP_AHEAD_BLOCKS")) cap = std::max(1, atoi(env));
+  return launch_catchup_wave(emb, m_emb, v_emb, lin, m_lin, v_lin, V, K, last, idx_next,
+                             idx_type_next, S_next, tag, step_ptr, step_table, h, st, cap);
+}
+
+static int launch_catchup_wave(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
+                               float* v_lin, int64_t V, int K, int32_t* last, const void* idx,
+                               int idx_type, int64_t S, const int32_t* owner,
+                               const int32_t* step_ptr, const float* step_table, AdamHP h,
+                               hipStream_t st, int64_t max_blocks) {
   const int K4 = K / 4;
   // one lane per slot: S / 256 blocks of 4 waves (a wave re-loops when S exceeds the grid)
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(S, 256), 8192));
+  const unsigned grid =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(S, 256), max_blocks));
 #define CTR_CATCHUP(IT, K4_)                                                                   \
   hipLaunchKernelGGL((deferred_catchup_wave<IT, K4_, 2>), grid, 256, 0, st,                    \
                      reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),         \

@@ -665,6 +665,26 @@ def adam_deferred_catchup_ids(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx: t
                                       float(eps), float(weight_decay), _stream())
 
 
+def adam_deferred_catchup_ahead(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx_cur: torch.Tensor,
+                                idx_next: torch.Tensor, tag: torch.Tensor, tag_value: int,
+                                step_dev: torch.Tensor, table: AdamStepTable, step_hint: int,
+                                betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> None:
+    """Bring the rows of idx_next that idx_cur does not hold to the step in step_dev (device
+    int32) — the catch-up of the next step, run while the current one executes. tag: an
+    int32[V] scratch; tag_value: negative, never reused with this tag array."""
+    V, K = emb.shape
+    ic, itc = _idx(idx_cur)
+    inx, itn = _idx(idx_next)
+    if tag.dtype != torch.int32 or tag.numel() < V:
+        raise ValueError("adam_deferred_catchup_ahead: tag must be int32[V]")
+    tab = table.ensure(max(step_hint, 1))
+    lib.ctr_adam_deferred_catchup_ahead(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin),
+                                        _p(v_lin), V, K, _p(last), _p(ic), itc, ic.numel(),
+                                        _p(inx), itn, inx.numel(), _p(tag), int(tag_value),
+                                        _p(step_dev), _p(tab), float(betas[0]), float(betas[1]),
+                                        float(eps), float(weight_decay), _stream())
+
+
 def step_begin(step_ctr: torch.Tensor) -> None:
     """ctr[1] = ctr[0] + 1 on the device (int32[2]: completed steps, step in flight)."""
     lib.ctr_step_begin(_p(step_ctr), _stream())

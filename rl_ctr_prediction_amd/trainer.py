@@ -208,6 +208,18 @@ class FusedCTRTrainer:
         # runs under dX / the scatter and slows them (C3 12.8 vs 12.7 M ex/s)
         env = os.environ.get("CTR_PLAN_LOOKAHEAD")
         self.plan_lookahead = (env == "1") if env in ("0", "1") else self.kind == "FM"
+        # catch-up ahead (step(next_x=)): the next batch's rows that this batch does not touch
+        # are brought to this step on the plan stream while it runs (_catchup_ahead). Off by
+        # default: bitwise correct, but measured slower on MI355X — the replay beside the
+        # step's GEMMs costs the step more than the catch-up it removes (C3 0.68 -> 0.75 ms
+        # per step with the full grid, 0.80 with 64 blocks, 1.05 with 16; IPNN likewise)
+        env = os.environ.get("CTR_CATCHUP_AHEAD")
+        self.catchup_ahead = env == "1"
+        self._ca_stream = None
+        self._tag = None
+        self._tag_seq = 0
+        self._ca_step = None
+        self._ca_pending: dict = {}
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -307,6 +319,10 @@ class FusedCTRTrainer:
     # ----------------------------------------------------------------- optimiser -----
     def flush(self) -> None:
         """Bring every embedding row up to the last completed step (deferred mode)."""
+        main = torch.cuda.current_stream()
+        for st in (self._ca_stream, self._plan_stream):  # work that runs beside the steps
+            if st is not None:
+                main.wait_stream(st)
         if self.deferred and self._dirty and self.step_count > 0:
             t = self._mark("flush")
             hip_ops.adam_deferred_flush(self.E_tab, self.m_E, self.v_E,
@@ -424,34 +440,43 @@ class FusedCTRTrainer:
         mean_div = float(global_batch if global_batch is not None else B * ws)
         self._sync_weight_planes()
         xkey = self._xkey(x)
-        if next_x is None:
-            ahead = []
+        if next_x is None or self._plan_stream is None or ws != 1:
+            nxts = []
         else:
-            ahead = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
-        if self._plan_stream is None or ws != 1 or not self.plan_lookahead:
-            ahead = []
-        ahead = [n for n in ahead if n.is_cuda and tuple(n.shape) == tuple(x.shape)
-                 and self._xkey(n) != xkey]
+            nxts = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
+        nxts = [n for n in nxts if n.is_cuda and tuple(n.shape) == tuple(x.shape)
+                and self._xkey(n) != xkey]
+        ahead = nxts if self.plan_lookahead else []
+        ca_next = nxts[0] if (self.catchup_ahead and nxts) else None
         main = torch.cuda.current_stream()
         ev = self._pending.pop(xkey, None)
         have = ev is not None
         if have:  # x's plan was built ahead
             main.wait_event(ev)
+        # x's rows were caught up during the previous step (have_ca). A catch-up made for a
+        # batch that did not come next is harmless (its rows just replayed earlier) but may
+        # share rows with x: every pending one completes before this step starts
+        have_ca = xkey in self._ca_pending
+        for ev_ca in self._ca_pending.values():
+            main.wait_event(ev_ca)
+        self._ca_pending.clear()
         keep = {self._xkey(n) for n in ahead}
         for k in [k for k in self._pending if k not in keep]:
             del self._pending[k]  # built for a batch that did not come next: unused
         todo = [n for n in ahead if self._xkey(n) not in self._pending]
         ev_start = None
-        if todo:
+        if todo or ca_next is not None:
             ev_start = torch.cuda.Event()
             ev_start.record(main)  # everything before this step (earlier readers of the plans)
         if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
                 and y.dtype == torch.float32 and y.is_contiguous()):
-            loss = self._graph_step(x, y, mean_div, have)
+            loss = self._graph_step(x, y, mean_div, have, have_ca)
         else:
             self.step_table.ensure(self.step_count + 1)
-            loss = self._launch(x, y, mean_div, have)
+            loss = self._launch(x, y, mean_div, have, have_ca)
             self._after_step()
+        if ca_next is not None:
+            self._catchup_ahead(x, ca_next, ev_start)
         seen = set()
         for n in todo:
             k = self._xkey(n)
@@ -459,6 +484,40 @@ class FusedCTRTrainer:
                 seen.add(k)
                 self._build_ahead(n, ev_start)
         return loss
+
+    def _catchup_ahead(self, x: torch.Tensor, nx: torch.Tensor, ev_start) -> None:
+        """The rows of nx that x does not hold, brought to the step just enqueued (it gives
+        them g = wd*p) on their own stream while that step runs: disjoint from every row the
+        step touches (ctr_adam_deferred_catchup_ahead), so the step that trains on nx needs no
+        catch-up. Eager launches: the target step and the tag are host values."""
+        if self._tag is None:
+            # zeros: a slot-index-like value that no tag value (always < 0) matches
+            self._tag = torch.zeros(self.V_tab, dtype=torch.int32, device=self.device)
+            self._ca_step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # the plan stream: a fourth stream would share one of the process's four hardware
+        # queues with the step (measured: C3 12.0 -> 10.9 M ex/s on a stream of its own)
+        cs = self._ca_stream = self._plan_stream
+        self._tag_seq += 1
+        if self._tag_seq >= 2**31 - 1:  # tag values are -seq: start over on a clean array
+            self._tag_seq = 1
+            with torch.cuda.stream(cs):
+                self._tag.zero_()
+        cs.wait_event(ev_start)
+        x.record_stream(cs)
+        nx.record_stream(cs)
+        m = self.model
+        w = m.linear.weight.data if self.kind != "IPNN" else None
+        with torch.cuda.stream(cs):
+            t = self._mark("adam")
+            self._ca_step.fill_(self.step_count)  # the step just enqueued
+            hip_ops.adam_deferred_catchup_ahead(
+                m.feature_embedding.weight.data, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                self.last, x, nx, self._tag, -self._tag_seq, self._ca_step, self.step_table,
+                self.step_count, self.betas, self.eps, self.weight_decay)
+            self._span("adam", t)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self._ca_pending[self._xkey(nx)] = ev
 
     def _build_ahead(self, nx: torch.Tensor, ev_start) -> None:
         """The lookahead plan of ids nx on the plan stream, concurrent with the step just
@@ -534,29 +593,29 @@ class FusedCTRTrainer:
         if self.deferred:
             self._dirty = True
 
-    def _graph_key(self, x, y, mean_div, have=False):
+    def _graph_key(self, x, y, mean_div, have=False, have_ca=False):
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
         return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
                 tuple(y.shape), mean_div, self.model.training, drops,
-                self._xkey(x) if have else None)
+                self._xkey(x) if have else None, have_ca)
 
-    def _graph_step(self, x, y, mean_div, have=False):
+    def _graph_step(self, x, y, mean_div, have=False, have_ca=False):
         if self.step_table.capacity < self.step_count + 2:
             self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
         if self._graph_tab_version != self.step_table.version:
             torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
-        key = self._graph_key(x, y, mean_div, have)
+        key = self._graph_key(x, y, mean_div, have, have_ca)
         hit = self._graphs.get(key)
         if hit is None:
-            loss = self._launch(x, y, mean_div, have)  # the real step; sizes buffers
+            loss = self._launch(x, y, mean_div, have, have_ca)  # the real step; sizes buffers
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, pool=self._graph_pool):
-                    self._launch(x, y, mean_div, have)  # captured, not executed
+                    self._launch(x, y, mean_div, have, have_ca)  # captured, not executed
                 if have:  # the graph reads x's lookahead plan buffers
                     self._pinned_plans.add(self._xkey(x))
                 self._graphs[key] = (g, self._bufs, self._bufs.plan)
@@ -570,7 +629,7 @@ class FusedCTRTrainer:
         return self._bufs.loss
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float,
-                have_plan: bool = False) -> torch.Tensor:
+                have_plan: bool = False, have_ca: bool = False) -> torch.Tensor:
         """Enqueue one step. Changes no host state: step-dependent values come from
         self.step_ctr (advanced on the device), so the launch sequence can be captured.
         have_plan: x's plan was built ahead (step(next_x=) of the previous step)."""
@@ -617,12 +676,13 @@ class FusedCTRTrainer:
 
             if self.plan_first:
                 plan()
-            t = self._mark("adam")
-            hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                                              self.last, x, self.rowmap, self.step_done,
-                                              self.step_table, step_hint, self.betas,
-                                              self.eps, self.weight_decay)
-            self._span("adam", t)
+            if not have_ca:  # else: caught up during the previous step (_catchup_ahead)
+                t = self._mark("adam")
+                hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                                                  self.last, x, self.rowmap, self.step_done,
+                                                  self.step_table, step_hint, self.betas,
+                                                  self.eps, self.weight_decay)
+                self._span("adam", t)
             if not self.plan_first:
                 plan()
             self._fork_sweep()

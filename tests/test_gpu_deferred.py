@@ -202,7 +202,8 @@ def test_c3_full_size_deferred_equals_dense_20_steps(cuda):
                                         ("IPNN", 100_000, 16, 512)])
 def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     """step(x, y, next_x=...) builds the next batches' plans during this step (one or two
-    ahead, the second one a guess the order sometimes breaks): bitwise the same
+    ahead, the second one a guess the order sometimes breaks) and catches the next batch's
+    rows up while it runs (catch-up ahead): bitwise the same
     losses, tables and moments as building every plan in its own step — over graph captures
     and replays, a lookahead the next step does not use (order changed), next_x == x, a step
     without next_x in between, and eager (no-graph) steps."""
@@ -217,7 +218,10 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     order = [(0, 1), (1, 2), (2, 0), (0, 1), (1, 2), (2, 0), (0, 2), (1, 1), (1, None),
              (2, 0), (0, 1), (1, 2), (2, 0), (0, 1)]
     out = []
-    for ahead, graphs in ((0, True), (1, True), (2, True), (2, False)):
+    # (batches ahead, HIP graphs, plan lookahead, catch-up ahead)
+    for ahead, graphs, pla, ca in ((0, True, False, False), (1, True, True, True),
+                                   (2, True, True, True), (2, False, True, True),
+                                   (2, True, False, True), (1, True, True, False)):
         torch.manual_seed(8)
         with torch.device(cuda):
             m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
@@ -226,7 +230,8 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
             m.feature_embedding.weight.mul_(0.05)
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7)
         tr.use_graphs = graphs
-        tr.plan_lookahead = True  # default for FM only; exercised for every kind here
+        tr.plan_lookahead = pla  # default: FM only; exercised for every kind here
+        tr.catchup_ahead = ca
         losses = []
         for j, (i, n) in enumerate(order):
             nxt = xs[n] if (ahead and n is not None) else None
