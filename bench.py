@@ -225,8 +225,18 @@ def bench_pg(args, cfg, world, rank, dev):
         trans_a = a[2] if len(a) > 2 else kw.get("trans_a", False)
         return 2.0 * res.shape[0] * res.shape[1] * (a[0].shape[0] if trans_a else a[0].shape[1])
 
-    # hip_ops.linear calls hip_ops.gemm through the module, so wrapping gemm sees every launch
+    def planes_flops(res, a, kw):  # hip_ops.gemm_planes(A, B, a_rc, b_rc, out=...)
+        A, Bp, a_rc, b_rc = a[0], a[1], a[2], a[3]
+        M, K = (A.cols, A.rows) if a_rc else (A.rows, A.cols)
+        N = Bp.cols if b_rc else Bp.rows
+        return 2.0 * M * N * K
+
+    # hip_ops.linear calls hip_ops.gemm through the module, so wrapping gemm sees every launch;
+    # the breakdown runs eagerly (a graph replay cannot carry timing events)
+    real_planes = hip_ops.gemm_planes
     hip_ops.gemm = timed(real_gemm, gemm_flops)
+    hip_ops.gemm_planes = timed(real_planes, planes_flops)
+    pg.use_graphs = False
     fe_ev = []
     real_fe = hip_ops.feature_embedding
 
@@ -246,6 +256,8 @@ def bench_pg(args, cfg, world, rank, dev):
         torch.cuda.synchronize()
     finally:
         hip_ops.gemm, hip_ops.feature_embedding = real_gemm, real_fe
+        hip_ops.gemm_planes = real_planes
+        pg.use_graphs = True
 
     if world > 1:
         dist.barrier()
@@ -282,7 +294,9 @@ def bench_pg(args, cfg, world, rank, dev):
                        " (one episode split over the ranks: reward all-gather, gradient "
                        "all-reduce)" if world > 1 else ""),
                    "optimizer": "Adam lr=1e-4 wd=1e-5 (PG_model.py:87)"},
-        "roofline": {"kernel": "gemm_f32_kernel (policy MLP fwd + bwd, averaged per launch)",
+        "roofline": {"kernel": "policy MLP GEMMs fwd + bwd, averaged per launch "
+                               "(gemm_planes_kernel on the 741-1024-512-256 layers, "
+                               "ctr_gemm_f32_ex on the 256-128-A tail)",
                      "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
                      "algorithmic_flops_per_launch": flops, "traffic": None,
@@ -291,7 +305,9 @@ def bench_pg(args, cfg, world, rank, dev):
                                "un-timed learn() calls before the timed region"},
         "kernels": {"feature_embedding_kernel": {"ms_per_call": fe_ms,
                                                  "GBps": fe_bytes / (fe_ms * 1e-3) / 1e9},
-                    "gemm_f32_kernel": {"ms_per_step": sum(g_ms) / n_bd}},
+                    "policy GEMMs": {"ms_per_step": sum(g_ms) / n_bd}},
+        "_graphs": "timed region: every learn() replays one HIP graph after the zero-std "
+                   "check of the returns (one host sync); breakdown: eager launches",
         "last_loss": float(loss.item()),
         "cpu_baseline": None,
     }

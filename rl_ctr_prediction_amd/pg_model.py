@@ -11,9 +11,11 @@ Reference quirk kept by default: ``Net`` sizes its first Linear as
 same shape error. ``fix_input_dims=True`` sizes it to the real state width (used for the
 C4 REINFORCE configuration; documented in DESIGN.md).
 
-``learn`` is one fused native pass: Feature_Embedding -> 5 fused GEMMs -> softmax ->
-loss + softmax-backward kernel -> 5 weight-gradient GEMMs with Dropout/ReLU mask
-epilogues -> dense Adam over one flat parameter buffer. The embedding is not updated: its
+``learn`` is one fused native pass: Feature_Embedding -> 5 fused GEMMs (the three wide
+layers on pre-split bf16 planes, csrc/gemm_planes.hip) -> softmax -> loss +
+softmax-backward kernel -> 5 weight-gradient GEMMs with Dropout/ReLU mask epilogues ->
+dense Adam over one flat parameter buffer; single-process learns replay it as one HIP graph
+(Adam scalars and the dropout stream from a device step counter). The embedding is not updated: its
 output is detached (Feature_embedding.py:59), so torch's Adam never sees a gradient for it.
 
 Data parallel: the ranks' transitions are slices of ONE episode, in
@@ -25,6 +27,8 @@ process learning the whole episode; the weight gradients are summed by one all-r
 masks are indexed by the transition's position in the episode, so they match too.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -134,7 +138,27 @@ class PolicyGradient:
         self.weight_decay = 1e-5  # PG_model.py:87
         self.betas, self.eps = (0.9, 0.999), 1e-8
         self._seed = _dropout_seed()
-        self._drop_offset = 0
+        # device step counter [completed learns, learn in flight] (advanced by ctr_step_end):
+        # the Adam scalars come from the step table and the dropout stream of learn k is
+        # (k << 32) + the transition's episode position, so a learn can be captured into a
+        # HIP graph and replayed (single process)
+        self._step_ctr = torch.tensor([0, 1], dtype=torch.int32, device=dev)
+        self._step_done, self._step_cur = self._step_ctr[0:1], self._step_ctr[1:2]
+        self._step_table = hip_ops.AdamStepTable(self.lr, self.betas, dev)
+        self.use_graphs = True
+        self._graphs: dict = {}
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        self._graph_tab_version = self._step_table.version
+        self._lbufs: dict = {}
+        # the layers whose GEMMs run on pre-split bf16 planes (csrc/gemm_planes.hip, the
+        # DeepFM MLP's kernel): the wide ones (C4: 741->1024, 1024->512, 512->256 = 97 % of
+        # the flops); the narrow tail (256->128->A) stays on ctr_gemm_f32_ex
+        self.planes_layers = 0
+        if os.environ.get("CTR_PG_PLANES", "1") != "0":
+            self.planes_layers = max(0, len(self._layers) - 2)
+        self._wplanes = [hip_ops.Planes(l.out_features, l.in_features, dev)
+                         for l in self._layers[:self.planes_layers]]
+        self._pbufs: dict = {}
 
     # ---------------------------------------------------------------- reference API ---
     @property
@@ -195,8 +219,13 @@ class PolicyGradient:
         acts = self.ep_as.to(self.device)
         rank, ws = world()
         if ws == 1:
-            _, vt = self._discount_norm_device()
-            loss = self._fused_learn(states, acts, vt)
+            _, vt = self._discount_norm_device()  # (host check of the zero std: one sync)
+            if self.use_graphs and states.is_cuda:
+                loss = self._graph_learn(states, acts, vt)
+            else:
+                self._step_table.ensure(self._step + 1)
+                loss = self._fused_learn(states, acts, vt)
+                self._step += 1
         else:
             r = self.ep_rs.to(self.device).float().reshape(-1)
             if r.numel() == 0:
@@ -205,12 +234,71 @@ class PolicyGradient:
             _, vt_all, stats = hip_ops.pg_discount_norm(r_all, float(self.gamma))
             if float(stats[1].item()) == 0.0:
                 raise FloatingPointError("divide by zero encountered in divide")
+            self._step_table.ensure(self._step + 1)
             loss = self._fused_learn(states, acts, None, vt_mean=hip_ops.pg_vt_mean(vt_all),
                                      row0=sum(counts[:rank]), n_episode=sum(counts))
+            self._step += 1
         self._ep_states, self._ep_as, self._ep_rs = [], [], []
         return loss
 
     # ------------------------------------------------------------------ fused pass ----
+    def _graph_learn(self, states, acts, vt):
+        """_fused_learn on persistent per-episode-size inputs, captured once per (size,
+        train mode, dropout) and replayed as a HIP graph (the ~40 launches of a learn)."""
+        n, F = states.shape
+        b = self._lbufs.get((n, F))
+        if b is None:
+            dev = self._flat.device
+            b = {"x": torch.empty(n, F, dtype=states.dtype, device=dev),
+                 "a": torch.empty(n, 1, dtype=torch.int64, device=dev),
+                 "vt": torch.empty(n, dtype=torch.float32, device=dev)}
+            self._lbufs = {(n, F): b}  # the last episode size only
+            self._graphs = {k: v for k, v in self._graphs.items() if k[0] == (n, F)}
+        if b["x"].dtype != states.dtype:
+            b["x"] = torch.empty(n, F, dtype=states.dtype, device=states.device)
+        b["x"].copy_(states)
+        b["a"].copy_(acts.reshape(n, 1))
+        b["vt"].copy_(vt.reshape(-1))
+        if self._step_table.capacity < self._step + 2:
+            self._step_table.ensure(max(self._step + 2, 2 * self._step_table.capacity))
+        if self._graph_tab_version != self._step_table.version:
+            torch.cuda.synchronize()
+            self._graphs.clear()  # they hold the old table's address
+            self._graph_tab_version = self._step_table.version
+        net = self.policy_net
+        drops = tuple(float(net.mlp[3 * i + 2].p) for i in range(4))
+        key = ((n, F), b["x"].dtype, net.training, drops, self.planes_layers)
+        hit = self._graphs.get(key)
+        if hit is None:
+            from .trainer import graph_capture
+            loss = self._fused_learn(b["x"], b["a"], b["vt"])  # the real learn
+            self._step += 1
+            g = torch.cuda.CUDAGraph()
+            with graph_capture(g, pool=self._graph_pool):
+                static = self._fused_learn(b["x"], b["a"], b["vt"])  # captured, not executed
+            self._graphs[key] = (g, static)
+            return loss
+        g, static = hit
+        g.replay()
+        self._step += 1
+        return static
+
+
+    def _planes_bufs(self, n: int) -> dict:
+        """Per-episode-size buffers of the planes layers: the planes of each layer input
+        (hp[i]), the fp32 layer outputs (h[i+1], the dropout / ReLU masks of the backward),
+        and the planes of the output gradients (dp[i])."""
+        b = self._pbufs.get(n)
+        if b is None:
+            dev, L, P = self._flat.device, self._layers, self.planes_layers
+            e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+            b = {"hp": [hip_ops.Planes(n, L[i].in_features, dev) for i in range(P)],
+                 "h": [None] + [e(n, L[i].out_features) for i in range(P)],
+                 "d": [e(n, L[i].out_features) for i in range(P)],
+                 "dp": [hip_ops.Planes(n, L[i].out_features, dev) for i in range(P)]}
+            self._pbufs = {n: b}  # one episode size at a time (the last one)
+        return b
+
     def _fused_learn(self, states, acts, vt, vt_mean=None, row0: int = 0,
                      n_episode: int | None = None) -> torch.Tensor:
         """vt: this episode's normalised returns (single process); or vt_mean: the
@@ -225,13 +313,31 @@ class PolicyGradient:
         h = x0
         mods = list(net.mlp)
         drops = [float(mods[3 * i + 2].p) if training else 0.0 for i in range(4)]
+        P = self.planes_layers
+        base = 0  # each layer's dropout stream: (learn << 32) + episode position
+        if P:
+            pb = self._planes_bufs(n)
+            for i in range(P):  # the weights' planes, from the fp32 parameters (every learn)
+                hip_ops.split_planes(self._layers[i].weight, out=self._wplanes[i])
+            hip_ops.split_planes(x0.contiguous(), out=pb["hp"][0])
         for i, lin in enumerate(self._layers):
             last = i == len(self._layers) - 1
-            off = self._drop_offset + row0 * lin.out_features
-            self._drop_offset += n_ep * lin.out_features
+            off = base + row0 * lin.out_features
+            base += n_ep * lin.out_features
             h_in = h
-            h = hip_ops.linear(h_in, lin.weight, lin.bias, relu=not last,
-                               drop_p=0.0 if last else drops[i], seed=self._seed, offset=off)
+            if i < P:  # same epilogue (bias, ReLU, the same dropout hash) on planes
+                p = 0.0 if last else drops[i]
+                hip_ops.gemm_planes(pb["hp"][i], self._wplanes[i], False, False,
+                                    out=pb["h"][i + 1],
+                                    out_planes=pb["hp"][i + 1] if i + 1 < P else None,
+                                    epi=hip_ops.EPI_BIAS_RELU_DROP if p > 0 else hip_ops.EPI_BIAS_RELU,
+                                    bias=lin.bias, drop_p=p, seed=self._seed, offset=off,
+                                    step_dev=self._step_done)
+                h = pb["h"][i + 1]
+            else:
+                h = hip_ops.linear(h_in, lin.weight, lin.bias, relu=not last,
+                                   drop_p=0.0 if last else drops[i], seed=self._seed, offset=off,
+                                   step_dev=self._step_done)
             acts_l.append(h_in)
         probs = hip_ops.softmax_rows(h)
         if vt_mean is None:
@@ -241,15 +347,31 @@ class PolicyGradient:
         for i in range(len(self._layers) - 1, -1, -1):
             lin = self._layers[i]
             inp = acts_l[i]
-            hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
+            if i < P:  # g = dL/d(layer i output) is in pb["d"][i] with its planes
+                hip_ops.gemm_planes(pb["dp"][i], pb["hp"][i], True, True, out=self._gviews[2 * i])
+            else:
+                hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
             hip_ops.colsum(g, out=self._gviews[2 * i + 1])
             if i > 0:
-                g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
-                                 scale=1.0 / (1.0 - drops[i - 1]))
+                sc = 1.0 / (1.0 - drops[i - 1])
+                if i - 1 < P:  # the next layer down runs on planes: write g's planes too
+                    if i < P:
+                        hip_ops.gemm_planes(pb["dp"][i], self._wplanes[i], False, True,
+                                            out=pb["d"][i - 1], out_planes=pb["dp"][i - 1],
+                                            epi=hip_ops.EPI_GRAD_MASK, aux=inp, scale=sc)
+                    else:
+                        hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp, scale=sc,
+                                     out=pb["d"][i - 1])
+                        hip_ops.split_planes(pb["d"][i - 1], out=pb["dp"][i - 1])
+                    g = pb["d"][i - 1]
+                else:
+                    g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
+                                     scale=sc)
         if vt_mean is not None:  # the episode's gradient and loss: sums of the ranks' shares
             allreduce_sum_(self._grad, self.group)
             allreduce_sum_(loss, self.group)
-        self._step += 1
-        hip_ops.adam_dense(self._flat, self._grad, self._m, self._v, self._step, self.lr,
-                           self.betas, self.eps, self.weight_decay)
+        hip_ops.adam_dense(self._flat, self._grad, self._m, self._v, self._step + 1, self.lr,
+                           self.betas, self.eps, self.weight_decay, step_dev=self._step_cur,
+                           table=self._step_table)
+        hip_ops.step_end(self._step_ctr)
         return loss

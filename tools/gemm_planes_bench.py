@@ -21,6 +21,18 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from rl_ctr_prediction_amd import hip_ops as H  # noqa: E402
 
 
+def pg_shapes(n=4096):
+    """The C4 policy MLP (741-1024-512-256 planes layers) at an episode of n transitions."""
+    return {"pg fwd0 S.W0^T": (n, 1024, 741, False, False),
+            "pg fwd1 H1.W1^T": (n, 512, 1024, False, False),
+            "pg fwd2 H2.W2^T": (n, 256, 512, False, False),
+            "pg d1 G2.W2": (n, 512, 256, False, True),
+            "pg d0 G1.W1": (n, 1024, 512, False, True),
+            "pg dW2 G2^T.H2": (256, 512, n, True, True),
+            "pg dW1 G1^T.H1": (512, 1024, n, True, True),
+            "pg dW0 G0^T.S": (1024, 741, n, True, True)}
+
+
 def shapes(B, W, H1=300, H2=200):
     # name: (M, N, K, a_rc, b_rc)
     return {"fwd0 X.W0^T": (B, H1, W, False, False),
@@ -54,11 +66,13 @@ def main():
     ap.add_argument("--W", type=int, default=1664)
     ap.add_argument("--tiles", type=int, default=25, help="sweep tilings 0 .. tiles-1")
     ap.add_argument("--only", default="", help="comma-separated tiling indices to sweep")
+    ap.add_argument("--pg", action="store_true", help="the C4 policy MLP shapes instead")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     total = 0.0
-    for name, (M, N, K, a_rc, b_rc) in shapes(args.B, args.W).items():
+    table = pg_shapes() if args.pg else shapes(args.B, args.W)
+    for name, (M, N, K, a_rc, b_rc) in table.items():
         A = torch.randn(*((K, M) if a_rc else (M, K)), device=dev, generator=g)
         Bm = torch.randn(*((K, N) if b_rc else (N, K)), device=dev, generator=g)
         pa, pb = H.split_planes(A), H.split_planes(Bm)
