@@ -127,8 +127,10 @@ class PolicyGradient:
         self._grad = torch.zeros_like(self._flat)
         self._m, self._v = torch.zeros_like(self._flat), torch.zeros_like(self._flat)
         self._gviews = []
+        self._offsets = []
         off = 0
         for p in params:
+            self._offsets.append(off)
             k = p.numel()
             self._flat[off:off + k].copy_(p.data.reshape(-1))
             p.data = self._flat[off:off + k].view_as(p)
@@ -158,6 +160,12 @@ class PolicyGradient:
             self.planes_layers = max(0, len(self._layers) - 2)
         self._wplanes = [hip_ops.Planes(l.out_features, l.in_features, dev)
                          for l in self._layers[:self.planes_layers]]
+        # weights whose planes the dense Adam rewrites itself (row length a multiple of 4,
+        # ctr_adam_dense_planes); the others are re-split at every learn. _wver: the weights'
+        # version counters when their planes were last split (load_state_dict & co. bump them)
+        self._adam_planes = [i for i in range(self.planes_layers)
+                             if self._layers[i].in_features % 4 == 0][-2:]  # <= 2 views
+        self._wver = None
         self._pbufs: dict = {}
 
     # ---------------------------------------------------------------- reference API ---
@@ -215,9 +223,15 @@ class PolicyGradient:
         return d64.cpu().numpy().reshape(-1, 1)
 
     def learn(self):
+        rank, ws = world()
+        if ws == 1 and self.use_graphs and self._ep_states and all(
+                t.device == self._flat.device for t in self._ep_states + self._ep_as):
+            _, vt = self._discount_norm_device()  # (host check of the zero std: one sync)
+            loss = self._graph_learn(None, None, vt)
+            self._ep_states, self._ep_as, self._ep_rs = [], [], []
+            return loss
         states = self.ep_states.to(self.device)
         acts = self.ep_as.to(self.device)
-        rank, ws = world()
         if ws == 1:
             _, vt = self._discount_norm_device()  # (host check of the zero std: one sync)
             if self.use_graphs and states.is_cuda:
@@ -245,19 +259,29 @@ class PolicyGradient:
     def _graph_learn(self, states, acts, vt):
         """_fused_learn on persistent per-episode-size inputs, captured once per (size,
         train mode, dropout) and replayed as a HIP graph (the ~40 launches of a learn)."""
-        n, F = states.shape
+        if states is None:  # straight from the stored transitions (one copy, no cat first)
+            n = sum(t.shape[0] for t in self._ep_states)
+            F = self._ep_states[0].shape[1]
+            sdt = self._ep_states[0].dtype
+        else:
+            n, F = states.shape
+            sdt = states.dtype
         b = self._lbufs.get((n, F))
         if b is None:
             dev = self._flat.device
-            b = {"x": torch.empty(n, F, dtype=states.dtype, device=dev),
+            b = {"x": torch.empty(n, F, dtype=sdt, device=dev),
                  "a": torch.empty(n, 1, dtype=torch.int64, device=dev),
                  "vt": torch.empty(n, dtype=torch.float32, device=dev)}
             self._lbufs = {(n, F): b}  # the last episode size only
             self._graphs = {k: v for k, v in self._graphs.items() if k[0] == (n, F)}
-        if b["x"].dtype != states.dtype:
-            b["x"] = torch.empty(n, F, dtype=states.dtype, device=states.device)
-        b["x"].copy_(states)
-        b["a"].copy_(acts.reshape(n, 1))
+        if b["x"].dtype != sdt:
+            b["x"] = torch.empty(n, F, dtype=sdt, device=self._flat.device)
+        if states is None:
+            torch.cat(self._ep_states, out=b["x"])
+            torch.cat([a.reshape(-1, 1).to(torch.int64) for a in self._ep_as], out=b["a"])
+        else:
+            b["x"].copy_(states)
+            b["a"].copy_(acts.reshape(n, 1))
         b["vt"].copy_(vt.reshape(-1))
         if self._step_table.capacity < self._step + 2:
             self._step_table.ensure(max(self._step + 2, 2 * self._step_table.capacity))
@@ -317,8 +341,12 @@ class PolicyGradient:
         base = 0  # each layer's dropout stream: (learn << 32) + episode position
         if P:
             pb = self._planes_bufs(n)
-            for i in range(P):  # the weights' planes, from the fp32 parameters (every learn)
-                hip_ops.split_planes(self._layers[i].weight, out=self._wplanes[i])
+            ver = tuple(self._layers[i].weight._version for i in range(P))
+            for i in range(P):  # the weights' planes from the fp32 parameters: those the
+                # Adam keeps current only after an outside change (first learn, load)
+                if i not in self._adam_planes or ver != self._wver:
+                    hip_ops.split_planes(self._layers[i].weight, out=self._wplanes[i])
+            self._wver = ver
             hip_ops.split_planes(x0.contiguous(), out=pb["hp"][0])
         for i, lin in enumerate(self._layers):
             last = i == len(self._layers) - 1
@@ -344,6 +372,7 @@ class PolicyGradient:
             loss, g = hip_ops.pg_loss_grad(probs, acts, vt)
         else:
             loss, g = hip_ops.pg_loss_grad_global(probs, acts, vt_mean)
+        bias_jobs = []
         for i in range(len(self._layers) - 1, -1, -1):
             lin = self._layers[i]
             inp = acts_l[i]
@@ -351,7 +380,7 @@ class PolicyGradient:
                 hip_ops.gemm_planes(pb["dp"][i], pb["hp"][i], True, True, out=self._gviews[2 * i])
             else:
                 hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
-            hip_ops.colsum(g, out=self._gviews[2 * i + 1])
+            bias_jobs.append((g, None, self._gviews[2 * i + 1]))  # db = colsum g
             if i > 0:
                 sc = 1.0 / (1.0 - drops[i - 1])
                 if i - 1 < P:  # the next layer down runs on planes: write g's planes too
@@ -367,11 +396,13 @@ class PolicyGradient:
                 else:
                     g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
                                      scale=sc)
+        hip_ops.colsum_multi(bias_jobs)  # the five bias gradients in one launch pair
         if vt_mean is not None:  # the episode's gradient and loss: sums of the ranks' shares
             allreduce_sum_(self._grad, self.group)
             allreduce_sum_(loss, self.group)
+        planes = [(self._offsets[2 * i], self._wplanes[i]) for i in self._adam_planes]
         hip_ops.adam_dense(self._flat, self._grad, self._m, self._v, self._step + 1, self.lr,
                            self.betas, self.eps, self.weight_decay, step_dev=self._step_cur,
-                           table=self._step_table)
+                           table=self._step_table, planes=planes or None)
         hip_ops.step_end(self._step_ctr)
         return loss
