@@ -60,6 +60,38 @@ __device__ __forceinline__ int64_t load_row(const IdxT* idx, int64_t i, int64_t 
   return r;
 }
 
+// One example's F embedding rows [K] staged by one wave into a wave-private LDS tile (row
+// stride ld) and, when `flat` is given, copied to flat[f*K + k]. Lane f loads id f once;
+// the F*K elements are then dealt over all 64 lanes with the row broadcast by a shuffle, so
+// every element load is independent (a loop over f with a dependent id -> row load per
+// field serialised F memory round trips: ~40 us for 4096 x 26 x 16). The shuffles run
+// with every lane active (uniform trip count); only the loads and stores are predicated.
+template <typename IdxT>
+__device__ __forceinline__ void stage_rows_wave(const IdxT* __restrict__ idx, int64_t b, int F,
+                                                int K, int64_t V,
+                                                const float* __restrict__ emb, float* tile,
+                                                int ld, float* __restrict__ flat,
+                                                int32_t* err, int lane) {
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int nf = F - f0 < 64 ? F - f0 : 64;
+    long long my_row = 0;
+    if (lane < nf) my_row = (long long)load_row(idx, b * F + f0 + lane, V, err);
+    const int n = nf * K, iters = (n + 63) / 64;
+    for (int it = 0; it < iters; ++it) {
+      const int t = lane + 64 * it;
+      int f = t / K;
+      f = f < nf ? f : nf - 1;
+      const long long row = __shfl(my_row, f, 64);
+      if (t < n) {
+        const int k = t - f * K;
+        const float e = emb[(int64_t)row * K + k];
+        tile[(f0 + f) * ld + k] = e;
+        if (flat) flat[(int64_t)f0 * K + t] = e;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ wave reductions -------
 // Butterfly over lanes that differ only in bits >= log2(stride): sums the `group`
 // lanes l, l+stride, l+2*stride, ... (stride*group == 64). __shfl_xor lowers to

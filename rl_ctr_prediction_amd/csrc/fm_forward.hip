@@ -234,9 +234,10 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
 }
 
 // --------------------------------------------------------- Feature_Embedding (A7) ---
-// Wave per example; the F rows are staged in LDS with a +1 float row pad so that the
-// 64 lanes (each on a different (i,j) pair) reading column k of rows i and j hit
-// different banks; flat rows are streamed straight to the output.
+// Wave per example; the F rows are staged in LDS (stage_rows_wave: all F*K loads in
+// flight at once) with a +1 float row pad so that the 64 lanes (each on a different (i,j)
+// pair) reading column k of rows i and j hit different banks; the flat rows go straight
+// to the output.
 template <typename IdxT>
 __global__ __launch_bounds__(256) void feature_embedding_kernel(
     const IdxT* __restrict__ idx, int64_t B, int F, int K, int64_t V,
@@ -245,27 +246,19 @@ __global__ __launch_bounds__(256) void feature_embedding_kernel(
   const int wave = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
+  if (b >= B) return;  // wave-uniform; the tile is wave-private (no block barrier)
   const int ld = K + 1;
   float* tile = lds + (int64_t)wave * F * ld;
   const int P = F * (F - 1) / 2;
   const int64_t width = (int64_t)P + (int64_t)F * K;
-  if (b < B) {
-    float* ob = out + b * width;
-    for (int f = 0; f < F; ++f) {
-      const int64_t row = load_row(idx, b * F + f, V, err);
-      for (int k = lane; k < K; k += kWave) {
-        const float e = emb[row * K + k];
-        tile[f * ld + k] = e;
-        ob[P + f * K + k] = e;
-      }
-    }
-  }
-  __syncthreads();
-  if (b >= B) return;
   float* ob = out + b * width;
-  for (int p = lane; p < P; p += kWave) {
-    // row-major pair order of Feature_embedding.py:40-43: (0,1),(0,2)...(0,F-1),(1,2)...
-    int i = 0, rem = p;
+  stage_rows_wave(idx, b, F, K, V, emb, tile, ld, ob + P, err, lane);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores are done
+  __builtin_amdgcn_wave_barrier();
+  // row-major pair order of Feature_embedding.py:40-43: (0,1),(0,2)...(0,F-1),(1,2)...;
+  // lane -> pairs p = lane, lane + 64, ...; (i, j) walked incrementally
+  int i = 0, rem = lane;
+  for (int p = lane; p < P; p += kWave, rem += kWave) {
     while (rem >= F - 1 - i) {
       rem -= F - 1 - i;
       ++i;

@@ -39,14 +39,7 @@ __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restric
   const int ld = K + 1;
   float* tile = lds + (int64_t)wave * F * ld;
   float* ob = cat + b * ldc;
-  for (int f = 0; f < F; ++f) {
-    const int64_t row = load_row(idx, b * F + f, V, err);
-    for (int k = lane; k < K; k += kWave) {
-      const float e = emb[row * K + k];
-      tile[f * ld + k] = e;
-      ob[f * K + k] = e;
-    }
-  }
+  stage_rows_wave(idx, b, F, K, V, emb, tile, ld, ob, err, lane);
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores are done
   __builtin_amdgcn_wave_barrier();
   const int P = F * (F - 1) / 2;
@@ -88,10 +81,7 @@ __global__ __launch_bounds__(256) void ipnn_backward_kernel(const IdxT* __restri
   const int P = F * (F - 1) / 2;
   float* tile = lds + (int64_t)wave * (F * ld + P);
   float* dp = tile + F * ld;
-  for (int f = 0; f < F; ++f) {
-    const int64_t row = load_row(idx, b * F + f, V, nullptr);
-    for (int k = lane; k < K; k += kWave) tile[f * ld + k] = emb[row * K + k];
-  }
+  stage_rows_wave(idx, b, F, K, V, emb, tile, ld, (float*)nullptr, (int32_t*)nullptr, lane);
   const float* db = dcat + b * ldd;
   for (int p = lane; p < P; p += kWave) dp[p] = db[(int64_t)F * K + p];
   __builtin_amdgcn_s_waitcnt(0xc07f);

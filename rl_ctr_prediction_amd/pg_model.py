@@ -29,6 +29,7 @@ masks are indexed by the transition's position in the episode, so they match too
 from __future__ import annotations
 
 import os
+from contextlib import nullcontext
 
 import numpy as np
 import torch
@@ -167,6 +168,13 @@ class PolicyGradient:
                              if self._layers[i].in_features % 4 == 0][-2:]  # <= 2 views
         self._wver = None
         self._pbufs: dict = {}
+        # the weight-gradient GEMMs (dW_i = g_i^T h_i) on a side stream forked where each g_i
+        # is complete, joined before the bias sums and the Adam: the dX chain of the
+        # backward keeps the main stream (as the DeepFM step's weight-gradient list)
+        # (CTR_PG_WGRAD_SIDE: 0 = off, 1 = every layer, 2 = the planes layers only)
+        self._wgrad_side, self._wgrad_mode = None, os.environ.get("CTR_PG_WGRAD_SIDE", "0")
+        if self._wgrad_mode != "0" and dev.type == "cuda":
+            self._wgrad_side = torch.cuda.Stream(device=dev)
 
     # ---------------------------------------------------------------- reference API ---
     @property
@@ -373,13 +381,21 @@ class PolicyGradient:
         else:
             loss, g = hip_ops.pg_loss_grad_global(probs, acts, vt_mean)
         bias_jobs = []
+        side = self._wgrad_side if states.is_cuda else None
+        held = []  # the side stream's inputs stay referenced until the join
         for i in range(len(self._layers) - 1, -1, -1):
             lin = self._layers[i]
             inp = acts_l[i]
-            if i < P:  # g = dL/d(layer i output) is in pb["d"][i] with its planes
-                hip_ops.gemm_planes(pb["dp"][i], pb["hp"][i], True, True, out=self._gviews[2 * i])
-            else:
-                hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
+            on_side = side is not None and (self._wgrad_mode != "2" or i < P)
+            if on_side:
+                side.wait_stream(torch.cuda.current_stream())
+                held.append((g, inp))
+            with torch.cuda.stream(side) if on_side else nullcontext():
+                if i < P:  # g = dL/d(layer i output) is in pb["d"][i] with its planes
+                    hip_ops.gemm_planes(pb["dp"][i], pb["hp"][i], True, True,
+                                        out=self._gviews[2 * i])
+                else:
+                    hip_ops.gemm(g, inp, trans_a=True, out=self._gviews[2 * i])
             bias_jobs.append((g, None, self._gviews[2 * i + 1]))  # db = colsum g
             if i > 0:
                 sc = 1.0 / (1.0 - drops[i - 1])
@@ -396,6 +412,9 @@ class PolicyGradient:
                 else:
                     g = hip_ops.gemm(g, lin.weight, epi=hip_ops.EPI_GRAD_MASK, aux=inp,
                                      scale=sc)
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
+        del held
         hip_ops.colsum_multi(bias_jobs)  # the five bias gradients in one launch pair
         if vt_mean is not None:  # the episode's gradient and loss: sums of the ranks' shares
             allreduce_sum_(self._grad, self.group)
