@@ -429,6 +429,17 @@ int ctr_segment_sum_rows_adam(const ctr_sparse_plan* plan, int K, const float* v
  *   finished before ctr_step_end. table_steps = entries of step_table (its capacity). */
 int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream);
 int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream);
+/* ctr_fm_step_tail: the FM step's dense tail (one process) in one launch —
+ *   loss_out[0] = loss_scale * sum(loss_elem[:B]), bias_grad[0] = sum(gz[:B]) (bitwise
+ *   ctr_sum_f32), Adam on the flat dense vector (p, g, m, v)[:n] at step ctr[1] (bitwise
+ *   ctr_adam_dense; bias_grad may point into g), then ctr_step_end(step_ctr).
+ *   Replaces: all_main/pretrain_main.py:74-78 (loss.backward's bias gradient, the batch
+ *   loss, optimizer.step() on the FM bias) at the end of a step. */
+int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t B, float loss_scale,
+                     float* loss_out, float* bias_grad, float* p, const float* g, float* m,
+                     float* v, int64_t n, const float* step_table, int32_t* step_ctr,
+                     double beta1, double beta2, double eps, double weight_decay,
+                     ctr_stream_t stream);
 int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                             float* v_lin, int64_t V, int K, int32_t* last,
                             const int32_t* step_ctr, int n_slices, const float* step_table,

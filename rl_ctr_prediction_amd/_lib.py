@@ -129,6 +129,8 @@ SIGNATURES = {
                                                _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_step_begin": (_i32, [_vp, _vp]),
     "ctr_step_end": (_i32, [_vp, _vp]),
+    "ctr_fm_step_tail": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_sweep": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32,
                                        _vp, _i64, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_flush": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp,

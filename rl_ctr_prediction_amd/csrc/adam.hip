@@ -430,6 +430,57 @@ __global__ void step_end_kernel(int32_t* ctr) {
   ctr[1] = t + 1;  // the next step's: ctr_step_begin is then a no-op
 }
 
+// The FM step's dense tail in one launch (single process): the batch loss and the FM
+// bias gradient summed exactly as sum_small does (same per-thread order, wave butterfly,
+// 16 wave partials in order: bitwise ctr_sum_f32), the flat dense parameters' Adam step at
+// ctr[1] (adam_elem, bitwise adam_dense_vec), then ctr_step_end — four launches of the C2
+// step graph (2 x sum_small, adam_dense_vec, step_end_kernel) become one.
+__global__ __launch_bounds__(1024) void fm_step_tail_kernel(
+    const float* __restrict__ loss_elem, const float* __restrict__ gz, int64_t B,
+    float loss_scale, float* __restrict__ loss_out, float* bias_grad, float* __restrict__ p,
+    const float* g, float* __restrict__ m, float* __restrict__ v, int64_t n, AdamHP h,
+    const float* __restrict__ tab, int32_t* ctr) {
+  __shared__ float sh[2][16];
+  const int t = threadIdx.x;
+  float al = 0.f, ag = 0.f;
+#pragma unroll 8
+  for (int64_t i = t; i < B; i += 1024) {
+    al += loss_elem[i];
+    ag += gz[i];
+  }
+  al = wave_sum(al);
+  ag = wave_sum(ag);
+  if ((t & 63) == 0) {
+    sh[0][t >> 6] = al;
+    sh[1][t >> 6] = ag;
+  }
+  load_step(h, tab, ctr[1]);
+  __syncthreads();
+  if (t == 0) {
+    float rl = 0.f, rg = 0.f;
+    for (int w2 = 0; w2 < 16; ++w2) {
+      rl += sh[0][w2];
+      rg += sh[1][w2];
+    }
+    loss_out[0] = rl * loss_scale;
+    bias_grad[0] = rg * 1.0f;
+  }
+  __syncthreads();  // the bias gradient (an element of g) is visible to the block
+  for (int64_t i = t; i < n; i += 1024) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, g[i], mm, vv, h);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+  }
+  __syncthreads();  // every thread has read ctr[1]
+  if (t == 0) {
+    const int32_t s = ctr[1];
+    ctr[0] = s;
+    ctr[1] = s + 1;
+  }
+}
+
 // Background sweep (deferred Adam): bring one slice of the rows — slice ctr[0] % n_slices —
 // up to the completed step ctr[0], while a training step runs on other streams. Rows of the
 // step's own batch are current to ctr[0] after its catch-up (from >= target: skipped), so
@@ -1002,6 +1053,22 @@ extern "C" int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream) {
   CTR_REQUIRE(step_ctr, "ctr_step_end: null pointer");
   hipLaunchKernelGGL(step_end_kernel, 1, 1, 0, as_stream(stream), step_ctr);
   CTR_LAUNCH_CHECK("step_end_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t B,
+                                float loss_scale, float* loss_out, float* bias_grad, float* p,
+                                const float* g, float* m, float* v, int64_t n,
+                                const float* step_table, int32_t* step_ctr, double beta1,
+                                double beta2, double eps, double weight_decay,
+                                ctr_stream_t stream) {
+  CTR_REQUIRE(loss_elem && gz && loss_out && bias_grad && step_table && step_ctr && B >= 0,
+              "ctr_fm_step_tail: bad arguments");
+  CTR_REQUIRE(n >= 0 && (n == 0 || (p && g && m && v)), "ctr_fm_step_tail: bad dense vector");
+  const AdamHP h = make_hp(0.0, 1.0, beta1, beta2, eps, weight_decay);
+  hipLaunchKernelGGL(fm_step_tail_kernel, 1, 1024, 0, as_stream(stream), loss_elem, gz, B,
+                     loss_scale, loss_out, bias_grad, p, g, m, v, n, h, step_table, step_ctr);
+  CTR_LAUNCH_CHECK("fm_step_tail_kernel");
   return CTR_OK;
 }
 

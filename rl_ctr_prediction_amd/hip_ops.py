@@ -19,7 +19,7 @@ __all__ = [
     "embedding_gather", "fm_forward", "fm_forward_planes", "bce_sigmoid", "deepfm_head", "gemm", "linear",
     "tensor_sum", "colsum", "transpose", "Planes", "split_planes", "gemm_planes", "SparsePlanBuffers", "fm_embedding_grad", "segment_sum_rows",
     "fm_embedding_grad_adam", "segment_sum_rows_adam",
-    "rows_to_dense", "adam_dense", "adam_embedding", "adam_scalars", "feature_embedding",
+    "rows_to_dense", "adam_dense", "fm_step_tail", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
     "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "pg_vt_mean", "pg_loss_grad_global", "check_index_error", "Workspace",
@@ -693,6 +693,28 @@ def step_begin(step_ctr: torch.Tensor) -> None:
 def step_end(step_ctr: torch.Tensor) -> None:
     """ctr[0] = ctr[1] on the device."""
     lib.ctr_step_end(_p(step_ctr), _stream())
+
+
+def fm_step_tail(loss_elem: torch.Tensor, gz: torch.Tensor, loss_scale: float,
+                 loss_out: torch.Tensor, bias_grad: torch.Tensor, p, g, m, v,
+                 table: AdamStepTable, step: int, step_ctr: torch.Tensor, betas=(0.9, 0.999),
+                 eps=1e-8, weight_decay=0.0) -> None:
+    """The FM step's dense tail in one launch: loss_out = loss_scale * sum(loss_elem),
+    bias_grad = sum(gz) (bitwise tensor_sum), the Adam step of the flat dense vector p at
+    step ctr[1] (bitwise adam_dense), then step_end(step_ctr)."""
+    for t, n in ((loss_elem, "loss_elem"), (gz, "gz"), (p, "param"), (g, "grad"),
+                 (m, "exp_avg"), (v, "exp_avg_sq")):
+        _f32(t, n)
+    B = gz.numel()
+    if loss_elem.numel() != B or bias_grad.numel() != 1 or loss_out.numel() < 1:
+        raise ValueError("fm_step_tail: loss_elem / gz of B elements, one bias gradient")
+    if not (g.numel() == m.numel() == v.numel() == p.numel()):
+        raise ValueError("fm_step_tail: p, g, m, v of one size")
+    tab = table.ensure(step)
+    lib.ctr_fm_step_tail(_p(loss_elem), _p(gz), B, float(loss_scale), _p(loss_out),
+                         _p(bias_grad), _p(p), _p(g), _p(m), _p(v), p.numel(), _p(tab),
+                         _p(step_ctr), float(betas[0]), float(betas[1]), float(eps),
+                         float(weight_decay), _stream())
 
 
 def adam_deferred_sweep(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step_ctr: torch.Tensor,

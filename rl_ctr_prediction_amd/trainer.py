@@ -208,6 +208,9 @@ class FusedCTRTrainer:
         # runs under dX / the scatter and slows them (C3 12.8 vs 12.7 M ex/s)
         env = os.environ.get("CTR_PLAN_LOOKAHEAD")
         self.plan_lookahead = (env == "1") if env in ("0", "1") else self.kind == "FM"
+        # FM's dense tail fused into one launch (ctr_fm_step_tail); CTR_FM_TAIL=0: the four
+        # separate launches (A/B)
+        self.fm_tail = os.environ.get("CTR_FM_TAIL", "1") != "0"
         # catch-up ahead (step(next_x=)): the next batch's rows that this batch does not touch
         # are brought to this step on the plan stream while it runs (_catchup_ahead). Off by
         # default: bitwise correct, but measured slower on MI355X — the replay beside the
@@ -716,7 +719,10 @@ class FusedCTRTrainer:
             gz = b.fm.gz
         else:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
-        if self.kind == "FM":  # MLP kinds: on the weight-gradient stream
+        # FM, one process: the bias gradient, the batch loss, the dense Adam and the step
+        # counter in one launch at the end of the step (ctr_fm_step_tail)
+        tail = self.kind == "FM" and ws == 1 and self.fm_tail and self._wplanes is None
+        if self.kind == "FM" and not tail:  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         if self._side is not None and not have_plan:
             torch.cuda.current_stream().wait_event(ev_plan)  # the plan
@@ -744,7 +750,7 @@ class FusedCTRTrainer:
         self._span("scatter", t)
         if self.kind in _MLP_KINDS:  # captured after the scatter: see the capture-order note
             self._weight_grads(b, gz)
-        if self.kind == "FM":  # MLP kinds: on the weight-gradient stream, off this chain
+        if self.kind == "FM" and not tail:  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
         grad_rows, grad_lin, plan = b.grad_rows, (b.grad_lin if w is not None else None), b.plan
         if ws > 1:
@@ -767,6 +773,15 @@ class FusedCTRTrainer:
         self._span("adam", t)
         # the dense Adam where the dense gradient completes: on the weight-gradient stream
         # at one process (beside the embedding apply), after the exchange otherwise
+        if tail:
+            self._join_sweep()
+            t = self._mark("adam")
+            hip_ops.fm_step_tail(b.fm.loss_elem, gz, 1.0 / B, b.loss, gv["bias"].view(1),
+                                 self.flat, self.flat_grad, self.m_flat, self.v_flat,
+                                 self.step_table, step_hint, self.step_ctr, self.betas,
+                                 self.eps, self.weight_decay)
+            self._span("adam", t)
+            return b.loss
         wg = self._wgrad_stream if ws == 1 else None
         if wg is None:
             self._join_wgrad()

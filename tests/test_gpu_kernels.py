@@ -497,3 +497,34 @@ def test_transpose_bitwise(cuda, shape):
     assert torch.equal(H.transpose(X), X.t().contiguous())
     if shape[0] and shape[1] > 2:  # a column slice: ld_src > cols
         assert torch.equal(H.transpose(X[:, 1:-1]), X[:, 1:-1].t().contiguous())
+
+
+def test_fm_step_tail_bitwise_separate_launches(cuda):
+    """ctr_fm_step_tail == tensor_sum (loss, bias grad) + adam_dense at ctr[1] + step_end,
+    bitwise (the FM step's dense tail, one launch)."""
+    H = _hip()
+    g0 = torch.Generator().manual_seed(7)
+    for B, n in ((4096, 4), (1000, 7), (65536, 1)):
+        loss_elem = torch.rand(B, generator=g0).to(cuda)
+        gz = (torch.randn(B, generator=g0) * 1e-3).to(cuda)
+        p0 = torch.randn(n, generator=g0).to(cuda)
+        m0 = (torch.randn(n, generator=g0) * 1e-3).to(cuda)
+        v0 = (torch.rand(n, generator=g0) * 1e-6).to(cuda)
+        g_rest = (torch.randn(n, generator=g0) * 1e-3).to(cuda)
+        out = {}
+        for mode in ("tail", "separate"):
+            tab = H.AdamStepTable(1e-3, (0.9, 0.999), cuda)
+            ctr = torch.tensor([4, 5], dtype=torch.int32, device=cuda)
+            p, m, v, g = p0.clone(), m0.clone(), v0.clone(), g_rest.clone()
+            loss = torch.zeros(1, device=cuda)
+            if mode == "tail":
+                H.fm_step_tail(loss_elem, gz, 1.0 / B, loss, g[:1], p, g, m, v, tab, 5, ctr,
+                               weight_decay=1e-5)
+            else:
+                H.tensor_sum(gz, out=g[:1])
+                H.tensor_sum(loss_elem, scale=1.0 / B, out=loss)
+                H.adam_dense(p, g, m, v, 5, 1e-3, weight_decay=1e-5, step_dev=ctr[1:2], table=tab)
+                H.step_end(ctr)
+            out[mode] = [t.cpu() for t in (loss, g, p, m, v, ctr)]
+        for a, b in zip(out["tail"], out["separate"]):
+            assert torch.equal(a, b), (B, n, a, b)
