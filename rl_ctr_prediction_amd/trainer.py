@@ -449,15 +449,18 @@ class FusedCTRTrainer:
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
         self._sync_weight_planes()
+        # the host side of a step paces small batches (C2: ~70 us of Python per step against
+        # ~75 us on the GPU), so each ids tensor's key is computed once and the current
+        # stream is looked up once (torch.cuda.current_stream() costs ~4 us)
         xkey = self._xkey(x)
         if next_x is None or self._plan_stream is None or ws != 1:
             nxts = []
         else:
             nxts = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
-        nxts = [n for n in nxts if n.is_cuda and tuple(n.shape) == tuple(x.shape)
-                and self._xkey(n) != xkey]
-        ahead = nxts if self.plan_lookahead else []
-        ca_next = nxts[0] if (self.catchup_ahead and nxts) else None
+        nk = [(n, self._xkey(n)) for n in nxts]
+        nk = [(n, k) for n, k in nk if n.is_cuda and k[1] == xkey[1] and k != xkey]
+        ahead = nk if self.plan_lookahead else []
+        ca_next = nk[0] if (self.catchup_ahead and nk) else None
         main = torch.cuda.current_stream()
         ev = self._pending.pop(xkey, None)
         have = ev is not None
@@ -467,32 +470,33 @@ class FusedCTRTrainer:
         # batch that did not come next is harmless (its rows just replayed earlier) but may
         # share rows with x: every pending one completes before this step starts
         have_ca = xkey in self._ca_pending
-        for ev_ca in self._ca_pending.values():
-            main.wait_event(ev_ca)
-        self._ca_pending.clear()
-        keep = {self._xkey(n) for n in ahead}
-        for k in [k for k in self._pending if k not in keep]:
-            del self._pending[k]  # built for a batch that did not come next: unused
-        todo = [n for n in ahead if self._xkey(n) not in self._pending]
+        if self._ca_pending:
+            for ev_ca in self._ca_pending.values():
+                main.wait_event(ev_ca)
+            self._ca_pending.clear()
+        if self._pending:
+            keep = {k for _, k in ahead}
+            for k in [k for k in self._pending if k not in keep]:
+                del self._pending[k]  # built for a batch that did not come next: unused
+        todo = [(n, k) for n, k in ahead if k not in self._pending]
         ev_start = None
         if todo or ca_next is not None:
             ev_start = torch.cuda.Event()
             ev_start.record(main)  # everything before this step (earlier readers of the plans)
         if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
                 and y.dtype == torch.float32 and y.is_contiguous()):
-            loss = self._graph_step(x, y, mean_div, have, have_ca)
+            loss = self._graph_step(x, y, mean_div, have, have_ca, xkey)
         else:
             self.step_table.ensure(self.step_count + 1)
             loss = self._launch(x, y, mean_div, have, have_ca)
             self._after_step()
         if ca_next is not None:
-            self._catchup_ahead(x, ca_next, ev_start)
+            self._catchup_ahead(x, ca_next[0], ev_start)
         seen = set()
-        for n in todo:
-            k = self._xkey(n)
+        for n, k in todo:
             if k not in seen:
                 seen.add(k)
-                self._build_ahead(n, ev_start)
+                self._build_ahead(n, ev_start, k, main)
         return loss
 
     def _catchup_ahead(self, x: torch.Tensor, nx: torch.Tensor, ev_start) -> None:
@@ -529,20 +533,27 @@ class FusedCTRTrainer:
             ev.record(cs)
         self._ca_pending[self._xkey(nx)] = ev
 
-    def _build_ahead(self, nx: torch.Tensor, ev_start) -> None:
+    def _build_ahead(self, nx: torch.Tensor, ev_start, key=None, main=None) -> None:
         """The lookahead plan of ids nx on the plan stream, concurrent with the step just
-        enqueued (replayed from its own graph once captured)."""
-        key = self._xkey(nx)
+        enqueued (replayed from its own graph once captured). key: _xkey(nx); main: the
+        current stream (both looked up here when not given)."""
+        if key is None:
+            key = self._xkey(nx)
+        if main is None:
+            main = torch.cuda.current_stream()
         si = self._plan_stream_of.get(key)
         if si is None:
             si = self._plan_stream_of[key] = len(self._plan_stream_of) % max(1, self.n_plan_streams)
         while si > len(self._extra_plan_streams):
             self._extra_plan_streams.append(torch.cuda.Stream(device=self.device))
         ps = self._plan_stream if si == 0 else self._extra_plan_streams[si - 1]
-        P = self._plan_for(nx)
+        P = self._plan_for(nx, key)
         ps.wait_event(ev_start)
         nx.record_stream(ps)
-        with torch.cuda.stream(ps):
+        # torch.cuda.set_stream on the two known streams instead of the torch.cuda.stream
+        # context manager (~9 us per use: it looks the current stream up again)
+        torch.cuda.set_stream(ps)
+        try:
             t = self._mark("plan")
             g = self._plan_graphs.get(key)
             if g is not None and self.timing is None:
@@ -559,15 +570,18 @@ class FusedCTRTrainer:
             self._span("plan", t)
             ev = torch.cuda.Event()
             ev.record(ps)
+        finally:
+            torch.cuda.set_stream(main)
         self._pending[key] = ev
 
     @staticmethod
     def _xkey(x):
         return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()))
 
-    def _plan_for(self, x) -> hip_ops.SparsePlanBuffers:
+    def _plan_for(self, x, key=None) -> hip_ops.SparsePlanBuffers:
         """The plan buffers of ids tensor x (lookahead); LRU, graph-held ones pinned."""
-        key = self._xkey(x)
+        if key is None:
+            key = self._xkey(x)
         p = self._plans.pop(key, None)
         if p is None:
             S = x.shape[0] * x.shape[1]
@@ -608,21 +622,24 @@ class FusedCTRTrainer:
         if self.deferred:
             self._dirty = True
 
-    def _graph_key(self, x, y, mean_div, have=False, have_ca=False):
+    def _graph_key(self, x, y, mean_div, have=False, have_ca=False, xkey=None):
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
-        return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
-                tuple(y.shape), mean_div, self.model.training, drops,
-                self._xkey(x) if have else None, have_ca)
+        if xkey is None:
+            xkey = self._xkey(x)
+        return (xkey, y.data_ptr(), tuple(y.shape), mean_div, self.model.training, drops,
+                have, have_ca)
 
-    def _graph_step(self, x, y, mean_div, have=False, have_ca=False):
+    def _graph_step(self, x, y, mean_div, have=False, have_ca=False, xkey=None):
         if self.step_table.capacity < self.step_count + 2:
             self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
         if self._graph_tab_version != self.step_table.version:
             torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
-        key = self._graph_key(x, y, mean_div, have, have_ca)
+        if xkey is None:
+            xkey = self._xkey(x)
+        key = self._graph_key(x, y, mean_div, have, have_ca, xkey)
         hit = self._graphs.get(key)
         if hit is None:
             loss = self._launch(x, y, mean_div, have, have_ca)  # the real step; sizes buffers
@@ -632,13 +649,13 @@ class FusedCTRTrainer:
                 with graph_capture(g, pool=self._graph_pool):
                     self._launch(x, y, mean_div, have, have_ca)  # captured, not executed
                 if have:  # the graph reads x's lookahead plan buffers
-                    self._pinned_plans.add(self._xkey(x))
+                    self._pinned_plans.add(xkey)
                 self._graphs[key] = (g, self._bufs, self._bufs.plan)
             return loss
         g, self._bufs, plan = hit  # the buffer set the graph was captured with
         self._bufs.plan = plan
         if have:
-            self._plan_for(x)  # LRU touch
+            self._plan_for(x, xkey)  # LRU touch
         g.replay()
         self._after_step()
         return self._bufs.loss
