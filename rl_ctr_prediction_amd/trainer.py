@@ -186,6 +186,8 @@ class FusedCTRTrainer:
         # fused scatter + Adam apply (one process, deferred mode); keep_grads keeps every
         # row's gradient sum in b.grad_rows / b.grad_lin (tests read them)
         self.fuse_apply = os.environ.get("CTR_FUSE_APPLY", "1") != "0"
+        # smallest K the fused apply is used at (A/B: CTR_FUSE_APPLY_MIN_K)
+        self.fuse_apply_min_k = int(os.environ.get("CTR_FUSE_APPLY_MIN_K", "16"))
         # capture order of the step's first fork: the plan first where it is the critical
         # path (FM: the forward / backward are short; C2 31.6 vs 28.4 M ex/s), the catch-up
         # and forward first where they are (MLP kinds; C3 12.39 vs 11.67 M ex/s)
@@ -746,8 +748,10 @@ class FusedCTRTrainer:
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         # one process, deferred Adam: the row sums are applied where they complete
-        # (K >= 32: at C2's K = 16 the separate apply pass measured faster, 31.4 vs 30.1 M ex/s)
-        fused = ws == 1 and self.deferred and self._vec_ok and self.fuse_apply and self.K >= 32
+        # (K >= 16: at C2 fused 48.5 vs separate 46.9 M ex/s, two alternating runs each, once
+        # the host no longer paces the step; below 16 the separate apply pass is kept)
+        fused = (ws == 1 and self.deferred and self._vec_ok and self.fuse_apply
+                 and self.K >= self.fuse_apply_min_k)
         table = (E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last)
         apply_kw = dict(step_dev=self.step_cur, step_table=self.step_table, step=step_hint,
                         betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
