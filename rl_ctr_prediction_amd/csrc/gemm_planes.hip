@@ -543,9 +543,15 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   if (!a_rc && b_rc && M >= 2048 && N >= 1024) return mk(19, 1);
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
   if (a_rc && b_rc && Kp >= 2048) {
+    // target block count of the weight-gradient GEMMs (A/B: CTR_GEMM_PLANES_WG_BLOCKS)
+    static const int64_t wg_blocks = [] {
+      const char* e = getenv("CTR_GEMM_PLANES_WG_BLOCKS");
+      const long v = e ? atol(e) : 0;
+      return (int64_t)(v >= 64 && v <= 8192 ? v : 512);
+    }();
     const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(
-                      ceil_div(512, tiles), Kp / 256), 32));
+                      ceil_div(wg_blocks, tiles), Kp / 256), 32));
     return mk(7, s);
   }
   // otherwise a makespan model: blocks dealt to 256 CUs x occ slots in rounds; a round costs one block's
