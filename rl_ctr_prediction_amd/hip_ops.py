@@ -883,12 +883,17 @@ def softmax_rows(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def pg_discount_norm(r: torch.Tensor, gamma: float):
-    """Returns (normalised returns fp64, the same as fp32, stats[mean, std] fp64)."""
+def pg_discount_norm(r: torch.Tensor, gamma: float, out32=None):
+    """Returns (normalised returns fp64, the same as fp32, stats[mean, std] fp64); out32: a
+    float32 [n] tensor to write the fp32 returns into."""
     r = _f32(r.reshape(-1).contiguous(), "rewards")
     n = r.numel()
     out = torch.empty(n, dtype=torch.float64, device=r.device)
-    out32 = torch.empty(n, dtype=torch.float32, device=r.device)
+    if out32 is None:
+        out32 = torch.empty(n, dtype=torch.float32, device=r.device)
+    elif (out32.dtype != torch.float32 or out32.numel() != n or not out32.is_contiguous()
+          or out32.device != r.device):
+        raise ValueError(f"pg_discount_norm: out32 must be a contiguous float32 [{n}] on {r.device}")
     stats = torch.empty(2, dtype=torch.float64, device=r.device)
     lib.ctr_pg_discount_norm(_p(r), n, float(gamma), _p(out), _p(out32), _p(stats), None, 0,
                              _stream())

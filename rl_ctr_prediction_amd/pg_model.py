@@ -219,9 +219,9 @@ class PolicyGradient:
         self._ep_as.append(a)
         self._ep_rs.append(r)
 
-    def _discount_norm_device(self):
+    def _discount_norm_device(self, out32=None):
         r = self.ep_rs.to(self.device).float().reshape(-1)
-        d64, d32, stats = hip_ops.pg_discount_norm(r, float(self.gamma))
+        d64, d32, stats = hip_ops.pg_discount_norm(r, float(self.gamma), out32=out32)
         if float(stats[1].item()) == 0.0:
             raise FloatingPointError("divide by zero encountered in divide")
         return d64, d32
@@ -234,8 +234,12 @@ class PolicyGradient:
         rank, ws = world()
         if ws == 1 and self.use_graphs and self._ep_states and all(
                 t.device == self._flat.device for t in self._ep_states + self._ep_as):
-            _, vt = self._discount_norm_device()  # (host check of the zero std: one sync)
-            loss = self._graph_learn(None, None, vt)
+            # the inputs are copied into the graph's buffers and the returns written there
+            # BEFORE the host waits for the zero-std check (one sync per learn, as the
+            # reference raises first), so the GPU idles only for the graph launch after it
+            b = self._learn_bufs(None, None)
+            self._discount_norm_device(out32=b["vt"])
+            loss = self._graph_learn(None, None, None, b=b)
             self._ep_states, self._ep_as, self._ep_rs = [], [], []
             return loss
         states = self.ep_states.to(self.device)
@@ -264,9 +268,9 @@ class PolicyGradient:
         return loss
 
     # ------------------------------------------------------------------ fused pass ----
-    def _graph_learn(self, states, acts, vt):
-        """_fused_learn on persistent per-episode-size inputs, captured once per (size,
-        train mode, dropout) and replayed as a HIP graph (the ~40 launches of a learn)."""
+    def _learn_bufs(self, states, acts) -> dict:
+        """The persistent per-episode-size inputs of the learn graph, filled with this
+        episode's transitions (states None: straight from the stored ones, one copy)."""
         if states is None:  # straight from the stored transitions (one copy, no cat first)
             n = sum(t.shape[0] for t in self._ep_states)
             F = self._ep_states[0].shape[1]
@@ -290,7 +294,17 @@ class PolicyGradient:
         else:
             b["x"].copy_(states)
             b["a"].copy_(acts.reshape(n, 1))
-        b["vt"].copy_(vt.reshape(-1))
+        return b
+
+    def _graph_learn(self, states, acts, vt, b=None):
+        """_fused_learn on persistent per-episode-size inputs, captured once per (size,
+        train mode, dropout) and replayed as a HIP graph (the ~40 launches of a learn).
+        b: the inputs already filled by _learn_bufs (vt None: already in b["vt"])."""
+        if b is None:
+            b = self._learn_bufs(states, acts)
+        n, F = b["x"].shape
+        if vt is not None:
+            b["vt"].copy_(vt.reshape(-1))
         if self._step_table.capacity < self._step + 2:
             self._step_table.ensure(max(self._step + 2, 2 * self._step_table.capacity))
         if self._graph_tab_version != self._step_table.version:
