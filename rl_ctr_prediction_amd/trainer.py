@@ -213,6 +213,10 @@ class FusedCTRTrainer:
         # FM's dense tail fused into one launch (ctr_fm_step_tail); CTR_FM_TAIL=0: the four
         # separate launches (A/B)
         self.fm_tail = os.environ.get("CTR_FM_TAIL", "1") != "0"
+        # a step whose plan was built ahead catches its rows up over the plan's unique rows
+        # (ctr_adam_deferred_rows, one launch) instead of marking owners from the ids first
+        # (CTR_CATCHUP_BY_PLAN=0: the id-driven pair, A/B)
+        self.catchup_by_plan = os.environ.get("CTR_CATCHUP_BY_PLAN", "1") != "0"
         # catch-up ahead (step(next_x=)): the next batch's rows that this batch does not touch
         # are brought to this step on the plan stream while it runs (_catchup_ahead). Off by
         # default: bitwise correct, but measured slower on MI355X — the replay beside the
@@ -712,10 +716,19 @@ class FusedCTRTrainer:
                 plan()
             if not have_ca:  # else: caught up during the previous step (_catchup_ahead)
                 t = self._mark("adam")
-                hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                                                  self.last, x, self.rowmap, self.step_done,
-                                                  self.step_table, step_hint, self.betas,
-                                                  self.eps, self.weight_decay)
+                if have_plan and self.catchup_by_plan:
+                    # the plan built ahead lists the batch's unique rows: one launch over
+                    # them instead of the owner-marking pass + the id-driven catch-up
+                    hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                                               self.last, b.plan, step_hint, self.step_table,
+                                               self.betas, self.eps, self.weight_decay,
+                                               step_dev=self.step_done)
+                else:
+                    hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w,
+                                                      self.v_w, self.last, x, self.rowmap,
+                                                      self.step_done, self.step_table,
+                                                      step_hint, self.betas, self.eps,
+                                                      self.weight_decay)
                 self._span("adam", t)
             if not self.plan_first:
                 plan()
