@@ -314,9 +314,9 @@ int ctr_adam_dense(float* p, const float* g, float* m, float* v, int64_t n, doub
                    double beta1, double beta2, double eps, double weight_decay,
                    ctr_stream_t stream);
 /* ctr_adam_dense_planes: ctr_adam_dense that also rewrites the bf16 planes (ctr_planes) of
- *   up to two row-major [rows, cols] sub-matrices of p (the MLP weights: p[offset + r*cols
+ *   up to three row-major [rows, cols] sub-matrices of p (the MLP weights: p[offset + r*cols
  *   + c]) with the updated values, so the next step's plane GEMMs need no ctr_split_planes.
- *   offset % 4 == 0, cols % 4 == 0, n % 4 == 0, 16-B aligned vectors.
+ *   offset % 4 == 0, n % 4 == 0, 16-B aligned vectors; any cols (a multiple of 4 is faster).
  *   Replaces: the same optimizer.step; the planes are this framework's GEMM operand format. */
 typedef struct ctr_plane_view {
   int64_t offset;

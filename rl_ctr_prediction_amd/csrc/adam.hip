@@ -70,7 +70,7 @@ __device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v,
 // weights the GEMMs read as bf16 planes) whose planes are rewritten with the updated values,
 // so the next step's GEMMs need no split pass. off and cols are multiples of 4: a float4
 // never straddles two rows.
-constexpr int kMaxPlaneViews = 2;
+constexpr int kMaxPlaneViews = 3;
 struct PlaneViews {
   int n;
   int64_t off[kMaxPlaneViews], len[kMaxPlaneViews], cols[kMaxPlaneViews];
@@ -97,8 +97,23 @@ __global__ __launch_bounds__(256) void adam_dense_vec(float4* __restrict__ p,
     for (int j = 0; j < kMaxPlaneViews; ++j) {
       const int64_t e = 4 * i - pv.off[j];
       if (j < pv.n && e >= 0 && e < pv.len[j]) {
-        const int64_t r = e / pv.cols[j], c = e - r * pv.cols[j];
-        store_planes4_at(pv.d[j] + r * pv.ld[j] + c, pv.ps[j], pp);
+        if (pv.cols[j] % 4 == 0) {  // the four elements share a row
+          const int64_t r = e / pv.cols[j], c = e - r * pv.cols[j];
+          store_planes4_at(pv.d[j] + r * pv.ld[j] + c, pv.ps[j], pp);
+        } else {  // rows of any width (PG's 741-wide first layer): element by element
+          const float pe[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int64_t eq = e + q;
+            if (eq < pv.len[j]) {
+              const int64_t r = eq / pv.cols[j], c = eq - r * pv.cols[j];
+              uint16_t h3[3];
+              psplit1(pe[q], h3);
+#pragma unroll
+              for (int pl = 0; pl < 3; ++pl) pv.d[j][pl * pv.ps[j] + r * pv.ld[j] + c] = h3[pl];
+            }
+          }
+        }
       }
     }
   }
@@ -741,7 +756,7 @@ extern "C" int ctr_adam_dense_planes(float* p, const float* g, float* m, float* 
     const ctr_plane_view& w = views[j];
     const ctr_planes& q = w.planes;
     CTR_REQUIRE(w.offset >= 0 && w.offset % 4 == 0 && w.rows > 0 && w.cols > 0 &&
-                    w.cols % 4 == 0 && w.offset + w.rows * w.cols <= n,
+                    w.offset + w.rows * w.cols <= n,
                 "ctr_adam_dense_planes: view %d outside the vector or not float4-aligned", j);
     CTR_REQUIRE(q.data && (uintptr_t)q.data % 16 == 0 && q.ld % 4 == 0 && q.ld >= w.cols &&
                     q.rows >= w.rows && q.plane_stride >= q.rows * q.ld,

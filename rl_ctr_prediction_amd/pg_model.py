@@ -161,11 +161,11 @@ class PolicyGradient:
             self.planes_layers = max(0, len(self._layers) - 2)
         self._wplanes = [hip_ops.Planes(l.out_features, l.in_features, dev)
                          for l in self._layers[:self.planes_layers]]
-        # weights whose planes the dense Adam rewrites itself (row length a multiple of 4,
-        # ctr_adam_dense_planes); the others are re-split at every learn. _wver: the weights'
-        # version counters when their planes were last split (load_state_dict & co. bump them)
-        self._adam_planes = [i for i in range(self.planes_layers)
-                             if self._layers[i].in_features % 4 == 0][-2:]  # <= 2 views
+        # weights whose planes the dense Adam rewrites itself (ctr_adam_dense_planes, up to
+        # three views, any row length: the 741-wide first layer too); the others are re-split
+        # at every learn. _wver: the weights' version counters when their planes were last
+        # split (load_state_dict & co. bump them)
+        self._adam_planes = list(range(self.planes_layers))[-3:]
         self._wver = None
         self._pbufs: dict = {}
         # the weight-gradient GEMMs (dW_i = g_i^T h_i) on a side stream forked where each g_i

@@ -163,14 +163,20 @@ def test_gemm_planes_epilogues_and_output_planes(cuda):
                                atol=1e-4)
 
 
-def test_adam_dense_planes_match_split(cuda):
+@pytest.mark.parametrize("views", [
+    [(4, 300, 64), (4 + 300 * 64 + 8, 200, 300)],
+    # rows not a multiple of 4 wide (PG's 741-wide first layer) and three views
+    [(0, 37, 741), (37 * 741 + 3, 16, 1024), (37 * 741 + 3 + 16 * 1024 + 4, 5, 13)],
+])
+def test_adam_dense_planes_match_split(cuda, views):
     """ctr_adam_dense_planes: the parameter update is bitwise ctr_adam_dense's, and the
     planes it rewrites equal split_planes of the updated sub-matrices."""
     H = _H()
     g = torch.Generator().manual_seed(1)
-    n = 4 + 300 * 64 + 8 + 200 * 300 + 4
+    views = [((off + 3) // 4 * 4, r, c) for off, r, c in views]  # 16-B aligned offsets
+    end = max(off + r * c for off, r, c in views)
+    n = (end + 4 + 3) // 4 * 4
     p0, gr = torch.randn(n, generator=g), torch.randn(n, generator=g) * 1e-2
-    views = [(4, 300, 64), (4 + 300 * 64 + 8, 200, 300)]
     outs = []
     for planes in (None, [(off, H.Planes(r, c, cuda)) for off, r, c in views]):
         p, m, v = p0.clone().to(cuda), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
