@@ -452,6 +452,14 @@ int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin, 
 int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int F, int K,
                                   int64_t V, const float* emb, float* out, int32_t* err_flag,
                                   ctr_stream_t stream);
+/* ctr_feature_embedding_forward_planes: the same, and the state's three exact bf16 planes
+ *   (ctr_planes, >= [B, F(F-1)/2 + F*K]) for the planes GEMM of the policy's first layer
+ *   (out_planes NULL: the plain call). Replaces: Feature_embedding.py:51-59 feeding
+ *   PG_model.py:52 (the first nn.Linear of Net). */
+int ctr_feature_embedding_forward_planes(const void* idx, int idx_type, int64_t B, int F,
+                                         int K, int64_t V, const float* emb, float* out,
+                                         const ctr_planes* out_planes, int32_t* err_flag,
+                                         ctr_stream_t stream);
 
 /* ------------------------------------------ §8f: binary on-disk batches (host) -----
  * ctr_csv_to_bin: the reference's encoded CSV (`label,idx_1..idx_F` per line,

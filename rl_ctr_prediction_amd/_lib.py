@@ -137,6 +137,8 @@ SIGNATURES = {
                                        _f64, _f64, _f64, _f64, _vp]),
     "ctr_feature_embedding_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp,
                                              _vp]),
+    "ctr_feature_embedding_forward_planes": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp,
+                                                    _vp, _planes_p, _vp, _vp]),
     "ctr_ensemble_preds": (_i32, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp,
                                   _vp, _vp, _vp]),
     "ctr_ffm_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _f32,

@@ -241,7 +241,8 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
 template <typename IdxT>
 __global__ __launch_bounds__(256) void feature_embedding_kernel(
     const IdxT* __restrict__ idx, int64_t B, int F, int K, int64_t V,
-    const float* __restrict__ emb, float* __restrict__ out, int32_t* err) {
+    const float* __restrict__ emb, float* __restrict__ out, int32_t* err,
+    uint16_t* __restrict__ xpl = nullptr, int64_t xpl_ld = 0, int64_t xpl_ps = 0) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
@@ -269,6 +270,21 @@ __global__ __launch_bounds__(256) void feature_embedding_kernel(
     float acc = 0.f;
     for (int k = 0; k < K; ++k) acc += ei[k] * ej[k];
     ob[p] = acc;
+    if (xpl) {
+      uint16_t h3[3];
+      psplit1(acc, h3);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xpl[q * xpl_ps + b * xpl_ld + p] = h3[q];
+    }
+  }
+  if (xpl) {  // the flat part's planes (columns P ..), from the staged tile
+    for (int t = lane; t < F * K; t += kWave) {
+      const int f = t / K, k = t - f * K;
+      uint16_t h3[3];
+      psplit1(tile[f * ld + k], h3);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xpl[q * xpl_ps + b * xpl_ld + P + t] = h3[q];
+    }
   }
 }
 
@@ -446,10 +462,17 @@ extern "C" int ctr_deepfm_head_planes(const float* h, int64_t B, int H, const fl
   return CTR_OK;
 }
 
-extern "C" int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int F,
-                                             int K, int64_t V, const float* emb, float* out,
-                                             int32_t* err_flag, ctr_stream_t stream) {
+extern "C" int ctr_feature_embedding_forward_planes(const void* idx, int idx_type, int64_t B,
+                                                    int F, int K, int64_t V, const float* emb,
+                                                    float* out, const ctr_planes* out_planes,
+                                                    int32_t* err_flag, ctr_stream_t stream) {
   CTR_REQUIRE(idx && emb && out, "ctr_feature_embedding_forward: null pointer");
+  const int64_t W = (int64_t)F * (F - 1) / 2 + (int64_t)F * K;
+  CTR_REQUIRE(!out_planes || (out_planes->data && out_planes->rows >= B &&
+                              out_planes->cols >= W && out_planes->ld >= W &&
+                              out_planes->plane_stride >= out_planes->rows * out_planes->ld),
+              "ctr_feature_embedding_forward_planes: planes smaller than the state [B, %lld]",
+              (long long)W);
   CTR_REQUIRE(B >= 0 && F > 1 && K > 0 && V > 0, "ctr_feature_embedding_forward: bad sizes");
   CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
   const size_t lds = (size_t)4 * F * (K + 1) * sizeof(float);
@@ -457,12 +480,24 @@ extern "C" int ctr_feature_embedding_forward(const void* idx, int idx_type, int6
   if (B == 0) return CTR_OK;
   hipStream_t st = as_stream(stream);
   const unsigned grid = (unsigned)ceil_div(B, 4);
+  uint16_t* xpl = out_planes ? static_cast<uint16_t*>(out_planes->data) : nullptr;
+  const int64_t xld = out_planes ? out_planes->ld : 0;
+  const int64_t xps = out_planes ? out_planes->plane_stride : 0;
   if (idx_type == CTR_IDX_I64)
     hipLaunchKernelGGL(feature_embedding_kernel<int64_t>, grid, 256, lds, st,
-                       static_cast<const int64_t*>(idx), B, F, K, V, emb, out, err_flag);
+                       static_cast<const int64_t*>(idx), B, F, K, V, emb, out, err_flag, xpl,
+                       xld, xps);
   else
     hipLaunchKernelGGL(feature_embedding_kernel<int32_t>, grid, 256, lds, st,
-                       static_cast<const int32_t*>(idx), B, F, K, V, emb, out, err_flag);
+                       static_cast<const int32_t*>(idx), B, F, K, V, emb, out, err_flag, xpl,
+                       xld, xps);
   CTR_LAUNCH_CHECK("ctr_feature_embedding_forward");
   return CTR_OK;
+}
+
+extern "C" int ctr_feature_embedding_forward(const void* idx, int idx_type, int64_t B, int F,
+                                             int K, int64_t V, const float* emb, float* out,
+                                             int32_t* err_flag, ctr_stream_t stream) {
+  return ctr_feature_embedding_forward_planes(idx, idx_type, B, F, K, V, emb, out, nullptr,
+                                              err_flag, stream);
 }

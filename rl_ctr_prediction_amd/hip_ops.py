@@ -739,14 +739,24 @@ def adam_deferred_flush(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step: int,
 
 
 # ------------------------------------------------------------- Feature_Embedding ----
-def feature_embedding(idx: torch.Tensor, emb: torch.Tensor, err_flag=None) -> torch.Tensor:
+def feature_embedding(idx: torch.Tensor, emb: torch.Tensor, err_flag=None,
+                      out_planes: "Planes | None" = None) -> torch.Tensor:
+    """Feature_Embedding's state [B, F(F-1)/2 + F*K]; out_planes: also write its three bf16
+    planes (the first planes GEMM's A operand)."""
     idx, it = _idx(idx)
     _f32(emb, "feature_embedding.weight")
     B, F = idx.shape
     V, K = emb.shape
-    out = torch.empty(B, F * (F - 1) // 2 + F * K, dtype=torch.float32, device=emb.device)
-    lib.ctr_feature_embedding_forward(_p(idx), it, B, F, K, V, _p(emb), _p(out), _p(err_flag),
-                                      _stream())
+    W = F * (F - 1) // 2 + F * K
+    out = torch.empty(B, W, dtype=torch.float32, device=emb.device)
+    if out_planes is None:
+        lib.ctr_feature_embedding_forward(_p(idx), it, B, F, K, V, _p(emb), _p(out),
+                                          _p(err_flag), _stream())
+        return out
+    if out_planes.rows < B or out_planes.cols < W or out_planes.device != emb.device:
+        raise ValueError(f"feature_embedding: out_planes must hold [{B}, {W}] on {emb.device}")
+    lib.ctr_feature_embedding_forward_planes(_p(idx), it, B, F, K, V, _p(emb), _p(out),
+                                             out_planes.desc, _p(err_flag), _stream())
     return out
 
 

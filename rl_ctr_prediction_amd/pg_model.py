@@ -352,7 +352,18 @@ class PolicyGradient:
         n_episode transitions split over the data-parallel ranks."""
         net = self.policy_net
         training = net.training
-        x0 = net._state(states)
+        P = self.planes_layers
+        fe = net.embedding_layer
+        E = fe.feature_embedding.weight if type(fe) is Feature_Embedding else None
+        if (P and E is not None and states.dim() == 2 and
+                (lambda F, K: F * (F - 1) // 2 + F * K)(states.shape[1], E.shape[1])
+                == net.input_dims):
+            # the state and the first planes layer's input planes in one pass (no split)
+            pb = self._planes_bufs(states.shape[0])
+            x0 = hip_ops.feature_embedding(states, E.detach(), out_planes=pb["hp"][0])
+            x0_planes = True
+        else:  # (a width mismatch raises the reference's shape error here)
+            x0, x0_planes = net._state(states), False
         n = x0.shape[0]
         n_ep = n if n_episode is None else n_episode
         acts_l = []
@@ -369,7 +380,8 @@ class PolicyGradient:
                 if i not in self._adam_planes or ver != self._wver:
                     hip_ops.split_planes(self._layers[i].weight, out=self._wplanes[i])
             self._wver = ver
-            hip_ops.split_planes(x0.contiguous(), out=pb["hp"][0])
+            if not x0_planes:
+                hip_ops.split_planes(x0.contiguous(), out=pb["hp"][0])
         for i, lin in enumerate(self._layers):
             last = i == len(self._layers) - 1
             off = base + row0 * lin.out_features

@@ -244,3 +244,20 @@ def test_gemm_planes_last_col(cuda, M, N, K):
     y = H.gemm_planes(px, H.split_planes(Y.t().contiguous().to(cuda)), False, False)
     yref = X.double() @ Y.double()
     assert ((y.cpu().double() - yref).abs() <= 2e-6 * (X.double().abs() @ Y.double().abs()) + 1e-30).all()
+
+
+@pytest.mark.parametrize("F,K,B", [(26, 16, 300), (5, 3, 7)])
+def test_feature_embedding_planes_match_split(cuda, F, K, B):
+    """ctr_feature_embedding_forward_planes: the state is bitwise the plain call's and its
+    planes equal split_planes of it (the PG first layer's A operand)."""
+    H = _H()
+    g = torch.Generator().manual_seed(3)
+    V = 1000
+    E = (torch.randn(V, K, generator=g) * 0.1).to(cuda)
+    x = torch.randint(0, V, (B, F), generator=g).to(cuda)
+    W = F * (F - 1) // 2 + F * K
+    pl = H.Planes(B, W, cuda)
+    a = H.feature_embedding(x, E)
+    b = H.feature_embedding(x, E, out_planes=pl)
+    assert torch.equal(a, b)
+    assert torch.equal(pl.t, H.split_planes(a).t)
