@@ -256,9 +256,10 @@ class FusedCTRTrainer:
             self._plan_stream = torch.cuda.Stream(device=self.device)
         # lookahead plans may alternate over n_plan_streams streams (each key keeps its own:
         # its captured graph holds that stream's scratch), two plans in flight at once.
-        # Default 1: measured at C2, two streams 47.0 / 45.4 vs one 48.0 / 49.7 M ex/s (the
-        # plans then contend with each other and the step; C5 unchanged)
-        self.n_plan_streams = int(os.environ.get("CTR_PLAN_STREAMS", "1"))
+        # Default 2: with the host off the step's critical path (step(): 30 us of Python),
+        # C2 two streams 50.5 / 54.8 / 53.4 vs one 50.5 / 48.9 / 47.3 M ex/s (alternating
+        # runs, tools/c2_knobs3.sh); while the host paced the step one stream measured faster
+        self.n_plan_streams = int(os.environ.get("CTR_PLAN_STREAMS", "2"))
         self._extra_plan_streams: list = []
         self._plan_stream_of: dict = {}
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
