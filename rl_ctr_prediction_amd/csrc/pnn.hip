@@ -90,11 +90,18 @@ __global__ __launch_bounds__(256) void ipnn_backward_kernel(const IdxT* __restri
   for (int t = lane; t < F * K; t += kWave) {  // output (f, k), contiguous per example
     const int f = t / K, k = t - f * K;
     float g = db[t];
-    for (int j = 0; j < F; ++j) {
-      if (j == f) continue;
-      const float w = dp[j < f ? pair_index(j, f, F) : pair_index(f, j, F)];
-      g += w * tile[j * ld + k];
+    // j ascending, j != f (the reference's order): pairs (j, f) for j < f sit at strides
+    // F - j - 2 from pair_index(0, f) = f - 1; pairs (f, j) for j > f are contiguous from
+    // pair_index(f, f + 1) — no per-j branch or index arithmetic, so the loops unroll
+    int q = f - 1;
+#pragma unroll 4
+    for (int j = 0; j < f; ++j) {
+      g += dp[q] * tile[j * ld + k];
+      q += F - j - 2;
     }
+    const int base = (f * (2 * F - f - 1)) / 2 - (f + 1);  // dp[base + j] = pair (f, j)
+#pragma unroll 4
+    for (int j = f + 1; j < F; ++j) g += dp[base + j] * tile[j * ld + k];
     out[t] = g;
   }
 }
