@@ -86,6 +86,12 @@ def gather_bytes(S, K, B, deep):
     return S * (8 + 4 * K + 4) + B * 4 * K + (S * 4 * K if deep else 0) + B * 16
 
 
+def ipnn_gather_bytes(S, K, B, F):
+    """ipnn_forward_kernel: int64 ids (8 B/slot) and the gathered row (4K B/slot) read, the MLP
+    input [B, F*K + F(F-1)/2] written (fp32)."""
+    return S * (8 + 4 * K) + B * 4 * (F * K + F * (F - 1) // 2)
+
+
 def scatter_bytes(S, K, U, deep, apply=False):
     """fm_embedding_grad: per slot its plan entries (12 B) and example terms (4 B gz +
     4K B sum_e), for DeepFM the MLP-input gradient row (4K B); per unique row the table
@@ -372,7 +378,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--batches", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--batches", type=int, default=0,
+                    help="0 (default): a fresh synthetic batch for every step (streaming, as the "
+                         "reference trains: all_main/pretrain_main.py:71-78); N > 0: N distinct "
+                         "batches cycled")
+    ap.add_argument("--flush-every", type=int, default=None,
+                    help="deferred Adam: flush every N steps (bounded staleness; default: the "
+                         "trainer's, CTR_FLUSH_EVERY or 32; 0 = only at the region end)")
     ap.add_argument("--breakdown-steps", type=int, default=10,
                     help="un-timed steps with every kernel group instrumented (kernel table)")
     ap.add_argument("--sharding", default="auto", choices=["auto", "rows", "replicated"],
@@ -419,11 +431,16 @@ def main():
                  "IPNN": lambda: InnerPNN(V, F, K)}[cfg["kind"]]()
     model.train()
     synth = CriteoSynth(V, F, seed=1)
-    # every distinct batch is seen during the warm-up, so its HIP graph is captured there
-    n_batches = max(1, min(args.batches, args.warmup))
-    host_batches = list(synth.batches(n_batches, B, rank=rank))
+    n_bd = max(1, min(args.steps, args.breakdown_steps))
+    # streaming (default): every step of the warm-up, the breakdown pass and the timed region
+    # trains on a batch of its own (the roofline pass after the region revisits the timed
+    # region's batches); the HIP graphs are keyed by input slot, not by batch
+    n_batches = args.batches if args.batches > 0 else args.warmup + n_bd + args.steps
+    t_gen = time.perf_counter()
+    host_batches = synth.stream(n_batches, B, rank=rank, threads=min(16, os.cpu_count() or 1))
     xs = [torch.from_numpy(x).to(dev) for x, _ in host_batches]
     ys = [torch.from_numpy(y).to(dev) for _, y in host_batches]
+    log(f"{n_batches} distinct batches generated in {time.perf_counter() - t_gen:.1f}s")
     sharding = args.sharding
     if sharding == "auto":
         sharding = "rows" if world > 1 and args.optimizer == "deferred" else "replicated"
@@ -433,6 +450,8 @@ def main():
         trainer = FusedCTRTrainer(model, lr=1e-3, weight_decay=1e-5, seed=1234,
                                   optimizer_mode=args.optimizer)
     trainer.sweep_slices = args.sweep_slices
+    if args.flush_every is not None:
+        trainer.flush_every = args.flush_every
     log(f"rank {rank}/{world}: {cfg['kind']} V={V} K={K} B={B} ready in {time.perf_counter() - t0:.1f}s")
 
     # one running batch index over every loop below, so each step's lookahead batch is the
@@ -456,8 +475,7 @@ def main():
 
     # breakdown pass (NOT timed): every kernel group bracketed by HIP events, to find the
     # dominant kernel and report the per-kernel table
-    keys = ("adam", "gather", "plan", "scatter", "flush", "gemm", "exchange", "sweep")
-    n_bd = max(1, min(args.steps, args.breakdown_steps))
+    keys = ("adam", "catchup", "gather", "plan", "scatter", "flush", "gemm", "exchange", "sweep")
     trainer.flush()
     trainer.timing = {k: [] for k in keys}
     for i in range(n_bd):
@@ -470,7 +488,7 @@ def main():
     fused_apply = (world == 1 and args.optimizer == "deferred" and isinstance(
         trainer, FusedCTRTrainer) and not isinstance(trainer, ShardedCTRTrainer)
         and trainer.fuse_apply and trainer._vec_ok and trainer.K >= 32)
-    dominant = max(("adam", "gather", "plan", "scatter", "gemm", "flush"),
+    dominant = max(("adam", "catchup", "gather", "plan", "scatter", "gemm", "flush"),
                    key=lambda k: per_step[k])
 
     if world > 1:
@@ -498,7 +516,7 @@ def main():
     # cannot carry timing events: hipErrorInvalidHandle); kernel durations do not depend
     # on how the kernel was launched, and the rocprofv3 trace of the graph-replayed run
     # (profiles/) is the cross-check
-    trainer.timing = {dominant: [], "flush": []}
+    trainer.timing = {dominant: [], "flush": [], "catchup": []}
     for i in range(args.steps):
         step(i)
     trainer.flush()
@@ -515,6 +533,11 @@ def main():
                  f"by HIP events; ms per step",
         "adam_rows" if args.optimizer == "deferred" else "adam_embedding_vec":
             {"ms_per_step": per_step["adam"]},
+        "catch-up (deferred rows of the batch replayed before the forward)": {
+            "ms_per_step": per_step["catchup"],
+            "ms_per_step_after_region": total_ms(timing["catchup"]) / args.steps,
+            "_note": "second figure: the roofline pass's K eager steps right after the timed "
+                     "region (staleness as deep as the region's flushes allow)"},
         "flush (deferred_flush_tile, once per region)": {"ms_per_step": per_step["flush"]},
         "_graphs": "timed region: HIP-graph replay of the whole step (N=1); breakdown and "
                    "roofline passes: eager launches with HIP events",
@@ -548,7 +571,7 @@ def main():
             roofline["mfma_busy"], roofline["mfma_busy_source"] = busy
         traffic, src = load_traffic(args.config, "gemm")
     else:
-        if dominant == "adam":
+        if dominant in ("adam", "catchup"):
             if args.optimizer == "dense":
                 nbytes = adam_bytes(V, K, U)
                 kname = "adam_embedding_vec (dense Adam over E[V,K] + w[V])"
@@ -560,7 +583,9 @@ def main():
             kname = ("deferred_flush_tile (every row of the table brought to the region's last "
                      "step, once per timed region)")
         elif dominant == "gather":
-            nbytes, kname = gather_bytes(S, K, B, deep), "fm_forward_vec (embedding gather + FM)"
+            nbytes, kname = ((ipnn_gather_bytes(S, K, B, F), "ipnn_forward_kernel")
+                             if cfg["kind"] == "IPNN" else
+                             (gather_bytes(S, K, B, deep), "fm_forward_vec (embedding gather + FM)"))
         elif dominant == "scatter":
             nbytes = scatter_bytes(S, K, U, deep, apply=fused_apply)
             kname = ("seg_chunk_kernel + seg_combine_apply_kernel (per-row gradient sums with "
@@ -579,9 +604,17 @@ def main():
                      "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each launch of this "
                                "kernel over K eager steps right after the timed region"})
-    kernels["flush (deferred_flush_tile, once per region)"]["region_of_K_steps_ms_total"] = \
-        total_ms(timing["flush"])
+    kernels["flush (deferred_flush_tile, every flush_every steps and at the region end)"] = \
+        kernels.pop("flush (deferred_flush_tile, once per region)")
+    kernels["flush (deferred_flush_tile, every flush_every steps and at the region end)"].update(
+        region_of_K_steps_ms_total=total_ms(timing["flush"]), flushes=len(timing["flush"]))
     gather_ms, scatter_ms = avg_ms(bd["gather"]), avg_ms(bd["scatter"])
+    if cfg["kind"] == "IPNN":
+        g_kernel, g_bytes = "ipnn_forward_kernel (gather + pair dots -> MLP input)", \
+            ipnn_gather_bytes(S, K, B, F)
+    else:
+        g_kernel, g_bytes = "fm_forward_vec (gather + FM" + (
+            ", MLP input as bf16 planes)" if deep else ")"), gather_bytes(S, K, B, deep)
     value = world * B * args.steps / elapsed
     result = {
         "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
@@ -597,14 +630,17 @@ def main():
                        " (replicated tables, sparse row-grad all-gather)" if world > 1 else ""),
                    "optimizer": f"dense Adam lr=1e-3 wd=1e-5 (reference semantics), "
                                 f"{args.optimizer} mode",
+                   "batches": ("fresh: one synthetic batch per step" if args.batches <= 0
+                               else f"{args.batches} distinct, cycled"),
+                   "flush_every": getattr(trainer, "flush_every", None),
                    "plan_lookahead": (args.lookahead if isinstance(trainer, ShardedCTRTrainer)
                                       or (getattr(trainer, "plan_lookahead", False)
                                           and args.optimizer == "deferred") else 0)},
         "roofline": roofline,
         "kernels": kernels,
         "gather_scatter": {
-            "gather_kernel": "fm_forward_vec", "gather_ms": gather_ms,
-            "gather_GBps": gather_bytes(S, K, B, deep) / (gather_ms * 1e-3) / 1e9,
+            "gather_kernel": g_kernel, "gather_ms": gather_ms,
+            "gather_GBps": g_bytes / (gather_ms * 1e-3) / 1e9,
             "scatter_kernels": ("seg_chunk_kernel + seg_combine_apply_kernel (per-row sums "
                                 "and the fused deferred-Adam apply of the batch's rows"
                                 if fused_apply else

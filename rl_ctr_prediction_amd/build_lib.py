@@ -24,7 +24,7 @@ ARCH = os.environ.get("CTR_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["abi.cpp", "fm_forward.hip", "sparse_plan.hip", "sparse_grad.hip", "adam.hip",
            "gemm.hip", "gemm_sb16.hip", "gemm_planes.hip", "reduce_pg.hip", "pnn.hip", "io.cpp", "ensemble.hip", "ffm.hip",
            "layout.hip"]
-HEADERS = [CSRC / "ctr_common.h", CSRC / "gemm_common.h", ROOT / "include" / "ctr_hip.h"]
+INCLUDE_DIRS = [CSRC, ROOT / "include"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
             "-Wall", "-Wno-unused-function", "-I", str(ROOT / "include")]
@@ -38,11 +38,31 @@ def _hipcc() -> str:
                        "libctr_hip.so")
 
 
+def _deps(src: Path, seen: set | None = None) -> set:
+    """src and every local header it includes, transitively (`#include "..."` lines
+    resolved against the source's directory, csrc/ and include/)."""
+    seen = set() if seen is None else seen
+    if src in seen:
+        return seen
+    seen.add(src)
+    for line in src.read_text(errors="replace").splitlines():
+        line = line.strip()
+        if not line.startswith("#include") or '"' not in line:
+            continue
+        name = line.split('"')[1]
+        for d in [src.parent, *INCLUDE_DIRS]:
+            h = d / name
+            if h.exists():
+                _deps(h.resolve(), seen)
+                break
+    return seen
+
+
 def _stale(obj: Path, src: Path) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in [src, *HEADERS])
+    return any(p.stat().st_mtime > t for p in _deps(src.resolve()))
 
 
 def _compile(hipcc: str, src: Path, obj: Path) -> None:

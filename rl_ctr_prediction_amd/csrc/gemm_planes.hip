@@ -55,6 +55,9 @@ struct PlanesArgs {
   uint16_t* cpl;        // output planes (nullptr: none)
   int64_t cpl_ld, cpl_ps;
   float* last_col;      // non-null: result column N-1 goes to last_col[m], C has N-1 columns
+  int xcd_ngroups;      // tiles partitioned over the 8 XCDs as (8/g) M-groups x g N-groups
+  int splits;           // > 1: split-K, (tile, split) flattened into blockIdx.x (see below)
+  int64_t tiles;        // output tiles per split
 };
 
 // ---- LDS image swizzles ----------------------------------------------------------------
@@ -99,6 +102,19 @@ __device__ __forceinline__ const uint16_t* piece_rc(const PlaneSrc& s, int plane
   return s.p + plane * s.ps + (k0 + kr) * s.ld + col + 8 * (pc & 1);
 }
 
+// An RC operand tile wider than 128 (the weight gradients' whole-M tiles: 192, 256, 320)
+// is held as several [32 k][64] images side by side (4 KiB each per plane); 64 and 128 are
+// one image. Piece c of a plane: image c / (R/16), piece c % (R/16) of that image.
+template <int BX>
+constexpr int rc_img() { return BX == 128 ? 128 : 64; }
+
+template <int R>
+__device__ __forceinline__ const uint16_t* piece_rc_img(const PlaneSrc& s, int plane, int c,
+                                                        int64_t col0, int64_t k0, int lane) {
+  constexpr int PPI = R / 16;  // 1 KiB pieces per image
+  return piece_rc<R>(s, plane, c % PPI, col0 + (int64_t)R * (c / PPI), k0, lane);
+}
+
 // ---- fragment reads ---------------------------------------------------------------
 // Byte offsets (within one plane image) of a lane's fragment reads: computed once per
 // kernel, so the k loop issues bare LDS reads.
@@ -112,6 +128,11 @@ __device__ __forceinline__ int frag_rc_off(int cb, int lane, int j) {
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int k = 8 * g + 4 * j + q;
   return k * (2 * R) + 32 * ((cb >> 4) ^ rc_swz<R>(k)) + 8 * pp;
+}
+
+template <int R>
+__device__ __forceinline__ int frag_rc_img_off(int cb, int lane, int j) {
+  return (cb / R) * (R * kPBK * 2) + frag_rc_off<R>(cb % R, lane, j);
 }
 
 __device__ __forceinline__ pbf16x8 frag_kc_at(const char* p) {
@@ -147,10 +168,11 @@ __device__ __forceinline__ void store_planes4(const PlanesArgs& a, int64_t m, in
 // through a wave-private [16][WN+4] LDS strip, then row-contiguous float4 stores
 template <int TM, int TN>
 __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[TM][TN],
-                                             float* strip, int64_t mb, int64_t nb, int lane) {
+                                             float* strip, int64_t mb, int64_t nb, int lane,
+                                             int64_t split) {
   constexpr int WN = 16 * TN, LD = WN + 4, C4 = WN / 4;
   const GemmArgs& g = a.g;
-  float* C = g.C + (int64_t)blockIdx.z * g.slab_stride;
+  float* C = g.C + split * g.slab_stride;
   const bool slab = g.slab_stride != 0;
   const int epi = slab ? (int)CTR_EPI_NONE : g.epi;
   GemmArgs ge = g;
@@ -196,6 +218,27 @@ __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[
   }
 }
 
+// Block -> output tile. Under round-robin dispatch blocks b, b+8, b+16... share an XCD; the
+// tiles are dealt so that each XCD owns a contiguous (M-group x N-group) sub-grid and walks
+// it M-row by M-row (the row's tiles back to back, its A strip L2-hot for all of them):
+// g = 1 gives each XCD whole M rows (every XCD reads all of B), g = 2 gives each XCD half
+// of the N tiles of a quarter of the M rows (dX: each XCD's share of W0 is 1.6 of 3.2 MB,
+// so it stays in the 4 MiB L2 beside the streamed dH1 rows). Falls back to g = 1, then to
+// the identity, where the grid does not divide.
+__device__ __forceinline__ int64_t planes_tile_index(int64_t gn, int g) {
+  const int64_t T = gridDim.x;
+  const int64_t b = blockIdx.x;
+  if (T % 8 != 0) return b;
+  const int64_t x = b % 8, i = b / 8;
+  const int64_t gm = T / gn;
+  if (g > 1 && 8 % g == 0 && gn % g == 0 && gm % (8 / g) == 0) {
+    const int64_t gnn = gn / g, gmm = gm / (8 / g);
+    const int64_t mt = (x / g) * gmm + i / gnn, nt = (x % g) * gnn + i % gnn;
+    return mt * gn + nt;
+  }
+  return x * (T / 8) + i;
+}
+
 // ---- the kernel ---------------------------------------------------------------------
 // Block = WAVES_M x WAVES_N waves, tile BM x BN; a wave owns (BM/WAVES_M) x (BN/WAVES_N) as
 // TM x TN 16x16 accumulators (x2: the a0b0 accumulator and the small-products one).
@@ -210,8 +253,9 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile in 16x16 MFMA blocks");
-  static_assert(!A_RC || BM == 64 || BM == 128, "RC operand tiles of 64 or 128");
-  static_assert(!B_RC || BN == 64 || BN == 128, "RC operand tiles of 64 or 128");
+  static_assert(!A_RC || BM == 128 || BM % 64 == 0, "RC operand tiles of 128 or 64 * n");
+  static_assert(!B_RC || BN == 128 || BN % 64 == 0, "RC operand tiles of 128 or 64 * n");
+  constexpr int RA = rc_img<BM>(), RB = rc_img<BN>();  // RC image widths
   static_assert(NS >= 2 && NS <= 7, "2- to 7-deep LDS ring");
   static_assert(KS == 1 || KS == 2, "1 or 2 MFMA k-steps per stage");
   constexpr int A_PL = BM * kPBK * 2, B_PL = BN * kPBK * 2;  // bytes per plane image
@@ -230,10 +274,23 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   const int wn0 = (wave % WAVES_N) * WN;
 
   const int64_t gn = (a.g.N + BN - 1) / BN;
-  const int64_t tix = xcd_tile_index();
+  int64_t tix, split = 0;
+  if (a.splits > 1) {
+    // split-K: block b -> XCD b % 8 -> the XCD's contiguous range of (split, tile) pairs,
+    // split-major, so the blocks of one k range (which share both operands' k slices) run
+    // on one XCD and each operand slice is fetched into ~one L2 (grid padded to 8 | T; the
+    // padding blocks exit here, before any barrier)
+    const int64_t T = gridDim.x, b = blockIdx.x;
+    const int64_t j = (b % 8) * (T / 8) + b / 8;
+    if (j >= a.tiles * a.splits) return;
+    split = j / a.tiles;
+    tix = j % a.tiles;
+  } else {
+    tix = planes_tile_index(gn, a.xcd_ngroups);
+  }
   const int64_t m0 = (tix / gn) * BM;
   const int64_t n0 = (tix % gn) * BN;
-  const int64_t kb = (int64_t)blockIdx.z * a.k_per_split;
+  const int64_t kb = split * a.k_per_split;
   const int64_t ke = min(a.Kp, kb + a.k_per_split);
   const int nt = kb < ke ? (int)((ke - kb) / (kPBK * KS)) : 0;  // stages
 
@@ -260,7 +317,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     const int plane = r / (BM / 16), c = r % (BM / 16);
     ldsA[j] = ks * SUB + plane * A_PL + c * 1024;
     const int64_t k0 = kb + ks * kPBK;
-    const uint16_t* p = A_RC ? piece_rc<A_RC ? BM : 64>(SA, plane, c, m0, k0, lane)
+    const uint16_t* p = A_RC ? piece_rc_img<RA>(SA, plane, c, m0, k0, lane)
                              : piece_kc(SA, plane, c, m0, k0, lane);
     offA[j] = (uint32_t)((const char*)p - (const char*)SA.p);
   }
@@ -271,7 +328,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     const int plane = r / (BN / 16), c = r % (BN / 16);
     ldsB[j] = ks * SUB + 3 * A_PL + plane * B_PL + c * 1024;
     const int64_t k0 = kb + ks * kPBK;
-    const uint16_t* p = B_RC ? piece_rc<B_RC ? BN : 64>(SB, plane, c, n0, k0, lane)
+    const uint16_t* p = B_RC ? piece_rc_img<RB>(SB, plane, c, n0, k0, lane)
                              : piece_kc(SB, plane, c, n0, k0, lane);
     offB[j] = (uint32_t)((const char*)p - (const char*)SB.p);
   }
@@ -294,13 +351,13 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   int aoff[TM][2], boff[TN][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    aoff[i][0] = A_RC ? frag_rc_off<A_RC ? BM : 64>(wm0 + 16 * i, lane, 0) : frag_kc_off(wm0 + 16 * i, lane);
-    aoff[i][1] = A_RC ? frag_rc_off<A_RC ? BM : 64>(wm0 + 16 * i, lane, 1) : 0;
+    aoff[i][0] = A_RC ? frag_rc_img_off<RA>(wm0 + 16 * i, lane, 0) : frag_kc_off(wm0 + 16 * i, lane);
+    aoff[i][1] = A_RC ? frag_rc_img_off<RA>(wm0 + 16 * i, lane, 1) : 0;
   }
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
-    boff[i][0] = B_RC ? frag_rc_off<B_RC ? BN : 64>(wn0 + 16 * i, lane, 0) : frag_kc_off(wn0 + 16 * i, lane);
-    boff[i][1] = B_RC ? frag_rc_off<B_RC ? BN : 64>(wn0 + 16 * i, lane, 1) : 0;
+    boff[i][0] = B_RC ? frag_rc_img_off<RB>(wn0 + 16 * i, lane, 0) : frag_kc_off(wn0 + 16 * i, lane);
+    boff[i][1] = B_RC ? frag_rc_img_off<RB>(wn0 + 16 * i, lane, 1) : 0;
   }
 
   auto compute_sub = [&](const char* st) {
@@ -368,7 +425,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] += lo[i][j];
   planes_store<TM, TN>(a, acc, reinterpret_cast<float*>(smem) + wave * 16 * (WN + 4),
-                       m0 + wm0, n0 + wn0, lane);
+                       m0 + wm0, n0 + wn0, lane, split);
 }
 
 // split-K: sum the fp32 slabs in split order (4 independent loads in flight per step of
@@ -497,17 +554,26 @@ static const PlDef kPl[] = {
     {128, 64, 4, 2, 2, 1, 0.65, 2},  // 22: 144 KB
     {64, 128, 4, 2, 2, 1, 0.65, 2},  // 23: 144 KB
     {64, 64, 2, 2, 2, 1, 0.55, 2},   // 24: 96 KB, 4 waves
+    // whole-M weight-gradient tiles (dW = G^T X over the batch, split-K): the k-strided
+    // X / H operand streams through ONCE (each of its column strips belongs to one block
+    // per split) instead of once per 64-row M tile; the narrow G^T operand is the re-read
+    // one (L2). RC images of 64 side by side.
+    {320, 64, 4, 2, 2, 1, 0.60},   // 25: 144 KB (dW0: M = 300)
+    {256, 64, 4, 2, 2, 1, 0.60},   // 26: 120 KB (dW1: M = 200)
+    {192, 64, 4, 2, 2, 1, 0.60},   // 27: 96 KB
+    {320, 64, 2, 2, 2, 1, 0.60},   // 28: 144 KB, 4 waves (TM 10)
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
 struct PlCfg {
   int tile, splits;
   int64_t kps;
+  int xg = 1;  // XCD N-groups of a single-pass launch (planes_tile_index)
 };
 
 static bool pl_valid(int ti, bool a_rc, bool b_rc) {
   const PlDef& d = kPl[ti];
-  return (!a_rc || d.bm == 64 || d.bm == 128) && (!b_rc || d.bn == 64 || d.bn == 128);
+  return (!a_rc || d.bm == 128 || d.bm % 64 == 0) && (!b_rc || d.bn == 128 || d.bn % 64 == 0);
 }
 
 // a KS = 2 tiling needs every split's k range in whole 64-deep stages
@@ -525,10 +591,11 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     return c;
   };
   if (const char* env = getenv("CTR_GEMM_PLANES_CFG")) {
-    int ti = -1, sp = 1;
-    if (sscanf(env, "%d,%d", &ti, &sp) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
+    int ti = -1, sp = 1, xg = 1;
+    if (sscanf(env, "%d,%d,%d", &ti, &sp, &xg) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
         pl_valid(ti, a_rc, b_rc)) {
-      const PlCfg c = mk(ti, sp);
+      PlCfg c = mk(ti, sp);
+      c.xg = xg == 2 || xg == 4 || xg == 8 ? xg : 1;
       if (pl_ks_ok(kPl[ti], Kp, c.kps)) return c;
     }
   }
@@ -540,8 +607,19 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   // sized to ~2 blocks per CU
   if (!a_rc && !b_rc && M >= 2048 && N > 256 && N <= 320) return mk(8, 1);
   if (!a_rc && !b_rc && M >= 2048 && N <= 256) return mk(17, 1);
-  if (!a_rc && b_rc && M >= 2048 && N >= 1024) return mk(19, 1);
+  if (!a_rc && b_rc && M >= 2048 && N >= 1024) {
+    PlCfg c = mk(19, 1);
+    c.xg = 2;  // dX: each XCD's half of the weight stays L2-resident
+    return c;
+  }
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
+  if (a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320) {
+    // whole-M tile (the wide operand read once), split-K to about one block per CU
+    const int ti = M <= 192 ? 27 : M <= 256 ? 26 : 25;
+    const int64_t tiles = ceil_div(N, 64);
+    const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(256 / tiles, Kp / 256), 64));
+    return mk(ti, s);
+  }
   if (a_rc && b_rc && Kp >= 2048) {
     // target block count of the weight-gradient GEMMs (A/B: CTR_GEMM_PLANES_WG_BLOCKS)
     static const int64_t wg_blocks = [] {
@@ -627,6 +705,10 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 22: CTR_PL_ALL4K(128, 64, 4, 2, 2, 2) break;
     case 23: CTR_PL_ALL4K(64, 128, 4, 2, 2, 2) break;
     case 24: CTR_PL_ALL4K(64, 64, 2, 2, 2, 2) break;
+    case 25: CTR_PL_ALL4(320, 64, 4, 2, 2) break;
+    case 26: CTR_PL_ALL4(256, 64, 4, 2, 2) break;
+    case 27: CTR_PL_ALL4(192, 64, 4, 2, 2) break;
+    case 28: CTR_PL_ALL4(320, 64, 2, 2, 2) break;
   }
 }
 #undef CTR_PL_AONLY
@@ -742,8 +824,12 @@ extern "C" int ctr_gemm_planes_lastcol(int a_rc, int b_rc, int64_t M, int64_t N,
   if (last_col) g.vec_c = g.vec_c && (N - 1) % 4 == 0;
   hipStream_t st = as_stream(stream);
   const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
-  CTR_REQUIRE(tiles <= INT32_MAX && c.splits <= 65535, "ctr_gemm_planes: grid too large");
-  const dim3 grid((unsigned)tiles, 1, (unsigned)c.splits);
+  CTR_REQUIRE(tiles * c.splits + 8 <= INT32_MAX, "ctr_gemm_planes: grid too large");
+  a.xcd_ngroups = c.xg;
+  a.splits = c.splits;
+  a.tiles = tiles;
+  // split-K: every (tile, split) pair in blockIdx.x, padded to a multiple of 8
+  const dim3 grid((unsigned)(c.splits > 1 ? align_up(tiles * c.splits, 8) : tiles), 1, 1);
   if (c.splits > 1) {
     PlanesArgs s = a;
     const int64_t sld = align_up(N, 4);

@@ -107,6 +107,13 @@ class FusedFFMTrainer:
         self.use_graphs = True
         self.max_graphs = 8
         self._graphs: dict = {}
+        # every batch is copied into the fixed input buffers of its shape (ids, labels), so
+        # one captured graph per shape serves a stream of fresh batches
+        self._inputs: dict = {}
+        self.captures = 0
+        # bounded staleness, as FusedCTRTrainer.flush_every
+        self.flush_every = int(os.environ.get("CTR_FLUSH_EVERY", "32"))
+        self._flushed_at = 0
         self._graph_pool = torch.cuda.graph_pool_handle()
         self._graph_tab_version = self.step_table.version
         self.timing = None  # FusedCTRTrainer's bench hook: not instrumented here
@@ -127,6 +134,7 @@ class FusedFFMTrainer:
 
     def flush(self) -> None:
         """Bring every row of every table up to the last completed step."""
+        self._flushed_at = self.step_count
         if self._dirty and self.step_count > 0:
             for tab in (self._table_args(), self._w_args()):
                 hip_ops.adam_deferred_flush(*tab, self.step_count, self.step_table, self.betas,
@@ -145,21 +153,26 @@ class FusedFFMTrainer:
             t.zero_()
         self.step_ctr.copy_(torch.tensor([0, 1], dtype=torch.int32))
         self.step_count = 0
+        self._flushed_at = 0
 
     def optimizer_state_dict(self) -> dict:
-        """torch.optim.Adam-compatible state_dict (parameter order = model.parameters():
-        linear.weight, bias, field_feature_embeddings.0..F-1.weight)."""
+        """torch.optim.Adam-compatible state_dict: parameter i is the i-th entry of
+        model.named_parameters() (for FFM: bias first — a root module's own parameters come
+        before its submodules' —, then linear.weight and the field tables)."""
         self.flush()
         V = self.V
-        m = [self.m_w, self.m_b] + [self.m_T[t * V:(t + 1) * V] for t in range(self.F)]
-        v = [self.v_w, self.v_b] + [self.v_T[t * V:(t + 1) * V] for t in range(self.F)]
-        n = len(m)
-        state = {i: {"step": torch.tensor(float(self.step_count)), "exp_avg": m[i].clone(),
-                     "exp_avg_sq": v[i].clone()} for i in range(n)}
+        moments = {"bias": (self.m_b, self.v_b), "linear.weight": (self.m_w, self.v_w)}
+        for t in range(self.F):
+            sl = slice(t * V, (t + 1) * V)
+            moments[f"field_feature_embeddings.{t}.weight"] = (self.m_T[sl], self.v_T[sl])
+        named = [n for n, _ in self.model.named_parameters()]
+        state = {i: {"step": torch.tensor(float(self.step_count)),
+                     "exp_avg": moments[n][0].clone(), "exp_avg_sq": moments[n][1].clone()}
+                 for i, n in enumerate(named)}
         return {"state": state if self.step_count else {},
                 "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
                                   "weight_decay": self.weight_decay, "amsgrad": False,
-                                  "params": list(range(n))}]}
+                                  "params": list(range(len(named)))}]}
 
     def check_errors(self) -> None:
         hip_ops.check_index_error(self.err)
@@ -188,12 +201,18 @@ class FusedFFMTrainer:
         B, F = x.shape
         if F != self.F:
             raise ValueError(f"FusedFFMTrainer: batch has {F} fields, model {self.F}")
-        if self.use_graphs and x.is_cuda and y.dtype == torch.float32 and y.is_contiguous():
+        if self._flush_due():
+            self.flush()
+        if self.use_graphs:
             return self._graph_step(x, y)
         self.step_table.ensure(self.step_count + 1)
         loss = self._launch(x, y)
         self._after_step()
         return loss
+
+    def _flush_due(self) -> bool:
+        """True when `flush_every` steps have passed since the last flush."""
+        return self.flush_every > 0 and self.step_count - self._flushed_at >= self.flush_every
 
     def _after_step(self) -> None:
         self.step_count += 1
@@ -206,17 +225,25 @@ class FusedFFMTrainer:
             torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
-        key = (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), y.data_ptr(),
-               tuple(y.shape))
+        B, F = x.shape
+        key = (B, F, x.dtype)
+        inp = self._inputs.get(key)
+        if inp is None:
+            inp = self._inputs[key] = (torch.empty(B, F, dtype=x.dtype, device=self.device),
+                                       torch.empty(B, dtype=torch.float32, device=self.device))
+        xs, ys = inp
+        xs.copy_(x, non_blocking=True)
+        ys.copy_(y.reshape(-1), non_blocking=True)
         hit = self._graphs.get(key)
         if hit is None:
-            loss = self._launch(x, y)  # the real step; also sizes every buffer
+            loss = self._launch(xs, ys)  # the real step; also sizes every buffer
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, pool=self._graph_pool):
-                    self._launch(x, y)  # captured, not executed
+                    self._launch(xs, ys)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
+                self.captures += 1
             return loss
         g, self._bufs = hit
         g.replay()

@@ -67,9 +67,11 @@ def _idx(t: torch.Tensor, name: str = "idx") -> tuple[torch.Tensor, int]:
 
 class Workspace:
     """Grow-only scratch buffer, one per (device, stream); kernels on one stream are
-    ordered, so consecutive ops can share it."""
+    ordered, so consecutive ops can share it. A buffer outgrown is retired, never freed:
+    HIP graphs captured earlier still hold its address."""
 
     _pool: dict = {}
+    _retired: list = []
 
     @classmethod
     def get(cls, nbytes: int, device: torch.device) -> torch.Tensor | None:
@@ -78,6 +80,8 @@ class Workspace:
         key = (device.index, _stream())
         buf = cls._pool.get(key)
         if buf is None or buf.numel() < nbytes:
+            if buf is not None:
+                cls._retired.append(buf)
             buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
             cls._pool[key] = buf
         return buf

@@ -287,6 +287,10 @@ class PolicyGradient:
             self._lbufs = {(n, F): b}  # the last episode size only
             self._graphs = {k: v for k, v in self._graphs.items() if k[0] == (n, F)}
         if b["x"].dtype != sdt:
+            # graphs captured against the old buffer must not replay (their key holds the
+            # dtype: switching back would read freed memory)
+            torch.cuda.synchronize(self._flat.device)
+            self._graphs.clear()
             b["x"] = torch.empty(n, F, dtype=sdt, device=self._flat.device)
         if states is None:
             torch.cat(self._ep_states, out=b["x"])
@@ -325,9 +329,23 @@ class PolicyGradient:
             self._graphs[key] = (g, static)
             return loss
         g, static = hit
+        self._sync_planes()
         g.replay()
         self._step += 1
         return static
+
+    def _sync_planes(self) -> None:
+        """Re-split the planes layers' weight planes when the fp32 weights changed outside
+        the learns (load_state_dict, in-place edits bump the version counters): a replayed
+        learn runs the graph captured at the first learn, whose version check ran then."""
+        P = self.planes_layers
+        if not P:
+            return
+        ver = tuple(self._layers[i].weight._version for i in range(P))
+        if ver != self._wver:
+            for i in range(P):
+                hip_ops.split_planes(self._layers[i].weight, out=self._wplanes[i])
+            self._wver = ver
 
 
     def _planes_bufs(self, n: int) -> dict:

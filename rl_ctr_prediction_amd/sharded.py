@@ -41,7 +41,15 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     model; gather_tables() assembles the trained tables."""
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
-                 eps: float = 1e-8, process_group=None, seed: int | None = None):
+                 eps: float = 1e-8, process_group=None, seed: int | None = None,
+                 count_group=None):
+        """process_group: the ranks sharing the table (default: the world). count_group: a
+        second communicator over the same ranks for the per-step counts exchange (it runs
+        on the plan stream beside the data collectives). Default: created here with
+        dist.new_group — a collective over the WHOLE world, so with the default
+        process_group every rank builds its trainer at the same point; trainers over a
+        sub-group must pass a count_group that every rank of the world created in the same
+        order (e.g. one of dist.new_subgroups())."""
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:
@@ -60,11 +68,37 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # previous step's kernels or collectives, and runs ahead of the GPU
         if self._plan_stream is None:
             self._plan_stream = torch.cuda.Stream(device=self.device)
-        self._count_group = None
-        if self.world_size > 1:
-            ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
-            self._count_group = dist.new_group(ranks=ranks)
+        self._count_group = count_group
+        if self.world_size > 1 and count_group is None:
+            if process_group is not None:
+                raise ValueError("ShardedCTRTrainer over a process_group needs a count_group "
+                                 "over the same ranks, created by every rank of the world "
+                                 "(dist.new_group is collective over the whole world)")
+            self._count_group = dist.new_group()
         self._ahead_counts: dict = {}
+        # lookahead plans per ids tensor (LRU): ids key -> plan buffers / pending event
+        self._plans: dict = {}
+        self._pending: dict = {}
+        self.max_plans = 16
+
+    def _plan_for(self, x) -> hip_ops.SparsePlanBuffers:
+        """The lookahead plan buffers of ids tensor x (least recently used reused first,
+        never one still pending)."""
+        key = self._xkey(x)
+        p = self._plans.pop(key, None)
+        if p is None:
+            S = x.shape[0] * x.shape[1]
+            if len(self._plans) >= self.max_plans:
+                for k in list(self._plans):
+                    if k not in self._pending:
+                        old = self._plans.pop(k)
+                        if old.capacity >= S:
+                            p = old
+                        break
+            if p is None:
+                p = hip_ops.SparsePlanBuffers(S, self.device)
+        self._plans[key] = p  # most recently used last
+        return p
 
     def _buffers(self, B: int, F: int):
         b = super()._buffers(B, F)
@@ -98,6 +132,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         has_lin = self.w_tab is not None  # InnerPNN: no linear table
 
         self._sync_weight_planes()
+        self._bound_staleness()
         main, ps = torch.cuda.current_stream(), self._plan_stream
         xkey = self._xkey(x)
         ahead = [] if next_x is None else (

@@ -120,3 +120,17 @@ class CriteoSynth:
         for _ in range(n_batches):
             x = self.ids(rng, B)
             yield x, self.labels(rng, x)
+
+    def batch(self, i: int, B: int, rank: int = 0):
+        """Batch i of an independently seeded stream (seed, rank, i): any batch can be
+        generated on its own, so a long stream is produced in parallel."""
+        rng = np.random.default_rng([self.seed, rank, 1 << 20, i])
+        x = self.ids(rng, B)
+        return x, self.labels(rng, x)
+
+    def stream(self, n_batches: int, B: int, rank: int = 0, threads: int = 8, start: int = 0):
+        """Batches start .. start + n_batches - 1 of batch(), generated on `threads` threads
+        (numpy releases the GIL in the bulk array work)."""
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            return list(ex.map(lambda i: self.batch(i, B, rank), range(start, start + n_batches)))

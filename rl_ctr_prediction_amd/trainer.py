@@ -83,6 +83,26 @@ IPNN_DENSE = DEEPFM_DENSE[1:]  # InnerPNN: the MLP only (no linear term, no bias
 _MLP_KINDS = ("DeepFM", "IPNN")
 
 
+class InputSlot:
+    """Fixed device buffers one batch is copied into before its step: the ids [B,F] (the
+    caller's dtype), the labels [B] as float32 and the batch's sparse plan. The step graph
+    of a slot is captured once against these addresses and replayed for every batch that
+    passes through the slot, so a stream of fresh batches replays the same graphs (the
+    reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
+
+    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "stream_i")
+
+    def __init__(self, shape, index: int, device):
+        B, F, dtype = shape
+        self.shape, self.index = shape, index
+        self.ids = torch.empty(B, F, dtype=dtype, device=device)
+        self.y = torch.empty(B, dtype=torch.float32, device=device)
+        self.plan = hip_ops.SparsePlanBuffers(B * F, device)
+        self.ev = None          # staged ahead: the copy + plan on the plan stream recorded here
+        self.plan_graph = None  # the plan build of this slot, captured on its plan stream
+        self.stream_i = 0
+
+
 @dataclass
 class _Bufs:
     B: int
@@ -194,22 +214,30 @@ class FusedCTRTrainer:
         env = os.environ.get("CTR_PLAN_FIRST")
         self.plan_first = (env == "1") if env in ("0", "1") else self.kind == "FM"
         self.keep_grads = False
-        # plan lookahead (step(..., next_x=)): the next batch's sparse plan is built on its
-        # own stream (own scratch workspace) concurrently with this step, OUTSIDE the step's
-        # graph (its own small graph), and the next step waits for it before it starts.
-        # Plans are kept per ids tensor (graphs hold their addresses), least recently used
-        # first out, never one a captured graph holds
-        self._plans: dict = {}
-        self._pinned_plans: set = set()
-        self._plan_graphs: dict = {}
-        self.max_plans = 16
-        self._pending: dict = {}  # ids key -> event of its plan built ahead, not yet used
+        # input staging (single process): every batch is copied into a fixed slot of its
+        # shape (InputSlot) and the step graph of that slot is replayed, so fresh batches
+        # never miss the graph cache. Plan lookahead (step(..., next_x=)): the next batches
+        # are copied into slots of their own on a plan stream and their sparse plans built
+        # there (each slot's plan build is its own small graph), concurrently with this step;
+        # the step that trains on one of them waits for it before it starts. A ring of
+        # lookahead + 1 slots per shape: a slot is restaged only after the step that used it
+        # (the plan stream waits for everything enqueued before the current step)
+        self._rings: dict = {}     # (B, F, dtype) -> [InputSlot]
+        self._staged: dict = {}    # ids key of a batch staged ahead -> its InputSlot
+        self.max_slots = 8
+        self.captures = 0          # step graphs captured (tests: bounded, batch-independent)
         # lookahead pays where the plan is the step's critical path (FM: C2 35.5 -> 50.9 M
         # ex/s); the MLP kinds build it on the graph's side list under the catch-up and the
         # forward, where it finishes long before the scatter needs it, while a lookahead plan
         # runs under dX / the scatter and slows them (C3 12.8 vs 12.7 M ex/s)
         env = os.environ.get("CTR_PLAN_LOOKAHEAD")
         self.plan_lookahead = (env == "1") if env in ("0", "1") else self.kind == "FM"
+        # bounded staleness of deferred Adam: every `flush_every` steps all rows are brought
+        # to the current step (one tiled flush pass), so a row a batch touches has missed at
+        # most that many steps and the in-step catch-up replays stay short under a stream
+        # of fresh batches (0: only at forward / state_dict / epoch end)
+        self.flush_every = int(os.environ.get("CTR_FLUSH_EVERY", "32"))
+        self._flushed_at = 0
         # FM's dense tail fused into one launch (ctr_fm_step_tail); CTR_FM_TAIL=0: the four
         # separate launches (A/B)
         self.fm_tail = os.environ.get("CTR_FM_TAIL", "1") != "0"
@@ -217,18 +245,6 @@ class FusedCTRTrainer:
         # (ctr_adam_deferred_rows, one launch) instead of marking owners from the ids first
         # (CTR_CATCHUP_BY_PLAN=0: the id-driven pair, A/B)
         self.catchup_by_plan = os.environ.get("CTR_CATCHUP_BY_PLAN", "1") != "0"
-        # catch-up ahead (step(next_x=)): the next batch's rows that this batch does not touch
-        # are brought to this step on the plan stream while it runs (_catchup_ahead). Off by
-        # default: bitwise correct, but measured slower on MI355X — the replay beside the
-        # step's GEMMs costs the step more than the catch-up it removes (C3 0.68 -> 0.75 ms
-        # per step with the full grid, 0.80 with 64 blocks, 1.05 with 16; IPNN likewise)
-        env = os.environ.get("CTR_CATCHUP_AHEAD")
-        self.catchup_ahead = env == "1"
-        self._ca_stream = None
-        self._tag = None
-        self._tag_seq = 0
-        self._ca_step = None
-        self._ca_pending: dict = {}
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -261,7 +277,6 @@ class FusedCTRTrainer:
         # runs, tools/c2_knobs3.sh); while the host paced the step one stream measured faster
         self.n_plan_streams = int(os.environ.get("CTR_PLAN_STREAMS", "2"))
         self._extra_plan_streams: list = []
-        self._plan_stream_of: dict = {}
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -271,9 +286,10 @@ class FusedCTRTrainer:
         self._bufs: _Bufs | None = None
         self._bufsets: dict = {}
         self.seed = int(torch.initial_seed() if seed is None else seed) & (2**63 - 1)
-        # HIP-graph replay of the single-process step (see step())
+        # HIP-graph replay of the single-process step (see step()): per shape at most
+        # 2 x ring-size graphs (slot x plan-built-ahead), independent of the batch count
         self.use_graphs = True
-        self.max_graphs = 8
+        self.max_graphs = 24
         self._graphs: dict = {}
         self._graph_pool = torch.cuda.graph_pool_handle()
         self._graph_tab_version = self.step_table.version
@@ -286,7 +302,7 @@ class FusedCTRTrainer:
         # a captured graph must not be destroyed while it still runs: plan-stream replays
         # (lookahead) are not ordered before anything the caller synchronises with
         try:
-            if getattr(self, "_graphs", None) or getattr(self, "_plan_graphs", None):
+            if getattr(self, "_graphs", None) or getattr(self, "_rings", None):
                 torch.cuda.synchronize(self.device)
         except Exception:  # interpreter shutdown
             pass
@@ -335,11 +351,9 @@ class FusedCTRTrainer:
 
     # ----------------------------------------------------------------- optimiser -----
     def flush(self) -> None:
-        """Bring every embedding row up to the last completed step (deferred mode)."""
-        main = torch.cuda.current_stream()
-        for st in [self._ca_stream, self._plan_stream] + self._extra_plan_streams:
-            if st is not None:  # work that runs beside the steps
-                main.wait_stream(st)
+        """Bring every embedding row up to the last completed step (deferred mode). The
+        plan streams only read staged ids and write plans: nothing to wait for."""
+        self._flushed_at = self.step_count
         if self.deferred and self._dirty and self.step_count > 0:
             t = self._mark("flush")
             hip_ops.adam_deferred_flush(self.E_tab, self.m_E, self.v_E,
@@ -364,6 +378,14 @@ class FusedCTRTrainer:
         self.last.zero_()
         self.step_ctr.copy_(torch.tensor([0, 1], dtype=torch.int32))
         self.step_count = 0
+        self._flushed_at = 0
+
+    def _bound_staleness(self) -> None:
+        """Flush once `flush_every` steps have passed since the last flush: no row is then
+        more than that many steps behind when a batch reads it."""
+        if (self.deferred and self.flush_every > 0
+                and self.step_count - self._flushed_at >= self.flush_every):
+            self.flush()
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.Adam-compatible state_dict (parameter order = model.parameters())."""
@@ -435,174 +457,140 @@ class FusedCTRTrainer:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
         batch's mean BCE as a 1-element device tensor (no host sync).
 
+        Single process: x and y are copied into a fixed input slot of their shape
+        (InputSlot; one D2D copy of the ids and labels) and the slot's step graph — the
+        step's ~40 launches captured once, every per-step scalar (the Adam step, the
+        dropout stream) read from the device step counter — is replayed, so every fresh
+        batch replays the same graph; the first step through a slot runs eagerly and
+        captures. x may also be a host tensor (the copy is then the H2D transfer).
+
         next_x (optional): the ids of the batch(es) the next step(s) will train on — one
-        tensor, or a sequence in step order. Their sparse plans (a pure function of the
-        ids) are built on a plan stream concurrently with this step (single process,
-        deferred mode), and the step that trains on one of them uses that plan instead of
-        building its own on its critical path. Two batches ahead hides the plan entirely:
-        its completion is then long past when the step waits for it (a cross-queue wait
-        that is still pending costs ~15 us). next_x must keep its contents until its step;
-        a step with other ids builds its plan as usual.
+        tensor, or a sequence in step order. They are copied into slots of their own and
+        their sparse plans (a pure function of the ids) built on a plan stream
+        concurrently with this step (single process, deferred mode, plan lookahead on);
+        the step that trains on one of them uses that plan instead of building its own on
+        its critical path. Two batches ahead hides the plan entirely: its completion is
+        then long past when the step waits for it (a cross-queue wait that is still
+        pending costs ~15 us). next_x is read on the plan stream after everything enqueued
+        before this call: its contents must stay valid until this call's work has run; a
+        step with other ids builds its plan as usual.
 
         The returned tensor is the trainer's persistent loss buffer for this batch shape
         (a captured HIP graph writes it in place): it is valid until the next step() with
-        the same shape. Keep a value with ``loss.item()`` or ``loss.clone()``.
-
-        Single process: the step's ~40 launches are captured once per (x, y) buffer pair
-        into a HIP graph and replayed (every per-step scalar — the Adam step, the dropout
-        stream — is read from the device step counter), so the host no longer paces small
-        batches; the first call with new buffers runs eagerly and captures."""
+        the same shape. Keep a value with ``loss.item()`` or ``loss.clone()``."""
         B, F = x.shape
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
         self._sync_weight_planes()
+        self._bound_staleness()
+        if ws != 1:  # replicated data parallel: eager (the exchange sizes live on the host)
+            self.step_table.ensure(self.step_count + 1)
+            loss = self._launch(x, y, mean_div)
+            self._after_step()
+            return loss
         # the host side of a step paces small batches (C2: ~70 us of Python per step against
         # ~75 us on the GPU), so each ids tensor's key is computed once and the current
         # stream is looked up once (torch.cuda.current_stream() costs ~4 us)
+        shape = (B, F, x.dtype)
         xkey = self._xkey(x)
-        if next_x is None or self._plan_stream is None or ws != 1:
-            nxts = []
-        else:
-            nxts = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
-        nk = [(n, self._xkey(n)) for n in nxts]
-        nk = [(n, k) for n, k in nk if n.is_cuda and k[1] == xkey[1] and k != xkey]
-        ahead = nk if self.plan_lookahead else []
-        ca_next = nk[0] if (self.catchup_ahead and nk) else None
+        nk = []
+        if next_x is not None and self.plan_lookahead and self._plan_stream is not None:
+            for n in ([next_x] if isinstance(next_x, torch.Tensor) else next_x):
+                k = self._xkey(n)
+                if k[1:3] == xkey[1:3] and k != xkey and all(k != kk for _, kk in nk):
+                    nk.append((n, k))
         main = torch.cuda.current_stream()
-        ev = self._pending.pop(xkey, None)
-        have = ev is not None
-        if have:  # x's plan was built ahead
-            main.wait_event(ev)
-        # x's rows were caught up during the previous step (have_ca). A catch-up made for a
-        # batch that did not come next is harmless (its rows just replayed earlier) but may
-        # share rows with x: every pending one completes before this step starts
-        have_ca = xkey in self._ca_pending
-        if self._ca_pending:
-            for ev_ca in self._ca_pending.values():
-                main.wait_event(ev_ca)
-            self._ca_pending.clear()
-        if self._pending:
-            keep = {k for _, k in ahead}
-            for k in [k for k in self._pending if k not in keep]:
-                del self._pending[k]  # built for a batch that did not come next: unused
-        todo = [(n, k) for n, k in ahead if k not in self._pending]
+        slot = self._staged.pop(xkey, None)
+        if self._staged:  # staged for batches that did not come next: free their slots
+            keep = {k for _, k in nk}
+            for k in [k for k in self._staged if k not in keep]:
+                main.wait_event(self._staged.pop(k).ev)  # its plan-stream writes come first
+        todo = [(n, k) for n, k in nk if k not in self._staged]
         ev_start = None
-        if todo or ca_next is not None:
+        if todo:  # everything enqueued before this step (the last users of the slots)
             ev_start = torch.cuda.Event()
-            ev_start.record(main)  # everything before this step (earlier readers of the plans)
-        if (self.use_graphs and ws == 1 and self.timing is None and x.is_cuda
-                and y.dtype == torch.float32 and y.is_contiguous()):
-            loss = self._graph_step(x, y, mean_div, have, have_ca, xkey)
+            ev_start.record(main)
+        have = slot is not None
+        if have:  # copied and planned ahead on the plan stream
+            main.wait_event(slot.ev)
+            slot.ev = None
+        else:
+            slot = self._acquire_slot(shape)
+            slot.ids.copy_(x, non_blocking=True)
+        slot.y.copy_(y.reshape(-1), non_blocking=True)
+        if self.use_graphs and self.timing is None:
+            loss = self._graph_step(slot, mean_div, have)
         else:
             self.step_table.ensure(self.step_count + 1)
-            loss = self._launch(x, y, mean_div, have, have_ca)
+            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
             self._after_step()
-        if ca_next is not None:
-            self._catchup_ahead(x, ca_next[0], ev_start)
-        seen = set()
         for n, k in todo:
-            if k not in seen:
-                seen.add(k)
-                self._build_ahead(n, ev_start, k, main)
+            self._stage_ahead(n, k, shape, slot, ev_start, main)
         return loss
 
-    def _catchup_ahead(self, x: torch.Tensor, nx: torch.Tensor, ev_start) -> None:
-        """The rows of nx that x does not hold, brought to the step just enqueued (it gives
-        them g = wd*p) on their own stream while that step runs: disjoint from every row the
-        step touches (ctr_adam_deferred_catchup_ahead), so the step that trains on nx needs no
-        catch-up. Eager launches: the target step and the tag are host values."""
-        if self._tag is None:
-            # zeros: a slot-index-like value that no tag value (always < 0) matches
-            self._tag = torch.zeros(self.V_tab, dtype=torch.int32, device=self.device)
-            self._ca_step = torch.zeros(1, dtype=torch.int32, device=self.device)
-        # the plan stream: a fourth stream would share one of the process's four hardware
-        # queues with the step (measured: C3 12.0 -> 10.9 M ex/s on a stream of its own)
-        cs = self._ca_stream = self._plan_stream
-        self._tag_seq += 1
-        if self._tag_seq >= 2**31 - 1:  # tag values are -seq: start over on a clean array
-            self._tag_seq = 1
-            with torch.cuda.stream(cs):
-                self._tag.zero_()
-        cs.wait_event(ev_start)
-        x.record_stream(cs)
-        nx.record_stream(cs)
-        m = self.model
-        w = m.linear.weight.data if self.kind != "IPNN" else None
-        with torch.cuda.stream(cs):
-            t = self._mark("adam")
-            self._ca_step.fill_(self.step_count)  # the step just enqueued
-            hip_ops.adam_deferred_catchup_ahead(
-                m.feature_embedding.weight.data, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                self.last, x, nx, self._tag, -self._tag_seq, self._ca_step, self.step_table,
-                self.step_count, self.betas, self.eps, self.weight_decay)
-            self._span("adam", t)
-            ev = torch.cuda.Event()
-            ev.record(cs)
-        self._ca_pending[self._xkey(nx)] = ev
+    def _ring(self, shape) -> list:
+        r = self._rings.get(shape)
+        if r is None:
+            r = self._rings[shape] = []
+        return r
 
-    def _build_ahead(self, nx: torch.Tensor, ev_start, key=None, main=None) -> None:
-        """The lookahead plan of ids nx on the plan stream, concurrent with the step just
-        enqueued (replayed from its own graph once captured). key: _xkey(nx); main: the
-        current stream (both looked up here when not given)."""
-        if key is None:
-            key = self._xkey(nx)
-        if main is None:
-            main = torch.cuda.current_stream()
-        si = self._plan_stream_of.get(key)
-        if si is None:
-            si = self._plan_stream_of[key] = len(self._plan_stream_of) % max(1, self.n_plan_streams)
-        while si > len(self._extra_plan_streams):
+    def _acquire_slot(self, shape, exclude=None) -> InputSlot:
+        """The lowest-index slot of the shape's ring that no staged batch holds (and that is
+        not `exclude`, the current step's); the ring grows up to max_slots. Lowest index
+        first keeps the set of (slot, planned-ahead) graphs small: the first step of an
+        epoch always lands in slot 0."""
+        ring = self._ring(shape)
+        busy = {id(s) for s in self._staged.values()}
+        if exclude is not None:
+            busy.add(id(exclude))
+        for s in ring:
+            if id(s) not in busy:
+                return s
+        if len(ring) >= self.max_slots:
+            raise RuntimeError(f"FusedCTRTrainer: more than {self.max_slots} batches staged ahead")
+        s = InputSlot(shape, len(ring), self.device)
+        s.stream_i = s.index % max(1, self.n_plan_streams)
+        ring.append(s)
+        return s
+
+    def _stage_ahead(self, nx: torch.Tensor, key, shape, current: InputSlot, ev_start,
+                     main) -> None:
+        """Copy ids nx into a free slot and build its sparse plan there, on the slot's plan
+        stream, concurrently with the step just enqueued (replayed from the slot's own
+        plan graph once captured)."""
+        s = self._acquire_slot(shape, exclude=current)
+        while s.stream_i > len(self._extra_plan_streams):
             self._extra_plan_streams.append(torch.cuda.Stream(device=self.device))
-        ps = self._plan_stream if si == 0 else self._extra_plan_streams[si - 1]
-        P = self._plan_for(nx, key)
+        ps = self._plan_stream if s.stream_i == 0 else self._extra_plan_streams[s.stream_i - 1]
         ps.wait_event(ev_start)
-        nx.record_stream(ps)
-        # torch.cuda.set_stream on the two known streams instead of the torch.cuda.stream
+        # torch.cuda.set_stream on the known streams instead of the torch.cuda.stream
         # context manager (~9 us per use: it looks the current stream up again)
         torch.cuda.set_stream(ps)
         try:
+            s.ids.copy_(nx, non_blocking=True)
+            if nx.is_cuda:
+                nx.record_stream(ps)
             t = self._mark("plan")
-            g = self._plan_graphs.get(key)
-            if g is not None and self.timing is None:
-                g.replay()
+            if s.plan_graph is not None and self.timing is None:
+                s.plan_graph.replay()
             else:
-                P.build(nx, self.V)
-                if (self.use_graphs and self.timing is None
-                        and len(self._plan_graphs) < self.max_plans):
+                s.plan.build(s.ids, self.V)
+                if self.use_graphs and self.timing is None:
                     g = torch.cuda.CUDAGraph()
                     with graph_capture(g, pool=self._graph_pool, stream=ps):
-                        P.build(nx, self.V)  # captured, not executed
-                    self._plan_graphs[key] = g
-                    self._pinned_plans.add(key)
+                        s.plan.build(s.ids, self.V)  # captured, not executed
+                    s.plan_graph = g
             self._span("plan", t)
             ev = torch.cuda.Event()
             ev.record(ps)
         finally:
             torch.cuda.set_stream(main)
-        self._pending[key] = ev
+        s.ev = ev
+        self._staged[key] = s
 
     @staticmethod
     def _xkey(x):
-        return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()))
-
-    def _plan_for(self, x, key=None) -> hip_ops.SparsePlanBuffers:
-        """The plan buffers of ids tensor x (lookahead); LRU, graph-held ones pinned."""
-        if key is None:
-            key = self._xkey(x)
-        p = self._plans.pop(key, None)
-        if p is None:
-            S = x.shape[0] * x.shape[1]
-            if len(self._plans) >= self.max_plans:
-                for k in list(self._plans):  # oldest first; reuse its buffers if big enough
-                    if k not in self._pinned_plans and k not in self._pending:
-                        old = self._plans.pop(k)
-                        if old.capacity >= S:
-                            p = old
-                        break
-            if p is None:
-                p = hip_ops.SparsePlanBuffers(S, self.device)
-        self._plans[key] = p  # most recently used last
-        return p
+        return (x.data_ptr(), tuple(x.shape), x.dtype, tuple(x.stride()), x.device)
 
     def _weights_version(self):
         mlp = self.model.mlp
@@ -629,56 +617,45 @@ class FusedCTRTrainer:
         if self.deferred:
             self._dirty = True
 
-    def _graph_key(self, x, y, mean_div, have=False, have_ca=False, xkey=None):
-        mlp = getattr(self.model, "mlp", None)
-        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
-        if xkey is None:
-            xkey = self._xkey(x)
-        return (xkey, y.data_ptr(), tuple(y.shape), mean_div, self.model.training, drops,
-                have, have_ca)
-
-    def _graph_step(self, x, y, mean_div, have=False, have_ca=False, xkey=None):
+    def _graph_step(self, slot: InputSlot, mean_div: float, have: bool):
         if self.step_table.capacity < self.step_count + 2:
             self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
         if self._graph_tab_version != self.step_table.version:
             torch.cuda.synchronize(self.device)  # none may still run when destroyed
             self._graphs.clear()  # they hold the old table's address
             self._graph_tab_version = self.step_table.version
-        if xkey is None:
-            xkey = self._xkey(x)
-        key = self._graph_key(x, y, mean_div, have, have_ca, xkey)
+        mlp = getattr(self.model, "mlp", None)
+        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
+        key = (slot.shape, slot.index, mean_div, self.model.training, drops, have)
         hit = self._graphs.get(key)
         if hit is None:
-            loss = self._launch(x, y, mean_div, have, have_ca)  # the real step; sizes buffers
+            # the real step (sizes every buffer), then the same launches captured
+            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, pool=self._graph_pool):
-                    self._launch(x, y, mean_div, have, have_ca)  # captured, not executed
-                if have:  # the graph reads x's lookahead plan buffers
-                    self._pinned_plans.add(xkey)
-                self._graphs[key] = (g, self._bufs, self._bufs.plan)
+                    self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
+                self._graphs[key] = (g, self._bufs)
+                self.captures += 1
             return loss
-        g, self._bufs, plan = hit  # the buffer set the graph was captured with
-        self._bufs.plan = plan
-        if have:
-            self._plan_for(x, xkey)  # LRU touch
+        g, self._bufs = hit  # the buffer set the graph was captured with
+        self._bufs.plan = slot.plan
         g.replay()
         self._after_step()
         return self._bufs.loss
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float,
-                have_plan: bool = False, have_ca: bool = False) -> torch.Tensor:
+                have_plan: bool = False, plan: hip_ops.SparsePlanBuffers | None = None
+                ) -> torch.Tensor:
         """Enqueue one step. Changes no host state: step-dependent values come from
         self.step_ctr (advanced on the device), so the launch sequence can be captured.
-        have_plan: x's plan was built ahead (step(next_x=) of the previous step)."""
+        plan: the batch's plan buffers (its input slot's; built here unless have_plan —
+        built ahead on the plan stream by the previous steps' lookahead)."""
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
-        if have_plan:
-            b.plan = self._plan_for(x)
-        elif b.plan_own is not None:
-            b.plan = b.plan_own
+        b.plan = plan if plan is not None else b.plan_own
         y = y.reshape(-1)
         if y.dtype != torch.float32:
             y = y.float()
@@ -715,22 +692,21 @@ class FusedCTRTrainer:
 
             if self.plan_first:
                 plan()
-            if not have_ca:  # else: caught up during the previous step (_catchup_ahead)
-                t = self._mark("adam")
-                if have_plan and self.catchup_by_plan:
-                    # the plan built ahead lists the batch's unique rows: one launch over
-                    # them instead of the owner-marking pass + the id-driven catch-up
-                    hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
-                                               self.last, b.plan, step_hint, self.step_table,
-                                               self.betas, self.eps, self.weight_decay,
-                                               step_dev=self.step_done)
-                else:
-                    hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w,
-                                                      self.v_w, self.last, x, self.rowmap,
-                                                      self.step_done, self.step_table,
-                                                      step_hint, self.betas, self.eps,
-                                                      self.weight_decay)
-                self._span("adam", t)
+            t = self._mark("catchup")
+            if have_plan and self.catchup_by_plan:
+                # the plan built ahead lists the batch's unique rows: one launch over
+                # them instead of the owner-marking pass + the id-driven catch-up
+                hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
+                                           self.last, b.plan, step_hint, self.step_table,
+                                           self.betas, self.eps, self.weight_decay,
+                                           step_dev=self.step_done)
+            else:
+                hip_ops.adam_deferred_catchup_ids(E, self.m_E, self.v_E, w, self.m_w,
+                                                  self.v_w, self.last, x, self.rowmap,
+                                                  self.step_done, self.step_table,
+                                                  step_hint, self.betas, self.eps,
+                                                  self.weight_decay)
+            self._span("catchup", t)
             if not self.plan_first:
                 plan()
             self._fork_sweep()
@@ -739,11 +715,11 @@ class FusedCTRTrainer:
             b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
             self._span("plan", t_plan)
             if self.deferred:
-                t = self._mark("adam")
+                t = self._mark("catchup")
                 hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w, self.last,
                                            b.plan, step_hint, self.step_table, self.betas,
                                            self.eps, self.weight_decay, step_dev=self.step_done)
-                self._span("adam", t)
+                self._span("catchup", t)
         if self.kind == "FM":
             t = self._mark("gather")
             hip_ops.fm_forward(x, E, w, bias, want_sum=True, labels=y, mean_div=mean_div,

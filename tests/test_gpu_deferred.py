@@ -94,9 +94,9 @@ def test_graph_replay_equals_eager_bitwise(cuda, kind, mode):
         m.train()
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7, optimizer_mode=mode)
         tr.use_graphs = graphs
-        losses = [tr.step(*data[i % 3]).item() for i in range(8)]  # 3 eager+capture, 5 replays
-        if graphs:
-            assert len(tr._graphs) == 3
+        losses = [tr.step(*data[i % 3]).item() for i in range(8)]  # 1 eager+capture, 7 replays
+        if graphs:  # every batch goes through the shape's one input slot: one graph
+            assert tr.captures == 1 and len(tr._graphs) == 1
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         out.append((losses, sd, tr.optimizer_state_dict()["state"]))
     (le, sde, ste), (lg, sdg, stg) = out
@@ -201,9 +201,8 @@ def test_c3_full_size_deferred_equals_dense_20_steps(cuda):
 @pytest.mark.parametrize("kind,V,K,B", [("FM", 50_000, 16, 1024), ("DeepFM", 200_000, 32, 1024),
                                         ("IPNN", 100_000, 16, 512)])
 def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
-    """step(x, y, next_x=...) builds the next batches' plans during this step (one or two
-    ahead, the second one a guess the order sometimes breaks) and catches the next batch's
-    rows up while it runs (catch-up ahead): bitwise the same
+    """step(x, y, next_x=...) stages the next batches and builds their plans during this
+    step (one or two ahead, the second one a guess the order sometimes breaks): bitwise the same
     losses, tables and moments as building every plan in its own step — over graph captures
     and replays, a lookahead the next step does not use (order changed), next_x == x, a step
     without next_x in between, and eager (no-graph) steps."""
@@ -218,10 +217,9 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     order = [(0, 1), (1, 2), (2, 0), (0, 1), (1, 2), (2, 0), (0, 2), (1, 1), (1, None),
              (2, 0), (0, 1), (1, 2), (2, 0), (0, 1)]
     out = []
-    # (batches ahead, HIP graphs, plan lookahead, catch-up ahead)
-    for ahead, graphs, pla, ca in ((0, True, False, False), (1, True, True, True),
-                                   (2, True, True, True), (2, False, True, True),
-                                   (2, True, False, True), (1, True, True, False)):
+    # (batches ahead, HIP graphs, plan lookahead)
+    for ahead, graphs, pla in ((0, True, False), (1, True, True), (2, True, True),
+                               (2, False, True), (2, True, False), (1, False, True)):
         torch.manual_seed(8)
         with torch.device(cuda):
             m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
@@ -231,7 +229,6 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7)
         tr.use_graphs = graphs
         tr.plan_lookahead = pla  # default: FM only; exercised for every kind here
-        tr.catchup_ahead = ca
         losses = []
         for j, (i, n) in enumerate(order):
             nxt = xs[n] if (ahead and n is not None) else None
@@ -241,8 +238,8 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         st = tr.optimizer_state_dict()["state"]
         out.append((losses, sd, st))
-        if ahead and graphs:
-            assert len(tr._graphs) <= tr.max_graphs
+        if graphs:  # (slot, planned ahead) pairs of a ring of ahead + 1 slots
+            assert tr.captures <= 2 * (ahead + 1)
     for losses, sd, st in out[1:]:
         assert losses == out[0][0]
         for k in sd:

@@ -113,7 +113,8 @@ def test_fused_ffm_steps_vs_oracle(cuda, V, F, K, B):
         sd = m.state_dict()
         for k in bd:
             bd[k].check(sd[k].cpu().numpy(), err_msg=f"step {s} {k}")
-    assert len(tr._graphs) == 2  # both batches captured, steps 2-3 replayed
+    # both batches copied into one input buffer: one graph, captured at step 0, replayed
+    assert tr.captures == 1 and len(tr._graphs) == 1
     tr.check_errors()
 
 
@@ -138,6 +139,41 @@ def test_fused_ffm_deferred_equals_every_step_flush(cuda):
         out.append({k: v.clone() for k, v in m.state_dict().items()})
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_ffm_optimizer_state_dict_loads_into_torch_adam(cuda):
+    """optimizer_state_dict() indexes parameters in model.parameters() order (FFM: bias
+    first), so torch.optim.Adam loads it and keeps stepping: after one more step with the
+    same gradients, torch's parameters equal the fused trainer's (deferred == dense)."""
+    P = _pkg()
+    V, F, K, B = 3000, 5, 8, 128
+    torch.manual_seed(3)
+    with torch.device(cuda):
+        m = P.FFM(V, F, K)
+    tr = P.FusedFFMTrainer(m, lr=1e-3, weight_decay=1e-5)
+    tr.keep_grads = True
+    gen = torch.Generator().manual_seed(4)
+    data = [(torch.randint(0, V, (B, F), generator=gen).to(cuda),
+             (torch.rand(B, generator=gen) < 0.3).float().to(cuda)) for _ in range(3)]
+    for x, y in data[:2]:
+        tr.step(x, y)
+    st = tr.optimizer_state_dict()
+    params = list(m.parameters())
+    for i, p in enumerate(params):
+        assert st["state"][i]["exp_avg"].shape == p.shape, i
+    clone = P.FFM(V, F, K).to(cuda)
+    clone.load_state_dict(m.state_dict())
+    opt = torch.optim.Adam(clone.parameters(), lr=1e-3, weight_decay=1e-5)
+    opt.load_state_dict(st)
+    tr.step(*data[2])
+    grads = _ffm_grads(tr)
+    for n, p in clone.named_parameters():
+        p.grad = torch.tensor(grads[n], device=cuda).reshape(p.shape)
+    opt.step()
+    sd = m.state_dict()
+    for n, p in clone.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), sd[n].cpu().numpy(),
+                                   rtol=1e-6, atol=1e-9, err_msg=n)
 
 
 def test_fused_ffm_index_error(cuda):

@@ -17,7 +17,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-N_TILES = 20
+N_TILES = 29
 AONLY = {0, 6, 8, 9}  # 64x160 tilings: the B operand must be KC (160 is not an RC tile width)
 
 
@@ -124,6 +124,20 @@ def test_gemm_planes_every_tiling(cuda, tile, monkeypatch):
                     C = _run(H, A, Bm, a_rc, b_rc, cuda).cpu().double()
                     bad = (C - ref).abs() > 2e-6 * bound + 1e-30
                     assert not bad.any(), (tile, splits, M, N, K, a_rc, b_rc, int(bad.sum()))
+
+
+@pytest.mark.parametrize("cfg,M,N,K", [("19,1,2", 512, 256, 300), ("19,1,4", 1024, 512, 96),
+                                       ("19,1,2", 8192, 1664, 300), ("7,1,8", 512, 512, 64)])
+def test_gemm_planes_xcd_groups(cuda, cfg, M, N, K, monkeypatch):
+    """The XCD tile partition (M-groups x N-groups, CTR_GEMM_PLANES_CFG's third field): every
+    output tile computed exactly once — integer data, bitwise."""
+    H = _H()
+    monkeypatch.setenv("CTR_GEMM_PLANES_CFG", cfg)
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randint(-3, 4, (M, K), generator=g).float()
+    Bm = torch.randint(-3, 4, (K, N), generator=g).float()
+    C = _run(H, A, Bm, False, True, cuda).cpu().double()
+    assert torch.equal(C, A.double() @ Bm.double())
 
 
 def test_gemm_planes_epilogues_and_output_planes(cuda):

@@ -639,3 +639,37 @@ def test_ffm_grads_vs_oracle(cuda, V, F, K, B):
     loss.backward()
     for k, v in m.named_parameters():
         assert_grad_close(v.grad.cpu().numpy(), gref[k].numpy(), err_msg=k)
+
+
+def test_pg_graph_learn_sees_load_state_dict(cuda):
+    """A replayed learn after policy_net.load_state_dict uses the loaded weights (the bf16
+    weight planes are re-split before the replay), and a state dtype switch drops the
+    graphs captured against the old input buffer: bitwise the same as learns without
+    graphs."""
+    P = _pkg()
+    V, F, K, A, T = 5000, 8, 4, 3, 512
+    gen = torch.Generator().manual_seed(3)
+    eps = [(torch.randint(0, V, (T, F), generator=gen), torch.randint(1, A + 1, (T, 1), generator=gen),
+            torch.randn(T, 1, generator=gen)) for _ in range(4)]
+    torch.manual_seed(5)
+    other = P.PolicyGradient(V, F, K, "g", action_nums=A, device="cuda:0", fix_input_dims=True)
+    other_sd = {k: v.clone() for k, v in other.policy_net.state_dict().items()}
+    out = []
+    for graphs in (False, True):
+        torch.manual_seed(6)
+        pg = P.PolicyGradient(V, F, K, "g", action_nums=A, device="cuda:0", fix_input_dims=True)
+        pg.use_graphs = graphs
+        for mod in pg.policy_net.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = 0.0
+        losses = []
+        for i, (x, a, r) in enumerate(eps):
+            if i == 2:
+                pg.policy_net.load_state_dict(other_sd)
+            xs = x.to(cuda) if i != 3 else x.to(cuda).to(torch.int32)
+            pg.store_transition(xs, a.to(cuda), r.to(cuda))
+            losses.append(pg.learn().item())
+        out.append((losses, {k: v.detach().clone() for k, v in pg.policy_net.state_dict().items()}))
+    assert out[0][0] == out[1][0]
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k], out[1][1][k]), k

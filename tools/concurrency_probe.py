@@ -41,9 +41,10 @@ def main():
     for i in range(8):
         tr.step(xs[i % 2], ys[i % 2], next_x=xs[(i + 1) % 2])
     torch.cuda.synchronize()
-    k0 = tr._xkey(xs[0])
-    g_step = next(g for key, (g, _, _) in tr._graphs.items() if key[-1] == k0)
-    g_plan = tr._plan_graphs[tr._xkey(xs[1])]
+    # a have-plan step graph (key[-1]: planned ahead) and a slot's lookahead plan graph
+    g_step = next(g for key, (g, _) in tr._graphs.items() if key[-1])
+    g_plan = next(s.plan_graph for ring in tr._rings.values() for s in ring
+                  if s.plan_graph is not None)
     main_s = torch.cuda.current_stream()
     ps = tr._plan_stream
     out = {}

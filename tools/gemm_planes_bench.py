@@ -67,12 +67,17 @@ def main():
     ap.add_argument("--tiles", type=int, default=25, help="sweep tilings 0 .. tiles-1")
     ap.add_argument("--only", default="", help="comma-separated tiling indices to sweep")
     ap.add_argument("--pg", action="store_true", help="the C4 policy MLP shapes instead")
+    ap.add_argument("--splits", default="1,2,4,8", help="split-K values of the sweep")
+    ap.add_argument("--xg", default="1", help="XCD N-group values of the sweep (third cfg field)")
+    ap.add_argument("--shapes", default="", help="comma-separated shape-name prefixes to run")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     total = 0.0
     table = pg_shapes() if args.pg else shapes(args.B, args.W)
     for name, (M, N, K, a_rc, b_rc) in table.items():
+        if args.shapes and not any(name.startswith(p) for p in args.shapes.split(",")):
+            continue
         A = torch.randn(*((K, M) if a_rc else (M, K)), device=dev, generator=g)
         Bm = torch.randn(*((K, N) if b_rc else (N, K)), device=dev, generator=g)
         pa, pb = H.split_planes(A), H.split_planes(Bm)
@@ -80,7 +85,8 @@ def main():
         cfgs = ["auto"]
         if args.sweep:
             tiles = [int(t) for t in args.only.split(",")] if args.only else range(args.tiles)
-            cfgs += [f"{t},{s}" for t in tiles for s in (1, 2, 4, 8)
+            cfgs += [f"{t},{s},{x}" for t in tiles for s in map(int, args.splits.split(","))
+                     for x in map(int, args.xg.split(","))
                      if not (b_rc and t in (0, 6, 8, 9))]
         best = None
         for cfg in cfgs:
