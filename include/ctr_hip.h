@@ -39,7 +39,10 @@ enum ctr_status {
 
 enum ctr_idx_type { CTR_IDX_I32 = 0, CTR_IDX_I64 = 1 };
 
-enum ctr_err_flag { CTR_EFLAG_INDEX = 1 };
+enum ctr_err_flag {
+  CTR_EFLAG_INDEX = 1,    /* a feature id outside [0, V) */
+  CTR_EFLAG_CAPACITY = 2  /* a row-sharded exchange run longer than its capacity */
+};
 
 /* GEMM epilogues (ctr_gemm_f32). */
 enum ctr_epilogue {
@@ -263,6 +266,25 @@ int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows, int n
                           int64_t* counts, ctr_stream_t stream);
 /* ids[i] += delta (global row ids <-> shard-local row ids). */
 int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t stream);
+/* Fixed-capacity exchange of a row-sharded step (no reference counterpart: the reference
+ * runs on one device, all_main/pretrain_main.py:232; this is the exchange SURVEY.md §8e
+ * adds around nn.Embedding's gather / embedding_dense_backward, p_model.py:47,303,311,320).
+ * Every (requester, owner j) pair moves `capacity` rows, so the all-to-alls are equal-split
+ * and their sizes depend on the capacity alone (a step is capturable in a HIP graph).
+ * ctr_shard_pack_ids: send[j*capacity + i] (int32) = the i-th unique row of the plan owned by
+ *   shard j as an owner-local id, or past that run the owner's spare row (its row count,
+ *   min(shard_rows, V - j*shard_rows)); counts[j] / offsets[j] (int32[n_shards]) = the run's
+ *   length and start in the plan's unique rows; a run longer than capacity ORs
+ *   CTR_EFLAG_CAPACITY into *err_flag.
+ * ctr_shard_runs_copy: rows of `width` floats between the compact order (run j at offsets[j])
+ *   and the padded layout (run j at j*capacity): pack = 1 writes every padded row (zeros past
+ *   a run), pack = 0 writes the runs back to their compact places. */
+int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V, int n_shards,
+                       int64_t capacity, int32_t* send, int32_t* counts, int32_t* offsets,
+                       int32_t* err_flag, ctr_stream_t stream);
+int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, int64_t capacity,
+                        int n_shards, const int32_t* counts, const int32_t* offsets, int pack,
+                        ctr_stream_t stream);
 int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
                           void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
 

@@ -649,6 +649,188 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
   }
 }
 
+// The background sweep, tiled like deferred_flush_tile: slice ctr[0] % n_slices of the rows
+// (slices of whole 64-row tiles) brought to the completed step ctr[0] (read on the device:
+// the sweep is a node of the captured step graph, forked after the catch-up so it never
+// touches the step's rows — those are current to ctr[0] and skipped). Every step sweeps one
+// slice, so no row is ever more than n_slices steps behind and no separate flush pass is
+// needed; the replay (VALU) runs beside the step's GEMMs (matrix pipe) on a bounded grid.
+template <int K4, int UNR>
+__global__ __launch_bounds__(256) void deferred_sweep_tile(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    int32_t* __restrict__ last, const int32_t* __restrict__ ctr, int n_slices, int lds_steps,
+    const float* __restrict__ tab, AdamHP h) {
+  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
+  const int step = ctr[0];
+  const bool use_lds = step < lds_steps;
+  if (use_lds) {
+    for (int i = threadIdx.x; i <= step; i += blockDim.x)
+      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
+    __syncthreads();
+  }
+  if (step <= 0) return;
+  constexpr int RPI = kWave / K4;
+  constexpr int ITERS = K4;
+  static_assert(ITERS % UNR == 0, "batches of UNR instructions");
+  const int64_t n_tiles_all = (V + kWave - 1) / kWave;
+  const int64_t per = (n_tiles_all + n_slices - 1) / n_slices;  // tiles per slice
+  const int64_t t_lo = (int64_t)(step % n_slices) * per;
+  const int64_t t_hi = min(n_tiles_all, t_lo + per);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = lane % K4, r_in = lane / K4;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  auto set_step = [&](int t) {
+    if (use_lds) {
+      const float2 v = s_tab[t];
+      h.neg_step_size = v.x;
+      h.inv_bc2_sqrt = v.y;
+    } else {
+      load_step(h, tab, t);
+    }
+  };
+  for (int64_t tile = t_lo + (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+       tile < t_hi; tile += waves) {
+    const int64_t base = tile * kWave;
+    const int64_t my = base + lane;
+    const bool ok = my < V;
+    const int from_l = ok ? last[my] : step;
+    if (__all(from_l >= step)) continue;
+    if (w && from_l < step) {
+      float pp = w[my], mm = mw[my], vv = vw[my];
+      for (int s = from_l + 1; s <= step; ++s) {
+        set_step(s);
+        adam_elem(pp, 0.f, mm, vv, h);
+      }
+      w[my] = pp; mw[my] = mm; vw[my] = vv;
+    }
+#pragma unroll 1
+    for (int it0 = 0; it0 < ITERS; it0 += UNR) {
+      float4 pp[UNR], mm[UNR], vv[UNR];
+      int from[UNR];
+      int64_t e[UNR];
+      int f0 = step;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = (it0 + u) * RPI + r_in;
+        from[u] = __shfl(from_l, r, kWave);
+        e[u] = (base + r) * K4 + c;
+        f0 = min(f0, from[u]);
+        if (from[u] < step) {
+          pp[u] = E[e[u]]; mm[u] = mE[e[u]]; vv[u] = vE[e[u]];
+        }
+      }
+      for (int s = f0 + 1; s <= step; ++s) {
+        set_step(s);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (s > from[u]) adam_replay_vec(pp[u], mm[u], vv[u], h);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (from[u] < step) {
+          E[e[u]] = pp[u]; mE[e[u]] = mm[u]; vE[e[u]] = vv[u];
+        }
+    }
+    if (from_l < step) last[my] = step;
+  }
+}
+
+// The tiled flush, software-pipelined: the loads of batch b+1 are issued before batch b's
+// replay, into a second register buffer (UNR rows per buffer; UNR = 2 keeps the register
+// footprint of the single-buffered UNR = 4 kernel), so each wave keeps HBM busy while its
+// VALU replays. Without it the waves of a CU run in phase — all load, all replay — and the
+// flush costs the SUM of its HBM pass and its replay arithmetic (C3 table: 2.1 ms + 0.115 ms
+// per replayed step), not their maximum. Same rows, same steps, same adam_elem: bitwise
+// deferred_flush_tile.
+template <int K4, int UNR, bool LDS_TAB>
+__global__ __launch_bounds__(256) void deferred_flush_pipe(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
+  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
+  if (LDS_TAB) {
+    for (int i = threadIdx.x; i <= step; i += blockDim.x)
+      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
+    __syncthreads();
+  }
+  constexpr int RPI = kWave / K4;
+  constexpr int NB = K4 / UNR;  // batches per 64-row tile
+  static_assert(K4 % UNR == 0 && NB % 2 == 0, "an even number of UNR-row batches per tile");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = lane % K4, r_in = lane / K4;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int64_t n_tiles = (V + kWave - 1) / kWave;
+  auto set_step = [&](int t) {
+    if (LDS_TAB) {
+      const float2 v = s_tab[t];
+      h.neg_step_size = v.x;
+      h.inv_bc2_sqrt = v.y;
+    } else {
+      load_step(h, tab, t);
+    }
+  };
+  struct Buf {
+    float4 p[UNR], m[UNR], v[UNR];
+    int from[UNR];
+    int f0;
+  };
+  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+       tile < n_tiles; tile += waves) {
+    const int64_t base = tile * kWave;
+    const int64_t my = base + lane;
+    const bool ok = my < V;
+    const int from_l = ok ? last[my] : step;
+    if (__all(from_l >= step)) continue;
+    auto load = [&](Buf& b, int bi) {
+      b.f0 = step;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = (bi * UNR + u) * RPI + r_in;
+        b.from[u] = __shfl(from_l, r, kWave);
+        b.f0 = min(b.f0, b.from[u]);
+        if (b.from[u] < step) {
+          const int64_t e = (base + r) * K4 + c;
+          b.p[u] = E[e]; b.m[u] = mE[e]; b.v[u] = vE[e];
+        }
+      }
+    };
+    auto run = [&](Buf& b, int bi) {
+      for (int s = b.f0 + 1; s <= step; ++s) {
+        set_step(s);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+          if (s > b.from[u]) adam_replay_vec(b.p[u], b.m[u], b.v[u], h);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (b.from[u] < step) {
+          const int64_t e = (base + (bi * UNR + u) * RPI + r_in) * K4 + c;
+          E[e] = b.p[u]; mE[e] = b.m[u]; vE[e] = b.v[u];
+        }
+    };
+    Buf b0, b1;
+    load(b0, 0);
+    // the tile's linear weights replay while batch 0's loads are in flight
+    if (w && from_l < step) {
+      float pp = w[my], mm = mw[my], vv = vw[my];
+      for (int s = from_l + 1; s <= step; ++s) {
+        set_step(s);
+        adam_elem(pp, 0.f, mm, vv, h);
+      }
+      w[my] = pp; mw[my] = mm; vw[my] = vv;
+    }
+#pragma unroll 1
+    for (int bi = 0; bi < NB; bi += 2) {
+      load(b1, bi + 1);
+      run(b0, bi);
+      if (bi + 2 < NB) load(b0, bi + 2);
+      run(b1, bi + 1);
+    }
+    if (from_l < step) last[my] = step;
+  }
+}
+
 // Any K: a thread per row (rows list, or all rows when rows == NULL).
 template <bool APPLY>
 __global__ __launch_bounds__(256) void deferred_scalar(
@@ -915,16 +1097,51 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
                        reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
                        step_table, h)
-    switch (K4) {
-      case 1: CTR_DEF_FLUSH(1, 1); break;
-      case 2: CTR_DEF_FLUSH(2, 2); break;
-      case 4: CTR_DEF_FLUSH(4, 4); break;
-      case 8: CTR_DEF_FLUSH(8, CTR_FLUSH_UNR); break;
-      case 16: CTR_DEF_FLUSH(16, CTR_FLUSH_UNR); break;
-      case 32: CTR_DEF_FLUSH(32, CTR_FLUSH_UNR); break;
-      case 64: CTR_DEF_FLUSH(64, CTR_FLUSH_UNR); break;
+#define CTR_DEF_PIPE(K4_, UNR_)                                                                  \
+  if (lds)                                                                                      \
+    hipLaunchKernelGGL((deferred_flush_pipe<K4_, UNR_, true>), grid, 256, lds_bytes, st,        \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
+                       step_table, h);                                                          \
+  else                                                                                          \
+    hipLaunchKernelGGL((deferred_flush_pipe<K4_, UNR_, false>), grid, 256, 0, st,               \
+                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
+                       step_table, h)
+    // CTR_FLUSH_PIPE: 0 the single-buffered tile kernel, 1 / 2 the pipelined one with 1 / 2
+    // rows per buffer (A/B)
+    const char* pe = getenv("CTR_FLUSH_PIPE");
+    const int pipe = pe ? atoi(pe) : 0;
+    if (pipe == 1 && K4 >= 2) {
+      switch (K4) {
+        case 2: CTR_DEF_PIPE(2, 1); break;
+        case 4: CTR_DEF_PIPE(4, 1); break;
+        case 8: CTR_DEF_PIPE(8, 1); break;
+        case 16: CTR_DEF_PIPE(16, 1); break;
+        case 32: CTR_DEF_PIPE(32, 1); break;
+        case 64: CTR_DEF_PIPE(64, 1); break;
+      }
+    } else if (pipe == 2 && K4 >= 4) {
+      switch (K4) {
+        case 4: CTR_DEF_PIPE(4, 2); break;
+        case 8: CTR_DEF_PIPE(8, 2); break;
+        case 16: CTR_DEF_PIPE(16, 2); break;
+        case 32: CTR_DEF_PIPE(32, 2); break;
+        case 64: CTR_DEF_PIPE(64, 2); break;
+      }
+    } else {
+      switch (K4) {
+        case 1: CTR_DEF_FLUSH(1, 1); break;
+        case 2: CTR_DEF_FLUSH(2, 2); break;
+        case 4: CTR_DEF_FLUSH(4, 4); break;
+        case 8: CTR_DEF_FLUSH(8, CTR_FLUSH_UNR); break;
+        case 16: CTR_DEF_FLUSH(16, CTR_FLUSH_UNR); break;
+        case 32: CTR_DEF_FLUSH(32, CTR_FLUSH_UNR); break;
+        case 64: CTR_DEF_FLUSH(64, CTR_FLUSH_UNR); break;
+      }
     }
 #undef CTR_DEF_FLUSH
+#undef CTR_DEF_PIPE
     CTR_LAUNCH_CHECK("deferred_flush_tile");
     return CTR_OK;
   }
@@ -1107,6 +1324,31 @@ extern "C" int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, f
   const size_t lds_bytes = (size_t)lds_steps * sizeof(float2);
   const int K4 = K / 4;
   const int64_t rows = ceil_div(V, n_slices);
+  // the tiled sweep on a bounded grid (CTR_SWEEP_BLOCKS, default 256: one 4-wave block per
+  // CU beside the step's kernels); CTR_SWEEP_TILE=0: the row-per-lane-group kernel (A/B)
+  const char* te = getenv("CTR_SWEEP_TILE");
+  if (!(te && te[0] == '0') && K4 >= 4) {
+    const char* be = getenv("CTR_SWEEP_BLOCKS");
+    const long bl = be ? atol(be) : 256;
+    const int64_t tiles = ceil_div(ceil_div(V, (int64_t)kWave), n_slices);
+    const unsigned g2 = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>(ceil_div(tiles, 4), bl >= 1 && bl <= 65536 ? bl : 256));
+#define CTR_SWEEPT(K4_, UNR_)                                                                   \
+  hipLaunchKernelGGL((deferred_sweep_tile<K4_, UNR_>), g2, 256, lds_bytes, st,                  \
+                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
+                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, step_ctr,    \
+                     n_slices, lds_steps, step_table, h)
+    switch (K4) {
+      case 4: CTR_SWEEPT(4, 4); break;
+      case 8: CTR_SWEEPT(8, 4); break;
+      case 16: CTR_SWEEPT(16, 4); break;
+      case 32: CTR_SWEEPT(32, 4); break;
+      case 64: CTR_SWEEPT(64, 4); break;
+    }
+#undef CTR_SWEEPT
+    CTR_LAUNCH_CHECK("deferred_sweep_tile");
+    return CTR_OK;
+  }
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows * K4, 256), 4096));
 #define CTR_SWEEP(K4_)                                                                          \
   hipLaunchKernelGGL((deferred_sweep_vec<K4_>), grid, 256, lds_bytes, st,                       \

@@ -39,6 +39,14 @@ typedef float pf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
 
+// CTR_PL_SPREAD = 1: the LDS-DMA pieces of stage t+NS-1 are issued between the MFMA groups
+// of stage t (one group per accumulator column) instead of all together right after the
+// stage's barrier, where their issue cost (~100-185 cycles per 1 KiB piece beside MFMAs,
+// MI355X_MICROARCH.md) held every wave's MFMAs back at the same moment
+#ifndef CTR_PL_SPREAD
+#define CTR_PL_SPREAD 0
+#endif
+
 struct PlaneSrc {
   const uint16_t* p;  // plane 0 (bf16 bits); planes `ps` elements apart
   int64_t ld;         // elements per storage row
@@ -139,10 +147,35 @@ __device__ __forceinline__ pbf16x8 frag_kc_at(const char* p) {
   return *reinterpret_cast<const pbf16x8*>(p);
 }
 
+// The transpose reads as inline asm (CTR_PL_TR_ASM, default): with the builtin, hipcc 7.2
+// cannot tell the read from the LDS-DMA writes in flight and waits vmcnt(0) before it — the
+// next stage's DMA then lands before the current stage computes (no load/compute overlap in
+// any GEMM with a k-strided operand). The asm form is invisible to the wait pass, so its
+// results are waited for explicitly (planes_wait_lds) before the MFMAs that use them.
+#ifndef CTR_PL_TR_ASM
+#define CTR_PL_TR_ASM 1
+#endif
 __device__ __forceinline__ pbf16x8 frag_rc_at(const char* p0, const char* p1) {
+#if CTR_PL_TR_ASM
+  pbf16x4 v0, v1;
+  const uint32_t a0 = (uint32_t)(uintptr_t)(const CTR_LDS char*)p0;
+  const uint32_t a1 = (uint32_t)(uintptr_t)(const CTR_LDS char*)p1;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v0) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v1) : "v"(a1));
+#else
   const pbf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CTR_LDS pbf16x4*)p0);
   const pbf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CTR_LDS pbf16x4*)p1);
+#endif
   return __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// every LDS read issued so far has landed (the asm transpose reads are not tracked by the
+// compiler), and no MFMA is hoisted above this point (cdna_hip_programming.md rule 18)
+__device__ __forceinline__ void planes_wait_lds() {
+#if CTR_PL_TR_ASM
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 // ---- epilogue --------------------------------------------------------------------
@@ -348,6 +381,21 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
         __builtin_amdgcn_global_load_lds((const void*)(bb_ + offB[j_]), (CTR_LDS void*)(st_ + ldsB[j_]), 16, 0, 0); \
   } while (0)
 
+  constexpr int IPW_ALL = IPWA + IPWB;
+  constexpr int PER = (IPW_ALL + TN - 1) / TN;  // pieces issued after each column group
+  auto issue_piece = [&](int t_, int j) {
+    char* st_ = smem + (t_ % NS) * STAGE;
+    if (j < IPWA) {
+      const char* ba_ = (const char*)SA.p + (int64_t)t_ * stepA;
+      __builtin_amdgcn_global_load_lds((const void*)(ba_ + offA[j]), (CTR_LDS void*)(st_ + ldsA[j]), 16, 0, 0);
+    } else {
+      const char* bb_ = (const char*)SB.p + (int64_t)t_ * stepB;
+      __builtin_amdgcn_global_load_lds((const void*)(bb_ + offB[j - IPWA]),
+                                       (CTR_LDS void*)(st_ + ldsB[j - IPWA]), 16, 0, 0);
+    }
+  };
+  (void)issue_piece;
+
   int aoff[TM][2], boff[TN][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -360,7 +408,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     boff[i][1] = B_RC ? frag_rc_img_off<RB>(wn0 + 16 * i, lane, 1) : 0;
   }
 
-  auto compute_sub = [&](const char* st) {
+  auto compute_sub = [&](const char* st, int t_issue) {
     pbf16x8 af[TM][3];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -377,6 +425,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
         const char* img = st + 3 * A_PL + p * B_PL;
         bf[p] = B_RC ? frag_rc_at(img + boff[tn][0], img + boff[tn][1]) : frag_kc_at(img + boff[tn][0]);
       }
+      if (A_RC || B_RC) planes_wait_lds();
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         // a0b0 into the main accumulator; the five products <= 2^-7 of it (smallest first)
@@ -390,11 +439,17 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
         lo[i][tn] = v;
         acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[0], acc[i][tn], 0, 0, 0);
       }
+      if (CTR_PL_SPREAD && t_issue >= 0) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+          if (tn * PER + q < IPW_ALL) issue_piece(t_issue, tn * PER + q);
+      }
     }
   };
-  auto compute = [&](int slot) {
+  auto compute = [&](int slot, int t_issue) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) compute_sub(smem + slot * STAGE + ks * SUB);
+    for (int ks = 0; ks < KS; ++ks)
+      compute_sub(smem + slot * STAGE + ks * SUB, ks == 0 ? t_issue : -1);
   };
 
   // prologue: stages 0 .. NS-2 in flight
@@ -415,8 +470,12 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     // ... and every wave's (and every wave is done reading the slot refilled next)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
-    compute(t % NS);
+    if (CTR_PL_SPREAD) {
+      compute(t % NS, t + NS - 1 < nt ? t + NS - 1 : -1);
+    } else {
+      if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
+      compute(t % NS, -1);
+    }
   }
 #undef CTR_PL_ISSUE
   __syncthreads();  // every stage read before the epilogue reuses the LDS
@@ -613,23 +672,31 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     return c;
   }
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
-  if (a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320) {
-    // whole-M tile (the wide operand read once), split-K to about one block per CU
+  static const bool wide_wg = [] {
+    const char* e = getenv("CTR_GEMM_PLANES_WIDE");
+    return e && e[0] == '1';
+  }();
+  if (wide_wg && a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320) {
+    // whole-M tile (the wide operand read once), split-K to about one block per CU.
+    // Measured standalone (operands MALL-warm, tools/gemm_planes_bench.py): slower than the
+    // 64x64 tiles below (dW0 71 vs 66 us, dW1 28-30 vs 22.5): opt-in (CTR_GEMM_PLANES_WIDE)
     const int ti = M <= 192 ? 27 : M <= 256 ? 26 : 25;
     const int64_t tiles = ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(256 / tiles, Kp / 256), 64));
     return mk(ti, s);
   }
   if (a_rc && b_rc && Kp >= 2048) {
-    // target block count of the weight-gradient GEMMs (A/B: CTR_GEMM_PLANES_WG_BLOCKS)
+    // target block count of the weight-gradient GEMMs (A/B: CTR_GEMM_PLANES_WG_BLOCKS):
+    // ~1170 (4.5 per CU) with the split-major XCD map — measured dW0 (130 tiles) 9 splits
+    // 66 us vs 4 splits 73, dW1 (20 tiles) 24-32 splits 22.5-23 us vs 16 24
     static const int64_t wg_blocks = [] {
       const char* e = getenv("CTR_GEMM_PLANES_WG_BLOCKS");
       const long v = e ? atol(e) : 0;
-      return (int64_t)(v >= 64 && v <= 8192 ? v : 512);
+      return (int64_t)(v >= 64 && v <= 8192 ? v : 1170);
     }();
     const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(
-                      ceil_div(wg_blocks, tiles), Kp / 256), 32));
+                      ceil_div(wg_blocks, tiles), Kp / 256), 64));
     return mk(7, s);
   }
   // otherwise a makespan model: blocks dealt to 256 CUs x occ slots in rounds; a round costs one block's

@@ -376,6 +376,68 @@ __global__ void shard_counts_kernel(const int32_t* __restrict__ unique_rows,
   counts[j] = lower((int64_t)(j + 1) * shard_rows) - lower((int64_t)j * shard_rows);
 }
 
+// Fixed-capacity exchange of a row-sharded step: every (requester, owner) pair moves C rows
+// (equal-split all-to-alls whose sizes depend on C alone, so a step is graph-capturable).
+// The plan's unique rows owned by shard j are the run [lo_j, hi_j) of unique_rows (ascending);
+// slot i of destination j carries run entry lo_j + i as an owner-local id, or, past the run,
+// the owner's dummy row id (its row count: owners keep one spare row that padding entries
+// read and update, never a real one). counts[j] / offsets[j] (int32) describe the runs; a
+// run longer than C raises CTR_EFLAG_CAPACITY.
+__device__ __forceinline__ int plan_lower_bound(const int32_t* __restrict__ rows, int U, int64_t v) {
+  int lo = 0, hi = U;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)rows[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void shard_pack_ids_kernel(
+    const int32_t* __restrict__ unique_rows, const int32_t* __restrict__ num_unique,
+    int64_t shard_rows, int64_t V, int64_t C, int32_t* __restrict__ send,
+    int32_t* __restrict__ counts, int32_t* __restrict__ offsets, int32_t* err) {
+  const int j = blockIdx.y;
+  const int U = *num_unique;
+  const int64_t base = (int64_t)j * shard_rows;
+  const int lo = plan_lower_bound(unique_rows, U, base);
+  const int hi = plan_lower_bound(unique_rows, U, base + shard_rows);
+  const int32_t dummy = (int32_t)max<int64_t>(0, min<int64_t>(shard_rows, V - base));
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < C;
+       i += (int64_t)gridDim.x * blockDim.x)
+    send[(int64_t)j * C + i] = lo + i < hi ? (int32_t)(unique_rows[lo + i] - base) : dummy;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    counts[j] = hi - lo;
+    offsets[j] = lo;
+    if (hi - lo > C && err) atomicOr(err, (int32_t)CTR_EFLAG_CAPACITY);
+  }
+}
+
+// Row runs between the compact order (run j at offsets[j], counts[j] rows) and the padded
+// exchange layout (run j at j*C, C rows): PACK writes every padded slot (zeros past a run),
+// UNPACK writes the runs only. W floats per row (float4 when W % 4 == 0).
+template <typename VT, bool PACK>
+__global__ __launch_bounds__(256) void shard_runs_copy_kernel(
+    const VT* __restrict__ src, VT* __restrict__ dst, int64_t W, int64_t C,
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets) {
+  const int j = blockIdx.y;
+  const int64_t cnt = counts[j], off = offsets[j];
+  const int64_t n = (PACK ? C : cnt) * W;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / W, k = t - i * W;
+    const int64_t padded = ((int64_t)j * C + i) * W + k, compact = (off + i) * W + k;
+    if (PACK) {
+      VT v;
+      if (i < cnt) v = src[compact];
+      else memset(&v, 0, sizeof(v));
+      dst[padded] = v;
+    } else {
+      dst[compact] = src[padded];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host side --------
 static int key_bits(int64_t V) {
   int bits = 1;
@@ -590,5 +652,41 @@ extern "C" int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t 
   const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n, 256), 4096);
   hipLaunchKernelGGL(ids_add_kernel, grid, 256, 0, as_stream(stream), ids, n, delta);
   CTR_LAUNCH_CHECK("ids_add_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V,
+                                  int n_shards, int64_t capacity, int32_t* send, int32_t* counts,
+                                  int32_t* offsets, int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan) && send && counts && offsets && shard_rows > 0 && n_shards > 0 &&
+                  capacity > 0 && V > 0 && shard_rows * n_shards >= V,
+              "ctr_shard_pack_ids: bad arguments");
+  CTR_REQUIRE(shard_rows < (int64_t(1) << 31), "ctr_shard_pack_ids: shard too large");
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(capacity, 256), 1024), (unsigned)n_shards);
+  hipLaunchKernelGGL(shard_pack_ids_kernel, grid, 256, 0, as_stream(stream), plan->unique_rows,
+                     plan->num_unique, shard_rows, V, capacity, send, counts, offsets, err_flag);
+  CTR_LAUNCH_CHECK("shard_pack_ids_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, int64_t capacity,
+                                   int n_shards, const int32_t* counts, const int32_t* offsets,
+                                   int pack, ctr_stream_t stream) {
+  CTR_REQUIRE(src && dst && counts && offsets && width > 0 && capacity > 0 && n_shards > 0,
+              "ctr_shard_runs_copy: bad arguments");
+  hipStream_t st = as_stream(stream);
+  const bool vec = width % 4 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0;
+  const int64_t W = vec ? width / 4 : width;
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(capacity * W, 256), 2048), (unsigned)n_shards);
+  if (vec) {
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    if (pack) hipLaunchKernelGGL((shard_runs_copy_kernel<float4, true>), grid, 256, 0, st, s4, d4, W, capacity, counts, offsets);
+    else hipLaunchKernelGGL((shard_runs_copy_kernel<float4, false>), grid, 256, 0, st, s4, d4, W, capacity, counts, offsets);
+  } else {
+    if (pack) hipLaunchKernelGGL((shard_runs_copy_kernel<float, true>), grid, 256, 0, st, src, dst, W, capacity, counts, offsets);
+    else hipLaunchKernelGGL((shard_runs_copy_kernel<float, false>), grid, 256, 0, st, src, dst, W, capacity, counts, offsets);
+  }
+  CTR_LAUNCH_CHECK("shard_runs_copy_kernel");
   return CTR_OK;
 }

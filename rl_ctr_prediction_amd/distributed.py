@@ -112,6 +112,23 @@ def alltoallv(send: torch.Tensor, send_counts: list[int], recv_counts: list[int]
     return out
 
 
+def alltoall_equal(out: torch.Tensor, send: torch.Tensor, group=None) -> torch.Tensor:
+    """Equal-split all-to-all along dim 0 (N equal blocks of the same rows each way): sizes
+    fixed by the shapes, no host-side counts — the row-sharded exchange at a fixed capacity.
+    One process: a copy. gloo (CPU test runs) stages device tensors through host memory."""
+    rank, ws = world()
+    if ws == 1:
+        out.copy_(send)
+        return out
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        o = out.cpu()
+        dist.all_to_all_single(o, send.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, send, group=group)
+    return out
+
+
 def exchange_counts(counts: torch.Tensor, group=None) -> tuple[list[int], list[int]]:
     """counts[j] = rows this rank sends to rank j (int64 device tensor) -> (send_counts,
     recv_counts) host lists. One small all-to-all and one host sync per call: the

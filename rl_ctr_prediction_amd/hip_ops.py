@@ -11,7 +11,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ._lib import (CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
+from ._lib import (CTR_EFLAG_CAPACITY, CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
                    EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, PlaneViewDesc, SparsePlan,
                    lib)
 
@@ -21,7 +21,7 @@ __all__ = [
     "fm_embedding_grad_adam", "segment_sum_rows_adam",
     "rows_to_dense", "adam_dense", "fm_step_tail", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
-    "step_begin", "step_end", "adam_deferred_sweep", "ids_add_",
+    "step_begin", "step_end", "adam_deferred_sweep", "ids_add_", "shard_pack_ids", "shard_runs_copy",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "pg_vt_mean", "pg_loss_grad_global", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -90,17 +90,24 @@ class Workspace:
 def check_index_error(err_flag: torch.Tensor) -> None:
     """Raise like nn.Embedding does when a kernel saw an id outside [0, V). Syncs."""
     v = int(err_flag.item())
+    if v & CTR_EFLAG_CAPACITY:  # a library invariant broke (the host sizes the capacity)
+        err_flag.zero_()
+        raise RuntimeError("row-sharded exchange: a run exceeded its capacity")
     if v & CTR_EFLAG_INDEX:
         err_flag.zero_()
         raise IndexError("index out of range in self")
 
 
 # ------------------------------------------------------------------------ forward ----
-def embedding_gather(table: torch.Tensor, idx: torch.Tensor, err_flag=None) -> torch.Tensor:
+def embedding_gather(table: torch.Tensor, idx: torch.Tensor, err_flag=None,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
     _f32(table, "table")
     idx, it = _idx(idx)
     V, K = table.shape
-    out = torch.empty(*idx.shape, K, dtype=torch.float32, device=table.device)
+    if out is None:
+        out = torch.empty(*idx.shape, K, dtype=torch.float32, device=table.device)
+    elif out.numel() < idx.numel() * K or not out.is_contiguous():
+        raise ValueError("embedding_gather: out must be contiguous with idx.numel() * K floats")
     lib.ctr_embedding_gather(_p(table), V, K, _p(idx), it, idx.numel(), _p(out), _p(err_flag),
                              _stream())
     return out
@@ -466,6 +473,38 @@ class SparsePlanBuffers:
             out = torch.empty(n_shards, dtype=torch.int64, device=self.device)
         lib.ctr_plan_shard_counts(self.struct(), int(shard_rows), int(n_shards), _p(out), _stream())
         return out
+
+
+def shard_pack_ids(plan: SparsePlanBuffers, shard_rows: int, V: int, n_shards: int,
+                   capacity: int, send: torch.Tensor, counts: torch.Tensor,
+                   offsets: torch.Tensor, err_flag: torch.Tensor | None = None) -> None:
+    """The plan's unique rows, per owner shard, into the padded exchange layout
+    send[j*capacity + i] (owner-local ids; the owner's spare row past each run); counts /
+    offsets: int32[n_shards] (ctr_shard_pack_ids)."""
+    for t, n, k in ((send, "send", n_shards * capacity), (counts, "counts", n_shards),
+                    (offsets, "offsets", n_shards)):
+        _dev(t, n)
+        if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() < k:
+            raise ValueError(f"shard_pack_ids: {n} must be contiguous int32 of >= {k}")
+    lib.ctr_shard_pack_ids(plan.struct(), int(shard_rows), int(V), int(n_shards), int(capacity),
+                           _p(send), _p(counts), _p(offsets), _p(err_flag), _stream())
+
+
+def shard_runs_copy(src: torch.Tensor, dst: torch.Tensor, capacity: int, counts: torch.Tensor,
+                    offsets: torch.Tensor, pack: bool) -> torch.Tensor:
+    """Rows between the compact order and the padded exchange layout (ctr_shard_runs_copy):
+    pack: dst[j*capacity + i] = src[offsets[j] + i] (zeros past counts[j]); else the reverse
+    for the runs only."""
+    _f32(src, "src")
+    _f32(dst, "dst")
+    n = counts.numel()
+    width = src.shape[1] if src.dim() == 2 else 1
+    padded, compact = (dst, src) if pack else (src, dst)
+    if padded.shape[0] < n * capacity or (dst.dim() == 2 and dst.shape[1] != width):
+        raise ValueError("shard_runs_copy: padded side must hold n_shards * capacity rows")
+    lib.ctr_shard_runs_copy(_p(src), _p(dst), int(width), int(capacity), int(n), _p(counts),
+                            _p(offsets), int(bool(pack)), _stream())
+    return dst
 
 
 def ids_add_(ids: torch.Tensor, delta: int) -> torch.Tensor:

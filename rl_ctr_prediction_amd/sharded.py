@@ -1,60 +1,116 @@
 """Row-sharded data parallelism for the CTR step (BASELINE configs C3 at 8
 GPUs and C5, the 40M-row table "sharded across 8xMI355X with RCCL all-to-all").
 
-Rank r of N owns the embedding rows [r*Vs, (r+1)*Vs), Vs = ceil(V/N): their Adam moments,
-their deferred-replay state and their updates. Every rank trains its own batch (weak
-scaling); per step:
+Rank r of N owns the embedding rows [r*Vs, (r+1)*Vs), Vs = ceil(V/N): their values, Adam
+moments, deferred-replay state and updates — and nothing else of the tables (the rank's
+copy of the model holds its shard only). Every rank trains its own batch (weak scaling);
+per step:
 
-  1. sparse plan of the local batch (global ids); its unique rows are ascending, hence
-     grouped by owner -> per-owner counts (ctr_plan_shard_counts), one tiny all-to-all of
-     counts (the only host sync: variable-split collectives need sizes on the host);
-  2. all-to-all of the unique row ids to their owners (each rank asks for each row once);
-  3. owners bring the requested rows up to date (plan-free deferred catch-up: duplicates
+  1. sparse plan of the local batch (global ids), built on the plan stream (ahead of the
+     step with next_x); its unique rows are ascending, hence grouped by owner;
+  2. the exchange capacity C: the largest per-owner run over every rank's batch (one
+     all-reduce MAX of a scalar on the plan stream, read by the host: the step's only host
+     read, and with next_x a read of work finished long before), rounded up to a multiple
+     of 1024 rows so a handful of capacities cover all batches;
+  3. equal-split all-to-alls of C rows per (requester, owner) pair — row ids out
+     (ctr_shard_pack_ids: each owner's run, padded with the owner's spare row), rows back,
+     gradients out (ctr_shard_runs_copy packs / unpacks the runs): their sizes depend on C
+     alone, so the step has no variable-split collective and, for a given C, is one fixed
+     launch sequence (captured as a HIP graph at N = 1; at N > 1 with RCCL when
+     CTR_SHARDED_GRAPHS=1);
+  4. owners bring the requested rows up to date (plan-free deferred catch-up: duplicates
      across requesters resolved by the owner scratch), gather E[row] and w[row] and send
-     them back (all-to-all): every rank now holds its batch's rows compacted in unique order;
-  4. forward + backward locally over that compact table (slot -> unique ordinal ids), the
+     them back: every rank then holds its batch's rows compacted in unique order;
+  5. forward + backward locally over that compact table (slot -> unique ordinal ids), the
      per-row gradient sums in plan order (the same kernels as the single-GPU step);
-  5. all-to-all of the per-row gradients to the owners, which sum them per row in (source
-     rank, position) order (a sparse plan over the received ids + the deterministic
-     segmented sum) and apply Adam to their rows; the dense MLP gradient goes through one
-     all-reduce as in the replicated path.
+  6. the per-row gradients go to the owners, which sum them per row in (source rank,
+     position) order — a sparse plan over the received ids + the deterministic segmented
+     sum; padding entries form the spare row's segment, summed and applied to the spare
+     row, which nothing reads — and apply Adam to their rows; the dense MLP gradient goes
+     through one all-reduce.
 
 Per rank and step at C3 with 8 GPUs: ~61k unique rows out and back (ids 0.25 MB, rows and
-gradients 16 MB each way) instead of all-gathering every rank's 16 MB of row gradients;
-the deferred flush and the catch-up/apply work cover V/N rows. With N = 1 every exchange
-is a local copy and the step is bitwise the single-GPU FusedCTRTrainer step
-(tests/test_gpu_sharded.py).
+gradients 16 MB each way, plus the padding up to C) instead of all-gathering every rank's
+16 MB of row gradients; the deferred flush and the catch-up / apply work cover V/N rows.
+With N = 1 every exchange is a local copy and the step is bitwise the single-GPU
+FusedCTRTrainer step (tests/test_gpu_sharded.py). exchange="varsplit" keeps the
+variable-split protocol (per-owner counts all-to-all, sizes on the host) for comparison:
+both give bitwise the same results.
 """
 from __future__ import annotations
+
+import os
+import weakref
 
 import torch
 import torch.distributed as dist
 
 from . import hip_ops
-from .distributed import allreduce_sum_, alltoallv, exchange_counts, world
-from .trainer import FusedCTRTrainer
+from .distributed import allreduce_sum_, alltoall_equal, alltoallv, exchange_counts, world
+from .trainer import FusedCTRTrainer, InputSlot, graph_capture
+
+CAP_QUANTUM = 1024  # exchange capacities are multiples of this many rows
+
+
+class _XBufs:
+    """The fixed-capacity exchange buffers of one (batch shape, capacity)."""
+
+    def __init__(self, n: int, C: int, S: int, K: int, lin: bool, dev):
+        i32 = dict(dtype=torch.int32, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        NC = n * C
+        self.send_ids, self.recv_ids = torch.empty(NC, **i32), torch.empty(NC, **i32)
+        self.counts, self.offsets = torch.empty(n, **i32), torch.empty(n, **i32)
+        self.rows_out, self.rows_in = torch.empty(NC, K, **f32), torch.empty(NC, K, **f32)
+        self.table = torch.empty(max(S, 1), K, **f32)  # the batch's rows, compact
+        self.g_out, self.g_in = torch.empty(NC, K, **f32), torch.empty(NC, K, **f32)
+        self.g_rows = torch.empty(NC, K, **f32)
+        if lin:
+            self.lin_out, self.lin_in = torch.empty(NC, **f32), torch.empty(NC, **f32)
+            self.lin_table = torch.empty(max(S, 1), **f32)
+            self.glin_out, self.glin_in = torch.empty(NC, **f32), torch.empty(NC, **f32)
+            self.g_lin = torch.empty(NC, **f32)
+        else:
+            self.lin_out = self.lin_in = self.lin_table = None
+            self.glin_out = self.glin_in = self.g_lin = None
+        self.gplan = hip_ops.SparsePlanBuffers(NC, dev)
+        self.slot2u = torch.empty(max(S, 1), **i32)
 
 
 class ShardedCTRTrainer(FusedCTRTrainer):
     """FusedCTRTrainer over this rank's row shard of the embedding tables (deferred-exact
-    Adam). Rows outside the shard keep their initial values in this rank's copy of the
-    model; gather_tables() assembles the trained tables."""
+    Adam). The shard is all this rank keeps: at construction the model's
+    ``feature_embedding.weight`` (and ``linear.weight``) data are replaced by rows
+    [row_lo, row_hi) — copied to the device, the full table released — so a rank holds
+    ceil(V/N) rows of E, w and their Adam state (+ one spare row, the exchange's padding
+    target), never the whole table. The model may be built on the host (the reference's own
+    init: ``get_model(...)`` then ``.to(device)``, all_main/pretrain_main.py:137), so a
+    vocabulary larger than one GPU is never materialised on any device.
+    ``model.state_dict()`` (every rank together: it gathers) and gather_tables() assemble
+    the full tables; the sharded model's own forward needs them and refuses to run on a
+    shard (N > 1)."""
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None,
-                 count_group=None):
+                 count_group=None, device=None, exchange: str = "padded"):
         """process_group: the ranks sharing the table (default: the world). count_group: a
-        second communicator over the same ranks for the per-step counts exchange (it runs
-        on the plan stream beside the data collectives). Default: created here with
-        dist.new_group — a collective over the WHOLE world, so with the default
-        process_group every rank builds its trainer at the same point; trainers over a
-        sub-group must pass a count_group that every rank of the world created in the same
-        order (e.g. one of dist.new_subgroups())."""
+        second communicator over the same ranks for the per-step capacity / counts
+        agreement (it runs on the plan stream beside the data collectives). Default:
+        created here with dist.new_group — a collective over the WHOLE world, so with the
+        default process_group every rank builds its trainer at the same point; trainers
+        over a sub-group must pass a count_group that every rank of the world created in
+        the same order (e.g. one of dist.new_subgroups()). exchange: "padded" (fixed
+        capacity, the default) or "varsplit"."""
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:
             raise ValueError(f"row sharding: vocabulary {V} smaller than world size")
+        if exchange not in ("padded", "varsplit"):
+            raise ValueError(f"exchange must be 'padded' or 'varsplit', not {exchange!r}")
+        self.exchange = exchange
         self.shard_rows = -(-V // self.world_size)
+        self._V_full = V
+        self._shard_model(model, device)
         super().__init__(model, lr=lr, weight_decay=weight_decay, betas=betas, eps=eps,
                          process_group=process_group, seed=seed, optimizer_mode="deferred")
         if not self._vec_ok:
@@ -62,10 +118,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._side = None  # the exchange needs the plan before anything else
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
-        # the plan and its per-owner counts are built on the plan stream (ahead of the step
-        # with next_x), and the counts all-to-all — the step's one host sync — runs there on
-        # a communicator of its own: the host then waits for the plan only, never for the
-        # previous step's kernels or collectives, and runs ahead of the GPU
+        # the plans (and per-owner counts / run maxima) are built on the plan stream, ahead
+        # of the step with next_x; the per-step agreement runs there on a communicator of
+        # its own, so the host waits for that stream only, never for the previous step
         if self._plan_stream is None:
             self._plan_stream = torch.cuda.Stream(device=self.device)
         self._count_group = count_group
@@ -76,11 +131,313 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                  "(dist.new_group is collective over the whole world)")
             self._count_group = dist.new_group()
         self._ahead_counts: dict = {}
-        # lookahead plans per ids tensor (LRU): ids key -> plan buffers / pending event
+        self._xbufs: dict = {}
+        # graph replay of the fixed-capacity step: at one process always (no collective), at
+        # N > 1 only where the collectives can be captured (RCCL) and it is asked for
+        backend = dist.get_backend(self.group) if self.world_size > 1 else None
+        self._graph_ok = self.world_size == 1 or (
+            backend == "nccl" and os.environ.get("CTR_SHARDED_GRAPHS", "0") == "1")
+        # varsplit: lookahead plans per ids tensor (LRU): ids key -> plan buffers / event
         self._plans: dict = {}
         self._pending: dict = {}
         self.max_plans = 16
 
+    # ----------------------------------------------------------------- the shard ------
+    def _shard_model(self, model, device) -> None:
+        """Replace the model's table data by this rank's rows on the device (before the
+        base class reads the model) and move the rest of the model there. The rows live in
+        a buffer with one spare row past the shard (the exchange's padding entries read and
+        update it); the Parameter is the view of the real rows."""
+        E = model.feature_embedding.weight
+        if device is None:
+            device = E.device if E.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        lo = min(self.rank * self.shard_rows, self._V_full)
+        hi = min(lo + self.shard_rows, self._V_full)
+        tabs = [E] + ([model.linear.weight] if hasattr(model, "linear") else [])
+        self._spare = {}
+        for p in tabs:
+            buf = torch.zeros((hi - lo + 1,) + tuple(p.shape[1:]), dtype=p.dtype, device=device)
+            buf[:hi - lo].copy_(p.data[lo:hi])  # the full table's storage goes with .data
+            p.data = buf[:hi - lo]
+            self._spare[id(p)] = buf
+        model.to(device)
+        self._sharded_params = tabs
+        if self.world_size > 1:
+            ref = weakref.ref(self)
+
+            def no_forward(*_):
+                raise RuntimeError("ShardedCTRTrainer: this model holds one row shard of its "
+                                   "tables; assemble them with trainer.gather_tables() (or "
+                                   "model.state_dict() on every rank) for inference")
+
+            def full_tables(module, state_dict, prefix, local_metadata):
+                t = ref()
+                if t is None:
+                    return state_dict
+                E_full, w_full = t.gather_tables()
+                state_dict[prefix + "feature_embedding.weight"] = E_full
+                if w_full is not None:
+                    state_dict[prefix + "linear.weight"] = w_full.view(-1, 1)
+                return state_dict
+            model.register_forward_pre_hook(no_forward)
+            model._register_state_dict_hook(full_tables)
+
+    def _vocab_size(self, E) -> int:
+        return self._V_full
+
+    def _own_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """The shard's buffer, spare row included (the Parameter is its first V_tab rows)."""
+        for p in self._sharded_params:
+            if p.data.data_ptr() == t.data_ptr():
+                buf = self._spare[id(p)]
+                return buf.view(-1) if t.dim() == 2 and t.shape[1] == 1 else buf
+        return t
+
+    def _buffers(self, B: int, F: int):
+        b = super()._buffers(B, F)
+        if b.gplan is None:  # world size 1: the owner-side plan is still needed
+            S = B * F * self.world_size
+            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+            b.gplan = hip_ops.SparsePlanBuffers(S, self.device)
+            b.g_rows, b.g_lin = e(S, self.K), e(S)
+        return b
+
+    def _table_rows(self) -> tuple[int, int]:
+        lo = min(self.rank * self.shard_rows, self.V)
+        return lo, min(lo + self.shard_rows, self.V)
+
+    def optimizer_state_dict(self) -> dict:
+        st = super().optimizer_state_dict()
+        for s in st["state"].values():  # the shard's rows (the spare row is internal)
+            for k in ("exp_avg", "exp_avg_sq"):
+                if s[k].dim() >= 1 and s[k].shape[0] == self.V_tab + 1:
+                    s[k] = s[k][:self.V_tab]
+        return st
+
+    # ------------------------------------------------------------------ the step ------
+    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
+             next_x=None) -> torch.Tensor:
+        """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches are
+        staged and their plans and per-owner run maxima built on the plan stream during this
+        step. Purely local (the capacity agreement is made when a batch's step comes), so
+        ranks may pass different next_x."""
+        if self.exchange == "varsplit":
+            return self._step_varsplit(x, y, global_batch, next_x)
+        B, F = x.shape
+        ws = self.world_size
+        mean_div = float(global_batch if global_batch is not None else B * ws)
+        self._sync_weight_planes()
+        self._bound_staleness()
+        main, ps = torch.cuda.current_stream(), self._plan_stream
+        shape = (B, F, x.dtype)
+        xkey = self._xkey(x)
+        ahead = []
+        if next_x is not None:
+            for n in ([next_x] if isinstance(next_x, torch.Tensor) else next_x):
+                k = self._xkey(n)
+                if k[1:3] == xkey[1:3] and k != xkey and all(k != kk for _, kk in ahead):
+                    ahead.append((n, k))
+        slot = self._staged.pop(xkey, None)
+        if self._staged:
+            keep = {k for _, k in ahead}
+            for k in [k for k in self._staged if k not in keep]:
+                main.wait_event(self._staged.pop(k).ev)
+        todo = [(n, k) for n, k in ahead if k not in self._staged]
+        ev_start = torch.cuda.Event()
+        ev_start.record(main)  # everything enqueued before this step
+        if slot is None:  # copy and plan now, on the plan stream
+            slot = self._acquire_slot(shape)
+            ps.wait_event(ev_start)
+            torch.cuda.set_stream(ps)
+            try:
+                slot.ids.copy_(x, non_blocking=True)
+                if x.is_cuda:
+                    x.record_stream(ps)
+                self._plan_slot(slot)
+            finally:
+                torch.cuda.set_stream(main)
+        slot.y.copy_(y.reshape(-1), non_blocking=True)
+        # the capacity: every rank's largest run, agreed on the plan stream (host waits there)
+        t = self._mark("plan")
+        with torch.cuda.stream(ps):
+            if ws > 1:
+                dist.all_reduce(slot.cap, op=dist.ReduceOp.MAX, group=self._count_group)
+            cmax = int(slot.cap.item())
+            ev_plan = torch.cuda.Event()
+            ev_plan.record(ps)
+        self._span("plan", t)
+        C = max(CAP_QUANTUM, -(-cmax // CAP_QUANTUM) * CAP_QUANTUM)
+        main.wait_event(ev_plan)
+        if self.use_graphs and self._graph_ok and self.timing is None:
+            loss = self._sharded_graph_step(slot, mean_div, C)
+        else:
+            self.step_table.ensure(self.step_count + 1)
+            loss = self._launch_sharded(slot, mean_div, C)
+            self._after_step()
+        for n, k in todo:
+            s = self._acquire_slot(shape, exclude=slot)
+            ps.wait_event(ev_start)
+            torch.cuda.set_stream(ps)
+            try:
+                s.ids.copy_(n, non_blocking=True)
+                if n.is_cuda:
+                    n.record_stream(ps)
+                self._plan_slot(s)
+            finally:
+                torch.cuda.set_stream(main)
+            self._staged[k] = s
+        return loss
+
+    def _plan_slot(self, slot: InputSlot) -> None:
+        """On the current (plan) stream: the slot's plan, its largest per-owner run
+        (slot.cap, int64 scalar) and an event."""
+        if slot.cap is None:
+            slot.cap = torch.zeros(1, dtype=torch.int64, device=self.device)
+            slot.counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+        slot.plan.build(slot.ids, self.V, err_flag=self.err)
+        slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts)
+        torch.amax(slot.counts, dim=0, keepdim=True, out=slot.cap)
+        slot.ev = torch.cuda.Event()
+        slot.ev.record()
+
+    def _xb(self, B: int, F: int, C: int) -> _XBufs:
+        key = (B, F, C)
+        xb = self._xbufs.get(key)
+        if xb is None:
+            xb = self._xbufs[key] = _XBufs(self.world_size, C, B * F, self.K,
+                                           self.w_tab is not None, self.device)
+        return xb
+
+    def _sharded_graph_step(self, slot: InputSlot, mean_div: float, C: int):
+        if self.step_table.capacity < self.step_count + 2:
+            self.step_table.ensure(max(self.step_count + 2, 2 * self.step_table.capacity))
+        if self._graph_tab_version != self.step_table.version:
+            torch.cuda.synchronize(self.device)
+            self._graphs.clear()
+            self._graph_tab_version = self.step_table.version
+        mlp = getattr(self.model, "mlp", None)
+        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
+        key = (slot.shape, slot.index, C, mean_div, self.model.training, drops)
+        hit = self._graphs.get(key)
+        if hit is None:
+            loss = self._launch_sharded(slot, mean_div, C)
+            self._after_step()
+            if len(self._graphs) < self.max_graphs:
+                g = torch.cuda.CUDAGraph()
+                with graph_capture(g, pool=self._graph_pool):
+                    self._launch_sharded(slot, mean_div, C)  # captured, not executed
+                self._graphs[key] = (g, self._bufs)
+                self.captures += 1
+            return loss
+        g, self._bufs = hit
+        self._bufs.plan = slot.plan
+        g.replay()
+        self._after_step()
+        return self._bufs.loss
+
+    def _launch_sharded(self, slot: InputSlot, mean_div: float, C: int) -> torch.Tensor:
+        """Enqueue one fixed-capacity step (no host read, no size taken from the device:
+        capturable for a given C)."""
+        x, y = slot.ids, slot.y
+        B, F = x.shape
+        n = self.world_size
+        b = self._buffers(B, F)
+        b.plan = plan = slot.plan
+        xb = self._xb(B, F, C)
+        bias, gv = self.views.get("bias"), self.grad_views
+        has_lin = self.w_tab is not None
+        step_hint = self.step_count + 1
+        Vo = self.E_tab.shape[0]  # the owner's rows, spare row included
+        # 1. row ids out: each owner's run, padded with its spare row
+        t = self._mark("exchange")
+        hip_ops.shard_pack_ids(plan, self.shard_rows, self.V, n, C, xb.send_ids, xb.counts,
+                               xb.offsets, err_flag=self.err)
+        alltoall_equal(xb.recv_ids, xb.send_ids, self.group)
+        self._span("exchange", t)
+        # 2. owners: catch the rows up, gather them, send them back
+        t = self._mark("catchup")
+        hip_ops.adam_deferred_catchup_ids(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                          self.v_w, self.last, xb.recv_ids, self.rowmap,
+                                          self.step_done, self.step_table, step_hint,
+                                          self.betas, self.eps, self.weight_decay)
+        self._span("catchup", t)
+        self._fork_sweep()
+        t = self._mark("exchange")
+        hip_ops.embedding_gather(self.E_tab, xb.recv_ids, out=xb.rows_out)
+        alltoall_equal(xb.rows_in, xb.rows_out, self.group)
+        hip_ops.shard_runs_copy(xb.rows_in, xb.table, C, xb.counts, xb.offsets, pack=False)
+        T_lin = None
+        if has_lin:
+            hip_ops.embedding_gather(self.w_tab.view(Vo, 1), xb.recv_ids,
+                                     out=xb.lin_out.view(-1, 1))
+            alltoall_equal(xb.lin_in, xb.lin_out, self.group)
+            hip_ops.shard_runs_copy(xb.lin_in, xb.lin_table, C, xb.counts, xb.offsets, pack=False)
+            T_lin = xb.lin_table.view(-1, 1)
+        self._span("exchange", t)
+        # 3. forward + backward over the compact table
+        ids = plan.slot_to_unique(out=xb.slot2u)[:B * F].view(B, F)
+        T = xb.table
+        gz = self._sharded_fwd_bwd(ids, y, b, T, T_lin, bias, mean_div, F)
+        # 4. gradients to the owners, summed per row in (source rank, position) order
+        t = self._mark("exchange")
+        hip_ops.shard_runs_copy(b.grad_rows, xb.g_out, C, xb.counts, xb.offsets, pack=True)
+        alltoall_equal(xb.g_in, xb.g_out, self.group)
+        if has_lin:
+            hip_ops.shard_runs_copy(b.grad_lin, xb.glin_out, C, xb.counts, xb.offsets, pack=True)
+            alltoall_equal(xb.glin_in, xb.glin_out, self.group)
+        self._join_wgrad()
+        allreduce_sum_(self.flat_grad, self.group)
+        if n > 1:
+            allreduce_sum_(b.loss, self.group)
+            b.loss.div_(n)
+        self._span("exchange", t)
+        t = self._mark("scatter")
+        xb.gplan.build(xb.recv_ids, Vo)
+        hip_ops.segment_sum_rows(xb.gplan, xb.g_in, xb.glin_in if has_lin else None,
+                                 rowmap=None, out=xb.g_rows,
+                                 out_lin=xb.g_lin if has_lin else None)
+        self._span("scatter", t)
+        t = self._mark("adam")
+        hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                   self.v_w, self.last, xb.gplan, step_hint, self.step_table,
+                                   self.betas, self.eps, self.weight_decay,
+                                   grad_rows=xb.g_rows, grad_lin=xb.g_lin if has_lin else None,
+                                   step_dev=self.step_cur)
+        self._span("adam", t)
+        self._adam_dense(step_hint)
+        self._join_sweep()
+        hip_ops.step_end(self.step_ctr)
+        return b.loss
+
+    def _sharded_fwd_bwd(self, ids, y, b, T, T_lin, bias, mean_div, F):
+        """Forward + backward over the compact table T (ids: slot -> unique ordinal), the
+        per-row gradient sums into b.grad_rows / b.grad_lin (plan order); returns gz."""
+        gv = self.grad_views
+        B = ids.shape[0]
+        if self.kind == "FM":
+            t = self._mark("gather")
+            hip_ops.fm_forward(ids, T, T_lin, bias, want_sum=True, labels=y, mean_div=mean_div,
+                               want_p=False, out=b.fm)
+            self._span("gather", t)
+            gz = b.fm.gz
+            hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
+        else:
+            gz = self._deepfm_forward_backward(ids, y, b, T, T_lin, bias, mean_div)
+        t = self._mark("scatter")
+        if self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
+            hip_ops.segment_sum_rows(b.plan, b.dslot, out=b.grad_rows)
+        else:
+            hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,
+                                      grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
+        self._span("scatter", t)
+        if self.kind != "FM":  # the dense-parameter gradients, on the weight-gradient stream
+            self._weight_grads(b, gz)
+        else:
+            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
+        return gz
+
+    # -------------------------------------------------- variable-split (comparison) ------
     def _plan_for(self, x) -> hip_ops.SparsePlanBuffers:
         """The lookahead plan buffers of ids tensor x (least recently used reused first,
         never one still pending)."""
@@ -100,24 +457,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._plans[key] = p  # most recently used last
         return p
 
-    def _buffers(self, B: int, F: int):
-        b = super()._buffers(B, F)
-        if b.gplan is None:  # world size 1: the owner-side plan is still needed
-            S = B * F * self.world_size
-            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
-            b.gplan = hip_ops.SparsePlanBuffers(S, self.device)
-            b.g_rows, b.g_lin = e(S, self.K), e(S)
-        return b
-
-    def _table_rows(self) -> tuple[int, int]:
-        lo = min(self.rank * self.shard_rows, self.V)
-        return lo, min(lo + self.shard_rows, self.V)
-
-    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-             next_x=None) -> torch.Tensor:
-        """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches'
-        plans and per-owner counts are built on the plan stream during this step. Purely
-        local (no collective depends on it), so ranks may pass different next_x."""
+    def _step_varsplit(self, x, y, global_batch=None, next_x=None) -> torch.Tensor:
+        """The variable-split protocol: per-owner counts all-to-all (sizes to the host),
+        variable all-to-alls of ids, rows and gradients; eager."""
         B, F = x.shape
         ws = self.world_size
         mean_div = float(global_batch if global_batch is not None else B * ws)
@@ -128,9 +470,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if y.dtype != torch.float32:
             y = y.float()
         y = y.contiguous()
-        bias, gv = self.views.get("bias"), self.grad_views
-        has_lin = self.w_tab is not None  # InnerPNN: no linear table
-
+        bias = self.views.get("bias")
+        has_lin = self.w_tab is not None
         self._sync_weight_planes()
         self._bound_staleness()
         main, ps = torch.cuda.current_stream(), self._plan_stream
@@ -140,8 +481,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         ahead = [n for n in ahead if n.is_cuda and n.dim() == 2 and n.shape[1] == F
                  and self._xkey(n) != xkey]
         ev_start = torch.cuda.Event()
-        ev_start.record(main)  # everything before this step (earlier readers of the plans)
-        # 1. plan of the local batch, per-owner counts of its unique rows (plan stream)
+        ev_start.record(main)
         t = self._mark("plan")
         keep = {self._xkey(n) for n in ahead} | {xkey}
         for k in [k for k in self._pending if k not in keep]:
@@ -163,51 +503,27 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             ev_plan.record(ps)
         main.wait_event(ev_plan)
         self._span("plan", t)
-        # 2. unique row ids to their owners, as shard-local ids
         t = self._mark("exchange")
         req = alltoallv(plan.unique_rows, send_c, recv_c, self.group)
         hip_ops.ids_add_(req, -self.row_lo)
         self._span("exchange", t)
-        # 3. owners: catch the rows up, send them back
-        t = self._mark("adam")
+        t = self._mark("catchup")
         hip_ops.adam_deferred_catchup_ids(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
                                           self.v_w, self.last, req, self.rowmap, self.step_done,
                                           self.step_table, self.step_count + 1, self.betas,
                                           self.eps, self.weight_decay)
-        self._span("adam", t)
+        self._span("catchup", t)
         self._fork_sweep()
         t = self._mark("exchange")
         rows = hip_ops.embedding_gather(self.E_tab, req)
         T = alltoallv(rows, recv_c, send_c, self.group)
         T_lin = None
         if has_lin:
-            lin = hip_ops.embedding_gather(self.w_tab, req)
+            lin = hip_ops.embedding_gather(self.w_tab.view(-1, 1), req)
             T_lin = alltoallv(lin, recv_c, send_c, self.group).view(-1)
         self._span("exchange", t)
-        # 4. forward + backward over the compact table
         ids = plan.slot_to_unique(out=self._slot2u)[:B * F].view(B, F)
-        if self.kind == "FM":
-            t = self._mark("gather")
-            hip_ops.fm_forward(ids, T, T_lin, bias, want_sum=True, labels=y, mean_div=mean_div,
-                               want_p=False, out=b.fm)
-            self._span("gather", t)
-            gz = b.fm.gz
-        else:
-            gz = self._deepfm_forward_backward(ids, y, b, T, T_lin, bias, mean_div)
-        if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream
-            hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
-        t = self._mark("scatter")
-        if self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
-            hip_ops.segment_sum_rows(plan, b.dslot, out=b.grad_rows)
-        else:
-            hip_ops.fm_embedding_grad(plan, F, T, gz, b.fm.sum_e, b.dx, None,
-                                      grad_rows=b.grad_rows, grad_lin=b.grad_lin, compact=True)
-        self._span("scatter", t)
-        if self.kind != "FM":  # the dense-parameter gradients, on the weight-gradient stream
-            self._weight_grads(b, gz)
-        if self.kind == "FM":  # DeepFM: summed on the weight-gradient stream (joined below)
-            hip_ops.tensor_sum(b.fm.loss_elem, scale=1.0 / B, out=b.loss)
-        # 5. gradients to the owners, summed per row in (source rank, position) order
+        self._sharded_fwd_bwd(ids, y, b, T, T_lin, bias, mean_div, F)
         t = self._mark("exchange")
         G = alltoallv(b.grad_rows, send_c, recv_c, self.group)
         G_lin = alltoallv(b.grad_lin, send_c, recv_c, self.group) if has_lin else None
@@ -218,7 +534,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             b.loss.div_(ws)
         self._span("exchange", t)
         t = self._mark("scatter")
-        b.gplan.build(req, self.V_tab)
+        b.gplan.build(req, self.E_tab.shape[0])
         hip_ops.segment_sum_rows(b.gplan, G, G_lin, rowmap=None, out=b.g_rows,
                                  out_lin=b.g_lin if has_lin else None)
         self._span("scatter", t)
@@ -251,26 +567,39 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._ahead_counts[k] = c
         return b.loss
 
-    def gather_tables(self) -> tuple[torch.Tensor, torch.Tensor | None]:
+    # ---------------------------------------------------------------- the tables ------
+    def gather_tables(self, device=None) -> tuple[torch.Tensor, torch.Tensor | None]:
         """Full (E [V,K], w [V,1] or None for InnerPNN) assembled from every rank's shard
-        (after a flush)."""
+        (after a flush); every rank calls it. device: where the result goes (default: the
+        trainer's device; "cpu" for a table larger than one GPU: the shards then travel one
+        at a time, nothing of full size is allocated on a device)."""
         self.flush()
-        E = self.model.feature_embedding.weight.data
-        w = self.model.linear.weight.data if self.w_tab is not None else None
+        dev = torch.device(device) if device is not None else self.device
+        E_loc = self.E_tab[:self.V_tab]
+        w_loc = self.w_tab[:self.V_tab] if self.w_tab is not None else None
         if self.world_size == 1:
-            return E.clone(), (w.clone() if w is not None else None)
+            return (E_loc.to(dev, copy=True),
+                    w_loc.to(dev, copy=True).view(-1, 1) if w_loc is not None else None)
+        gloo = dist.get_backend(self.group) == "gloo"
 
         def gather(tab, width):
-            out = torch.empty(self.shard_rows * self.world_size, width, dtype=tab.dtype,
-                              device=tab.device)
             send = torch.zeros(self.shard_rows, width, dtype=tab.dtype, device=tab.device)
-            send[:self.V_tab] = tab.view(self.V_tab, width)
-            if tab.is_cuda and dist.get_backend(self.group) == "gloo":
-                o = out.cpu()
-                dist.all_gather_into_tensor(o, send.cpu(), group=self.group)
-                out.copy_(o)
-            else:
+            send[:self.V_tab] = tab.reshape(self.V_tab, width)
+            if dev.type == "cuda" and not gloo:
+                out = torch.empty(self.shard_rows * self.world_size, width, dtype=tab.dtype,
+                                  device=dev)
                 dist.all_gather_into_tensor(out, send, group=self.group)
-            return out[:self.V]
+                return out[:self.V]
+            out = torch.empty(self.V, width, dtype=tab.dtype, device=dev)
+            buf = send.cpu() if gloo else torch.empty_like(send)
+            for r in range(self.world_size):  # one shard in flight at a time
+                src = dist.get_global_rank(self.group, r) if self.group is not None else r
+                if r == self.rank:
+                    buf.copy_(send)
+                dist.broadcast(buf, src=src, group=self.group)
+                lo = r * self.shard_rows
+                cnt = max(0, min(self.shard_rows, self.V - lo))
+                out[lo:lo + cnt].copy_(buf[:cnt])
+            return out
 
-        return gather(self.E_tab, self.K), (gather(self.w_tab, 1) if w is not None else None)
+        return gather(E_loc, self.K), (gather(w_loc, 1) if w_loc is not None else None)

@@ -90,7 +90,8 @@ class InputSlot:
     passes through the slot, so a stream of fresh batches replays the same graphs (the
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
-    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "stream_i")
+    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "stream_i", "cap",
+                 "counts")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -101,6 +102,7 @@ class InputSlot:
         self.ev = None          # staged ahead: the copy + plan on the plan stream recorded here
         self.plan_graph = None  # the plan build of this slot, captured on its plan stream
         self.stream_i = 0
+        self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
 
 
 @dataclass
@@ -153,7 +155,7 @@ class FusedCTRTrainer:
         self.device = E.device
         if self.device.type != "cuda":
             raise RuntimeError("FusedCTRTrainer needs the model on a ROCm device")
-        self.V, self.K = E.shape
+        self.V, self.K = self._vocab_size(E), E.shape[1]
         named = dict(model.named_parameters())
         self.dense_names = {"DeepFM": DEEPFM_DENSE, "FM": FM_DENSE, "IPNN": IPNN_DENSE}[self.kind]
         # 16-B aligned views (offsets multiples of 4 floats): the GEMMs read the weights
@@ -179,22 +181,23 @@ class FusedCTRTrainer:
         # ShardedCTRTrainer (rl_ctr_prediction_amd/sharded.py)
         self.row_lo, self.row_hi = self._table_rows()
         self.V_tab = self.row_hi - self.row_lo
-        self.E_tab = E.data[self.row_lo:self.row_hi]
+        self.E_tab = self._own_rows(E.data)
+        n_rows = self.E_tab.shape[0]  # V_tab (+ a spare row under row sharding)
         self.m_E = torch.zeros_like(self.E_tab)
         self.v_E = torch.zeros_like(self.E_tab)
         if self.kind == "IPNN":  # no linear table: every lin pointer of the ABI is NULL
             self.w_tab = self.m_w = self.v_w = None
         else:
-            self.w_tab = model.linear.weight.data[self.row_lo:self.row_hi]
-            self.m_w = torch.zeros(self.V_tab, dtype=torch.float32, device=self.device)
+            self.w_tab = self._own_rows(model.linear.weight.data)
+            self.m_w = torch.zeros(n_rows, dtype=torch.float32, device=self.device)
             self.v_w = torch.zeros_like(self.m_w)
         if optimizer_mode not in ("deferred", "dense"):
             raise ValueError(f"optimizer_mode must be 'deferred' or 'dense', not {optimizer_mode!r}")
         self.deferred = optimizer_mode == "deferred"
         # dense mode: row -> compact gradient slot map; deferred mode: the owner scratch of
         # the plan-free catch-up (csrc/adam.hip deferred_mark_kernel)
-        self.rowmap = torch.full((self.V_tab,), -1, dtype=torch.int32, device=self.device)
-        self.last = torch.zeros(self.V_tab, dtype=torch.int32, device=self.device)
+        self.rowmap = torch.full((n_rows,), -1, dtype=torch.int32, device=self.device)
+        self.last = torch.zeros(n_rows, dtype=torch.int32, device=self.device)
         # device step counters: [0] completed steps, [1] the step in flight (ctr_step_begin/end)
         # initialised to {0, 1}: ctr_step_end advances both, so no step-begin launch is needed
         self.step_ctr = torch.tensor([0, 1], dtype=torch.int32, device=self.device)
@@ -310,6 +313,14 @@ class FusedCTRTrainer:
     def _table_rows(self) -> tuple[int, int]:
         return 0, self.V
 
+    def _vocab_size(self, E) -> int:
+        return E.shape[0]
+
+    def _own_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """This trainer's rows of a table Parameter's data (ShardedCTRTrainer: the data IS
+        the shard)."""
+        return t[self.row_lo:self.row_hi]
+
     def _mark(self, key):
         if self.timing is None or key not in self.timing:
             return None
@@ -382,8 +393,9 @@ class FusedCTRTrainer:
 
     def _bound_staleness(self) -> None:
         """Flush once `flush_every` steps have passed since the last flush: no row is then
-        more than that many steps behind when a batch reads it."""
-        if (self.deferred and self.flush_every > 0
+        more than that many steps behind when a batch reads it (with the background sweep
+        on, the sweep bounds the staleness instead)."""
+        if (self.deferred and self.flush_every > 0 and not self.sweep_slices
                 and self.step_count - self._flushed_at >= self.flush_every):
             self.flush()
 

@@ -215,3 +215,34 @@ def assert_preds_within_spread(actual, desired, spread_key, *, factor=2.0, err_m
     assert dev <= bar, (f"{err_msg}: prediction deviation {dev:.3g} > bar {bar:.3g} "
                         f"(reference spread {spread:.3g})")
     return dev
+
+
+def collect_ranks(procs, q, n, timeout=240.0):
+    """n results from the rank processes' queue; fails at once when a rank exits with an
+    error (its peers would otherwise wait in a collective until the timeout), and prints
+    a heartbeat so a long multi-process test is not mistaken for a hung one."""
+    import queue
+    import sys
+    import time
+    out, t0, beat = [], time.time(), time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=5))
+            continue
+        except queue.Empty:
+            pass
+        dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+        if dead:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+            raise AssertionError(f"a rank process failed (exit codes {dead})")
+        if time.time() - t0 > timeout:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+            raise AssertionError(f"ranks timed out after {timeout:.0f} s")
+        if time.time() - beat > 30:
+            print(f"[ranks] waiting {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+            beat = time.time()
+    return out

@@ -17,6 +17,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import collect_ranks
+
 
 def _free_port():
     s = socket.socket()
@@ -74,8 +76,7 @@ def test_sparse_exchange_gloo(world):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r = q.get(timeout=120)
+    for r in collect_ranks(procs, q, world):
         res[r[0]] = r[1:]
     for p in procs:
         p.join(timeout=60)
@@ -148,8 +149,7 @@ def test_row_sharded_exchange_gloo(world):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r = q.get(timeout=120)
+    for r in collect_ranks(procs, q, world):
         res[r[0]] = r[1:]
     for p in procs:
         p.join(timeout=60)
@@ -168,3 +168,84 @@ def test_row_sharded_exchange_gloo(world):
         np.testing.assert_array_equal(u_o, np.nonzero(expect[rank * shard:(rank + 1) * shard])[0]
                                       + rank * shard)
         np.testing.assert_allclose(sums[:, 0], expect[u_o])
+
+
+# ------------------------------------------------- fixed-capacity (padded) exchange ----
+def _padded_worker(rank, world, port, q):
+    """ShardedCTRTrainer's fixed-capacity protocol with numpy standing in for the GPU
+    kernels (ctr_shard_pack_ids / ctr_shard_runs_copy): capacity agreed by an all-reduce MAX,
+    equal-split all-to-alls of ids, rows and gradients, padding entries on each owner's spare
+    row (index = its row count)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rl_ctr_prediction_amd.distributed import alltoall_equal
+        V, K = 1000, 4
+        shard = -(-V // world)
+        lo, hi = rank * shard, min(V, (rank + 1) * shard)
+        table = np.arange(V * K, dtype=np.float32).reshape(V, K)
+        mine = np.concatenate([table[lo:hi], np.full((1, K), -7, np.float32)])  # + spare row
+        rng = np.random.default_rng(7 + rank)
+        ids = rng.integers(0, V, size=500 + 111 * rank)
+        ids[:50] = 3
+        uniq = np.unique(ids)
+        owner = uniq // shard
+        counts = np.bincount(owner, minlength=world)
+        offsets = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        cap = torch.tensor([int(counts.max())])
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+        C = int(-(-int(cap) // 64) * 64)
+        send = np.empty(world * C, np.int32)
+        for j in range(world):
+            spare = min(shard, V - j * shard)
+            run = uniq[offsets[j]:offsets[j] + counts[j]] - j * shard
+            send[j * C:(j + 1) * C] = np.concatenate([run, np.full(C - counts[j], spare)])
+        recv = torch.empty(world * C, dtype=torch.int32)
+        alltoall_equal(recv, torch.tensor(send))
+        loc = recv.numpy()
+        assert ((loc >= 0) & (loc <= hi - lo)).all()
+        rows_in = torch.empty(world * C, K)
+        alltoall_equal(rows_in, torch.tensor(mine[loc]))
+        got = np.concatenate([rows_in.numpy()[j * C:j * C + counts[j]] for j in range(world)])
+        np.testing.assert_array_equal(got, table[uniq])          # unpacked, compact order
+        cnt = np.array([(ids == u).sum() for u in uniq], dtype=np.float32)
+        g = np.repeat((cnt * (rank + 1))[:, None], K, axis=1)
+        g_pad = np.zeros((world * C, K), np.float32)
+        for j in range(world):
+            g_pad[j * C:j * C + counts[j]] = g[offsets[j]:offsets[j] + counts[j]]
+        g_in = torch.empty(world * C, K)
+        alltoall_equal(g_in, torch.tensor(g_pad))
+        sums = np.zeros((hi - lo + 1, K), np.float32)
+        np.add.at(sums, loc, g_in.numpy())
+        assert (sums[-1] == 0).all()                               # padding: zero gradients
+        nz = np.nonzero(sums[:-1, 0])[0]
+        q.put((rank, nz + lo, sums[nz]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_padded_exchange_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in collect_ranks(procs, q, world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    V = 1000
+    shard = -(-V // world)
+    expect = np.zeros(V)
+    for rank in range(world):
+        rng = np.random.default_rng(7 + rank)
+        ids = rng.integers(0, V, size=500 + 111 * rank)
+        ids[:50] = 3
+        np.add.at(expect, ids, rank + 1)
+    for rank in range(world):
+        rows, sums = res[rank]
+        np.testing.assert_array_equal(rows, np.nonzero(expect[rank * shard:(rank + 1) * shard])[0]
+                                      + rank * shard)
+        np.testing.assert_allclose(sums[:, 0], expect[rows])

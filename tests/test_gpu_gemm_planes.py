@@ -106,7 +106,8 @@ def test_gemm_planes_every_tiling(cuda, tile, monkeypatch):
     g = torch.Generator().manual_seed(tile)
     for splits in (1, 3):
         monkeypatch.setenv("CTR_GEMM_PLANES_CFG", f"{tile},{splits}")
-        for (M, N, K) in ((333, 452, 1060), (97, 451, 259)):
+        # K: not multiples of 32; padded to multiples of 64 (the KS = 2 tilings' stage)
+        for (M, N, K) in ((333, 452, 1060), (97, 451, 380)):
             Ai = torch.randint(-3, 4, (M, K), generator=g).float()
             Bi = torch.randint(-3, 4, (K, N), generator=g).float()
             A = torch.randn(M, K, generator=g)

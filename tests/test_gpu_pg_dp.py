@@ -21,7 +21,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import AdamBound, grad_bound
+from conftest import collect_ranks, AdamBound, grad_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -90,8 +90,7 @@ def _run(world, train, cuts):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r = q.get(timeout=300)
+    for r in collect_ranks(procs, q, world):
         res[r[0]] = r[1:]
     for p in procs:
         p.join(timeout=60)

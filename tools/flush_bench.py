@@ -26,8 +26,19 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-lin", action="store_true")
+    ap.add_argument("--variants", default="", help="comma-separated CTR_FLUSH_PIPE values (A/B)")
+    ap.add_argument("--steps-list", default="", help="comma-separated replay lengths")
     args = ap.parse_args()
-    V, K, T = args.V, args.K, args.steps
+    import os
+    for pv in (args.variants.split(",") if args.variants else [None]):
+        for T in (map(int, args.steps_list.split(",")) if args.steps_list else [args.steps]):
+            if pv is not None:
+                os.environ["CTR_FLUSH_PIPE"] = pv
+            run(args, T, pv)
+
+
+def run(args, T, variant):
+    V, K = args.V, args.K
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     E = torch.randn(V, K, device=dev, generator=g).mul_(0.05)
@@ -50,7 +61,7 @@ def main():
             times.append(e0.elapsed_time(e1))
     ms = sorted(times)[len(times) // 2]
     nbytes = 24 * V * K + (0 if lin is None else 24 * V) + 8 * V
-    print(json.dumps({"kernel": "deferred_flush_vec (+deferred_flush_lin)", "V": V, "K": K,
+    print(json.dumps({"kernel": "deferred_flush", "variant": variant, "V": V, "K": K,
                       "steps_replayed": T, "ms": ms, "ms_all": times,
                       "GBps": nbytes / (ms * 1e-3) / 1e9,
                       "elem_steps_per_s": V * (K + (0 if lin is None else 1)) * T / (ms * 1e-3)}))
