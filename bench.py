@@ -398,6 +398,9 @@ def main():
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="launch every step eagerly (no HIP-graph replay): the host-paced "
+                         "launch path that N > 1 row sharding takes without CTR_SHARDED_GRAPHS")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -450,6 +453,8 @@ def main():
         trainer = FusedCTRTrainer(model, lr=1e-3, weight_decay=1e-5, seed=1234,
                                   optimizer_mode=args.optimizer)
     trainer.sweep_slices = args.sweep_slices
+    if args.no_graphs:
+        trainer.use_graphs = False
     if args.flush_every is not None:
         trainer.flush_every = args.flush_every
     log(f"rank {rank}/{world}: {cfg['kind']} V={V} K={K} B={B} ready in {time.perf_counter() - t0:.1f}s")

@@ -10,8 +10,10 @@ per step:
      step with next_x); its unique rows are ascending, hence grouped by owner;
   2. the exchange capacity C: the largest per-owner run over every rank's batch (one
      all-reduce MAX of a scalar on the plan stream, read by the host: the step's only host
-     read, and with next_x a read of work finished long before), rounded up to a multiple
-     of 1024 rows so a handful of capacities cover all batches;
+     read, and with next_x a read of work finished long before); the capacity in use only
+     grows — past a batch that exceeds it, to that run + 1/32, rounded up to 1024 rows — so
+     after the first few steps every batch fits one capacity (one set of buffers, one
+     graph per input slot);
   3. equal-split all-to-alls of C rows per (requester, owner) pair — row ids out
      (ctr_shard_pack_ids: each owner's run, padded with the owner's spare row), rows back,
      gradients out (ctr_shard_runs_copy packs / unpacks the runs): their sizes depend on C
@@ -132,6 +134,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._count_group = dist.new_group()
         self._ahead_counts: dict = {}
         self._xbufs: dict = {}
+        self._cap = 0  # the exchange capacity in use (rows per (requester, owner) pair)
         # graph replay of the fixed-capacity step: at one process always (no collective), at
         # N > 1 only where the collectives can be captured (RCCL) and it is asked for
         backend = dist.get_backend(self.group) if self.world_size > 1 else None
@@ -247,7 +250,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         ev_start = torch.cuda.Event()
         ev_start.record(main)  # everything enqueued before this step
         if slot is None:  # copy and plan now, on the plan stream
-            slot = self._acquire_slot(shape)
+            slot = self._acquire_slot(shape, ahead=True)
             ps.wait_event(ev_start)
             torch.cuda.set_stream(ps)
             try:
@@ -267,7 +270,15 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             ev_plan = torch.cuda.Event()
             ev_plan.record(ps)
         self._span("plan", t)
-        C = max(CAP_QUANTUM, -(-cmax // CAP_QUANTUM) * CAP_QUANTUM)
+        if cmax > self._cap:  # grows only (every rank sees the same cmax: the same C)
+            grown = cmax + cmax // 32  # headroom: a later, slightly larger batch still fits
+            C = max(CAP_QUANTUM, -(-grown // CAP_QUANTUM) * CAP_QUANTUM)
+            if self._xbufs:  # the smaller capacity's buffers and graphs are never used again
+                torch.cuda.synchronize(self.device)
+                self._graphs = {k: v for k, v in self._graphs.items() if k[2] == C}
+                self._xbufs = {k: v for k, v in self._xbufs.items() if k[2] == C}
+            self._cap = C
+        C = self._cap
         main.wait_event(ev_plan)
         if self.use_graphs and self._graph_ok and self.timing is None:
             loss = self._sharded_graph_step(slot, mean_div, C)
@@ -276,7 +287,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             loss = self._launch_sharded(slot, mean_div, C)
             self._after_step()
         for n, k in todo:
-            s = self._acquire_slot(shape, exclude=slot)
+            s = self._acquire_slot(shape, exclude=slot, ahead=True)
             ps.wait_event(ev_start)
             torch.cuda.set_stream(ps)
             try:
@@ -288,6 +299,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 torch.cuda.set_stream(main)
             self._staged[k] = s
         return loss
+
+    def _slot_stream(self, stream_i: int):
+        return self._plan_stream  # every slot is copied and planned on the one plan stream
 
     def _plan_slot(self, slot: InputSlot) -> None:
         """On the current (plan) stream: the slot's plan, its largest per-owner run
@@ -554,11 +568,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             k = self._xkey(n)
             if k in self._pending:
                 continue
-            P = self._plan_for(n)
-            c = torch.empty(ws, dtype=torch.int64, device=self.device)
             ps.wait_event(ev_start)
             n.record_stream(ps)
-            with torch.cuda.stream(ps):
+            with torch.cuda.stream(ps):  # allocated from the plan stream's pool: its writer
+                P = self._plan_for(n)
+                c = torch.empty(ws, dtype=torch.int64, device=self.device)
                 P.build(n, self.V, err_flag=self.err)
                 P.shard_counts(self.shard_rows, ws, out=c)
                 ev = torch.cuda.Event()

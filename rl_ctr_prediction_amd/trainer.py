@@ -546,11 +546,19 @@ class FusedCTRTrainer:
             r = self._rings[shape] = []
         return r
 
-    def _acquire_slot(self, shape, exclude=None) -> InputSlot:
+    def _slot_stream(self, stream_i: int):
+        """Plan stream number stream_i (created on first use)."""
+        while stream_i > len(self._extra_plan_streams):
+            self._extra_plan_streams.append(torch.cuda.Stream(device=self.device))
+        return self._plan_stream if stream_i == 0 else self._extra_plan_streams[stream_i - 1]
+
+    def _acquire_slot(self, shape, exclude=None, ahead: bool = False) -> InputSlot:
         """The lowest-index slot of the shape's ring that no staged batch holds (and that is
         not `exclude`, the current step's); the ring grows up to max_slots. Lowest index
         first keeps the set of (slot, planned-ahead) graphs small: the first step of an
-        epoch always lands in slot 0."""
+        epoch always lands in slot 0. ahead: the new slot's first writer is its plan stream,
+        so its buffers come from that stream's pool (a block the current stream freed during
+        this step may still be read by work the plan stream does not wait for)."""
         ring = self._ring(shape)
         busy = {id(s) for s in self._staged.values()}
         if exclude is not None:
@@ -560,8 +568,14 @@ class FusedCTRTrainer:
                 return s
         if len(ring) >= self.max_slots:
             raise RuntimeError(f"FusedCTRTrainer: more than {self.max_slots} batches staged ahead")
-        s = InputSlot(shape, len(ring), self.device)
-        s.stream_i = s.index % max(1, self.n_plan_streams)
+        index = len(ring)
+        stream_i = index % max(1, self.n_plan_streams)
+        if ahead and self._plan_stream is not None:
+            with torch.cuda.stream(self._slot_stream(stream_i)):
+                s = InputSlot(shape, index, self.device)
+        else:
+            s = InputSlot(shape, index, self.device)
+        s.stream_i = stream_i
         ring.append(s)
         return s
 
@@ -570,10 +584,8 @@ class FusedCTRTrainer:
         """Copy ids nx into a free slot and build its sparse plan there, on the slot's plan
         stream, concurrently with the step just enqueued (replayed from the slot's own
         plan graph once captured)."""
-        s = self._acquire_slot(shape, exclude=current)
-        while s.stream_i > len(self._extra_plan_streams):
-            self._extra_plan_streams.append(torch.cuda.Stream(device=self.device))
-        ps = self._plan_stream if s.stream_i == 0 else self._extra_plan_streams[s.stream_i - 1]
+        s = self._acquire_slot(shape, exclude=current, ahead=True)
+        ps = self._slot_stream(s.stream_i)
         ps.wait_event(ev_start)
         # torch.cuda.set_stream on the known streams instead of the torch.cuda.stream
         # context manager (~9 us per use: it looks the current stream up again)
