@@ -502,8 +502,11 @@ def main():
     # timed region: nothing instrumented (at N=1 the steps replay as HIP graphs)
     trainer.timing = None
     t_start = time.perf_counter()
+    host_s = 0.0  # time spent inside step() (enqueueing): the host's share of a step
     for i in range(args.steps):
+        t_h = time.perf_counter()
         step(i)
+        host_s += time.perf_counter() - t_h
     # deferred mode: every row is brought to the last step INSIDE the timed region, so the
     # measured work is the complete dense-Adam trajectory of K steps (nothing left owed)
     trainer.flush()
@@ -643,6 +646,7 @@ def main():
                                           and args.optimizer == "deferred") else 0)},
         "roofline": roofline,
         "kernels": kernels,
+        "host_ms_per_step": host_s / args.steps * 1e3,  # inside step(): the enqueue cost
         "gather_scatter": {
             "gather_kernel": g_kernel, "gather_ms": gather_ms,
             "gather_GBps": g_bytes / (gather_ms * 1e-3) / 1e9,

@@ -570,6 +570,31 @@ int ctr_pg_loss_grad_global(const float* probs, const int64_t* acts, int64_t B, 
                             const float* vt_mean, float grad_scale, float* loss_out,
                             float* dlogits, ctr_stream_t stream);
 
+/* ---- step launch (host-side sequence of one single-process training step) ------------
+ * Replaces the host side of the reference's per-batch loop body (all_main/pretrain_main.py:
+ * 71-78: forward, loss, backward and optimizer.step issued once per batch) once that body is
+ * a captured HIP graph per input slot: in ONE call,
+ *   1. if n_stages > 0: record start_event on main_stream (everything enqueued before this
+ *      step — the last readers of the slots the stages overwrite);
+ *   2. if wait_event: main_stream waits for it (the slot's ids staged and planned ahead);
+ *   3. copy y_bytes from y_src to y_dst on main_stream (the batch's labels into the slot);
+ *   4. launch step_graph (a hipGraphExec_t) on main_stream;
+ *   5. for each stage: its stream waits for start_event, `bytes` are copied src -> dst on it
+ *      (the next batch's ids into its slot), plan_graph (its sparse plan build, or NULL) is
+ *      launched there and done_event recorded after.
+ * Device-to-device copies only; events, streams and graph execs are the caller's. */
+typedef struct ctr_stage {
+  const void* src;
+  void* dst;
+  int64_t bytes;
+  ctr_stream_t stream;
+  void* plan_graph; /* hipGraphExec_t or NULL */
+  void* done_event; /* hipEvent_t */
+} ctr_stage;
+int ctr_step_launch(ctr_stream_t main_stream, void* wait_event, const void* y_src, void* y_dst,
+                    int64_t y_bytes, void* step_graph, void* start_event,
+                    const ctr_stage* stages, int n_stages);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,13 @@ class PlaneViewDesc(C.Structure):
     """Mirror of ``ctr_plane_view`` (include/ctr_hip.h)."""
     _fields_ = [("offset", _i64), ("rows", _i64), ("cols", _i64), ("planes", PlanesDesc)]
 
+
+class StageDesc(C.Structure):
+    """Mirror of ``ctr_stage`` (include/ctr_hip.h)."""
+    _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64), ("stream", _vp),
+                ("plan_graph", _vp), ("done_event", _vp)]
+
+
 # name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
 # against the header.
 SIGNATURES = {
@@ -107,6 +114,7 @@ SIGNATURES = {
     "ctr_ids_add": (_i32, [_vp, _i64, _i32, _vp]),
     "ctr_shard_pack_ids": (_i32, [_plan_p, _i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "ctr_shard_runs_copy": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _vp]),
+    "ctr_step_launch": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, C.POINTER(StageDesc), _i32]),
     "ctr_segment_workspace_bytes": (_i64, [_i64, _i32]),
     "ctr_fm_embedding_grad": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _i64, _vp]),

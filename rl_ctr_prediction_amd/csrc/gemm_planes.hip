@@ -672,14 +672,20 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     return c;
   }
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
-  static const bool wide_wg = [] {
+  static const int wide_wg = [] {  // 0 off, 1 (default) wide operands of N >= 768, 2 any N
     const char* e = getenv("CTR_GEMM_PLANES_WIDE");
-    return e && e[0] == '1';
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
   }();
-  if (wide_wg && a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320) {
+  if (wide_wg && a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320 &&
+      (wide_wg == 2 || N >= 768)) {
     // whole-M tile (the wide operand read once), split-K to about one block per CU.
-    // Measured standalone (operands MALL-warm, tools/gemm_planes_bench.py): slower than the
-    // 64x64 tiles below (dW0 71 vs 66 us, dW1 28-30 vs 22.5): opt-in (CTR_GEMM_PLANES_WIDE)
+    // Standalone (operands MALL-warm) it is no faster than 64x64 tiles (dW0 71 vs 66 us
+    // with the compiler's transpose reads); in the step, where dW0 runs beside the scatter
+    // chain and the two compete for HBM, reading X's planes once instead of once per
+    // 64-row M tile measured C3 11.94 -> 12.32 M ex/s (12.48 -> 12.75 with plan lookahead;
+    // two alternating runs each). Not for narrower N: the policy net's 256 x 512 weight
+    // gradient (C4) measured 8.49 wide vs 8.72 M transitions/s on the 64x64 tiles.
+    // CTR_GEMM_PLANES_WIDE=0: the 64x64 tiles everywhere; 2: wide for any N
     const int ti = M <= 192 ? 27 : M <= 256 ? 26 : 25;
     const int64_t tiles = ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(256 / tiles, Kp / 256), 64));

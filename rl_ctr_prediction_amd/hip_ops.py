@@ -430,6 +430,10 @@ class SparsePlanBuffers:
         self.num_unique = torch.zeros(1, **i32)
         self.S = 0
         self._struct = SparsePlan()
+        # the plan's own radix scratch (not the per-stream Workspace): plans are built on the
+        # plan streams concurrently with steps, and their captured graphs replay there, so
+        # their scratch must be private to the plan
+        self._ws = None
 
     def struct(self, rows_are_segments: bool = False) -> SparsePlan:
         """The ctr_sparse_plan of these buffers. rows_are_segments: present each position's
@@ -448,12 +452,17 @@ class SparsePlanBuffers:
         if S > self.capacity:
             raise ValueError(f"sparse plan: {S} slots > capacity {self.capacity}")
         self.S = S
-        nbytes = lib.ctr_sparse_plan_workspace_bytes(S, int(V))
-        if nbytes < 0:
+        need = lib.ctr_sparse_plan_workspace_bytes(S, int(V))
+        if need < 0:
             raise RuntimeError(lib.load().ctr_last_error().decode())
-        ws = Workspace.get(nbytes, self.device)
-        lib.ctr_sparse_plan_build(_p(idx), it, int(V), self.struct(), _p(ws),
-                                  0 if ws is None else ws.numel(), _p(err_flag), _stream())
+        if self._ws is None or self._ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("sparse plan: scratch grown inside a graph capture (build "
+                                   "these buffers once eagerly first)")
+            full = lib.ctr_sparse_plan_workspace_bytes(max(self.capacity, 1), int(V))
+            self._ws = torch.empty(max(need, full, 256), dtype=torch.uint8, device=self.device)
+        lib.ctr_sparse_plan_build(_p(idx), it, int(V), self.struct(), _p(self._ws),
+                                  self._ws.numel(), _p(err_flag), _stream())
         return self
 
     def num_unique_host(self) -> int:

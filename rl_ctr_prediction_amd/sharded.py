@@ -124,7 +124,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # of the step with next_x; the per-step agreement runs there on a communicator of
         # its own, so the host waits for that stream only, never for the previous step
         if self._plan_stream is None:
-            self._plan_stream = torch.cuda.Stream(device=self.device)
+            self._plan_stream = self._new_stream()
         self._count_group = count_group
         if self.world_size > 1 and count_group is None:
             if process_group is not None:
@@ -339,7 +339,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool):
+                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
                     self._launch_sharded(slot, mean_div, C)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1

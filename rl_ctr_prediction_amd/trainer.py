@@ -36,6 +36,7 @@ import torch
 import torch.nn as nn
 
 from . import hip_ops
+from ._lib import StageDesc, lib
 from .distributed import allgather_sparse_rows, allreduce_sum_, world
 from .p_model import FM, DeepFM, InnerPNN
 
@@ -90,8 +91,8 @@ class InputSlot:
     passes through the slot, so a stream of fresh batches replays the same graphs (the
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
-    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "stream_i", "cap",
-                 "counts")
+    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "plan_exec",
+                 "done_ev", "stream_i", "cap", "counts")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -101,6 +102,8 @@ class InputSlot:
         self.plan = hip_ops.SparsePlanBuffers(B * F, device)
         self.ev = None          # staged ahead: the copy + plan on the plan stream recorded here
         self.plan_graph = None  # the plan build of this slot, captured on its plan stream
+        self.plan_exec = None   # its hipGraphExec_t (ctr_step_launch launches it natively)
+        self.done_ev = None     # the slot's staging event (one per slot, re-recorded)
         self.stream_i = 0
         self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
 
@@ -229,12 +232,19 @@ class FusedCTRTrainer:
         self._staged: dict = {}    # ids key of a batch staged ahead -> its InputSlot
         self.max_slots = 8
         self.captures = 0          # step graphs captured (tests: bounded, batch-independent)
-        # lookahead pays where the plan is the step's critical path (FM: C2 35.5 -> 50.9 M
-        # ex/s); the MLP kinds build it on the graph's side list under the catch-up and the
-        # forward, where it finishes long before the scatter needs it, while a lookahead plan
-        # runs under dX / the scatter and slows them (C3 12.8 vs 12.7 M ex/s)
+        # the steady-state single-process step issued by one native call (ctr_step_launch)
+        # instead of ~10 torch calls from Python (CTR_NATIVE_LAUNCH=0: the Python path)
+        self.native_launch = os.environ.get("CTR_NATIVE_LAUNCH", "1") != "0"
+        self._native_launch = lib.ctr_step_launch
+        self._ev_start = None
+        self.native_steps = 0  # steps issued by ctr_step_launch (tests)
+        # lookahead (every kind): the next batches' ids are staged and planned on the plan
+        # stream, so the step graph starts with no copy and no plan branch, and catches its
+        # rows up over the plan's unique rows in one launch. FM: C2 35.5 -> 50.9 M ex/s; C3
+        # streaming fresh batches 11.94 -> 12.48 M ex/s (two alternating runs each; with
+        # cycled batches it had measured 12.7 vs 12.8, the in-step copies then absent)
         env = os.environ.get("CTR_PLAN_LOOKAHEAD")
-        self.plan_lookahead = (env == "1") if env in ("0", "1") else self.kind == "FM"
+        self.plan_lookahead = (env == "1") if env in ("0", "1") else True
         # bounded staleness of deferred Adam: every `flush_every` steps all rows are brought
         # to the current step (one tiled flush pass), so a row a batch touches has missed at
         # most that many steps and the in-step catch-up replays stay short under a stream
@@ -249,7 +259,14 @@ class FusedCTRTrainer:
         # (CTR_CATCHUP_BY_PLAN=0: the id-driven pair, A/B)
         self.catchup_by_plan = os.environ.get("CTR_CATCHUP_BY_PLAN", "1") != "0"
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
-        self._side = torch.cuda.Stream(device=self.device) if self.deferred and self._vec_ok else None
+        # every stream of this trainer has a HIP handle of its own (_new_stream): the scratch
+        # buffers of hip_ops.Workspace are per stream handle, and torch hands streams out of
+        # a 32-stream pool round-robin, so two roles could otherwise alias one stream and
+        # share scratch while running concurrently (the step graphs are captured on the
+        # trainer's own capture stream for the same reason, not on torch's global one)
+        self._own_streams: list = []
+        self._capture_stream = self._new_stream()
+        self._side = self._new_stream() if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
         # long after the plan is built): the captured graph then has exactly two parallel
         # lists — the critical path and one side list — and the HIP graph executor cannot
@@ -257,7 +274,7 @@ class FusedCTRTrainer:
         # with three: the plan queued behind the weight gradients, +100 us per step)
         self._wgrad_stream = None
         if self.kind in _MLP_KINDS:
-            self._wgrad_stream = self._side if self._side is not None else torch.cuda.Stream(device=self.device)
+            self._wgrad_stream = self._side if self._side is not None else self._new_stream()
         # the MLP weights' planes: rewritten by the dense Adam with every update
         # (ctr_adam_dense_planes), re-split from the fp32 parameters (the source of truth:
         # state_dict / load_state_dict see fp32) whenever those changed outside the trainer
@@ -272,7 +289,7 @@ class FusedCTRTrainer:
         self._sweep_stream = None
         self._plan_stream = None
         if self._side is not None:
-            self._plan_stream = torch.cuda.Stream(device=self.device)
+            self._plan_stream = self._new_stream()
         # lookahead plans may alternate over n_plan_streams streams (each key keeps its own:
         # its captured graph holds that stream's scratch), two plans in flight at once.
         # Default 2: with the host off the step's critical path (step(): 30 us of Python),
@@ -518,11 +535,15 @@ class FusedCTRTrainer:
             for k in [k for k in self._staged if k not in keep]:
                 main.wait_event(self._staged.pop(k).ev)  # its plan-stream writes come first
         todo = [(n, k) for n, k in nk if k not in self._staged]
+        have = slot is not None
+        if have and self.native_launch and self.use_graphs and self.timing is None:
+            loss = self._native_step(slot, y, mean_div, todo, shape, main)
+            if loss is not None:
+                return loss
         ev_start = None
         if todo:  # everything enqueued before this step (the last users of the slots)
-            ev_start = torch.cuda.Event()
+            ev_start = self._start_event()
             ev_start.record(main)
-        have = slot is not None
         if have:  # copied and planned ahead on the plan stream
             main.wait_event(slot.ev)
             slot.ev = None
@@ -546,10 +567,22 @@ class FusedCTRTrainer:
             r = self._rings[shape] = []
         return r
 
+    def _new_stream(self):
+        """A torch stream whose HIP handle no other stream of this trainer (nor the stream
+        current at construction, where the steps are usually issued) has."""
+        taken = {s.cuda_stream for s in self._own_streams}
+        taken |= {0, torch.cuda.current_stream(self.device).cuda_stream}
+        for _ in range(64):
+            st = torch.cuda.Stream(device=self.device)
+            if st.cuda_stream not in taken:
+                self._own_streams.append(st)
+                return st
+        raise RuntimeError("FusedCTRTrainer: no free stream in torch's stream pool")
+
     def _slot_stream(self, stream_i: int):
         """Plan stream number stream_i (created on first use)."""
         while stream_i > len(self._extra_plan_streams):
-            self._extra_plan_streams.append(torch.cuda.Stream(device=self.device))
+            self._extra_plan_streams.append(self._new_stream())
         return self._plan_stream if stream_i == 0 else self._extra_plan_streams[stream_i - 1]
 
     def _acquire_slot(self, shape, exclude=None, ahead: bool = False) -> InputSlot:
@@ -603,14 +636,85 @@ class FusedCTRTrainer:
                     g = torch.cuda.CUDAGraph()
                     with graph_capture(g, pool=self._graph_pool, stream=ps):
                         s.plan.build(s.ids, self.V)  # captured, not executed
-                    s.plan_graph = g
+                    s.plan_graph, s.plan_exec = g, g.raw_cuda_graph_exec()
             self._span("plan", t)
-            ev = torch.cuda.Event()
+            ev = self._slot_event(s)
             ev.record(ps)
         finally:
             torch.cuda.set_stream(main)
         s.ev = ev
         self._staged[key] = s
+
+    def _slot_event(self, s: InputSlot):
+        if s.done_ev is None:
+            s.done_ev = torch.cuda.Event()
+        return s.done_ev
+
+    def _start_event(self):
+        if self._ev_start is None:
+            self._ev_start = torch.cuda.Event()
+        return self._ev_start
+
+    def _native_step(self, slot: InputSlot, y, mean_div: float, todo, shape, main):
+        """The steady-state step — labels into the staged slot, the slot's step graph, the
+        next batches copied into their slots and their plan graphs — in ONE native call
+        (ctr_step_launch: same calls, same order as the Python path below). Returns the
+        loss, or None (nothing done) when this step needs the Python path: a graph not
+        captured yet, a step-table re-size, or inputs that need a conversion."""
+        if (self.step_table.capacity < self.step_count + 2
+                or self._graph_tab_version != self.step_table.version):
+            return None
+        mlp = getattr(self.model, "mlp", None)
+        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
+        hit = self._graphs.get((slot.shape, slot.index, mean_div, self.model.training, drops,
+                                True))
+        if hit is None:
+            return None
+        B, _, dtype = shape
+        if not (y.is_cuda and y.dtype == torch.float32 and y.is_contiguous()
+                and y.numel() == B and y.device == self.device):
+            return None
+        for n, _ in todo:
+            if not (n.is_cuda and n.dtype == dtype and n.is_contiguous()
+                    and n.device == self.device):
+                return None
+        picked = []
+        for n, k in todo:
+            s = self._acquire_slot(shape, exclude=slot, ahead=True)
+            if s.plan_exec is None:  # its plan graph is captured by the Python path
+                for _, kk, _ in picked:
+                    del self._staged[kk]
+                return None
+            self._staged[k] = s  # marks it busy for the next acquire
+            picked.append((n, k, s))
+        stages = (StageDesc * max(1, len(picked)))()
+        for i, (n, _, s) in enumerate(picked):
+            ps = self._slot_stream(s.stream_i)
+            ev = self._slot_event(s)
+            st = stages[i]
+            st.src, st.dst, st.bytes = n.data_ptr(), s.ids.data_ptr(), n.numel() * n.element_size()
+            st.stream, st.plan_graph = ps.cuda_stream, s.plan_exec
+            st.done_event = self._event_handle(ev)
+        start = self._start_event()
+        g, self._bufs, exec_handle = hit
+        self._native_launch(main.cuda_stream, self._event_handle(slot.ev), y.data_ptr(),
+                            slot.y.data_ptr(), B * 4, exec_handle,
+                            self._event_handle(start) if picked else None, stages, len(picked))
+        for n, _, s in picked:
+            n.record_stream(self._slot_stream(s.stream_i))  # read there until the copy ran
+            s.ev = s.done_ev
+        slot.ev = None
+        self._bufs.plan = slot.plan
+        self._after_step()
+        self.native_steps += 1
+        return self._bufs.loss
+
+    @staticmethod
+    def _event_handle(ev):
+        """The hipEvent_t of a torch event (created by a first record if needed)."""
+        if ev.cuda_event == 0:
+            ev.record()
+        return ev.cuda_event
 
     @staticmethod
     def _xkey(x):
@@ -658,12 +762,12 @@ class FusedCTRTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool):
+                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
                     self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
-                self._graphs[key] = (g, self._bufs)
+                self._graphs[key] = (g, self._bufs, g.raw_cuda_graph_exec())
                 self.captures += 1
             return loss
-        g, self._bufs = hit  # the buffer set the graph was captured with
+        g, self._bufs, _ = hit  # the buffer set the graph was captured with
         self._bufs.plan = slot.plan
         g.replay()
         self._after_step()
@@ -850,7 +954,7 @@ class FusedCTRTrainer:
         if not (self.deferred and self._vec_ok and self.sweep_slices):
             return
         if self._sweep_stream is None:
-            self._sweep_stream = torch.cuda.Stream(device=self.device)
+            self._sweep_stream = self._new_stream()
         self._sweep_stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self._sweep_stream):
             t = self._mark("sweep")
