@@ -233,11 +233,17 @@ class FusedCTRTrainer:
         self.max_slots = 8
         self.captures = 0          # step graphs captured (tests: bounded, batch-independent)
         # the steady-state single-process step issued by one native call (ctr_step_launch)
-        # instead of ~10 torch calls from Python (CTR_NATIVE_LAUNCH=0: the Python path)
-        self.native_launch = os.environ.get("CTR_NATIVE_LAUNCH", "1") != "0"
+        # instead of ~10 torch calls from Python: opt-in (CTR_NATIVE_LAUNCH=1). It frees
+        # host time but measured no faster on MI355X boxes, where the step is GPU-bound
+        # (C2 50.6 / 49.7 vs 51.5 / 51.9 and 50.0 / 50.7 vs 49.8 / 53.2 M ex/s Python; C3
+        # within noise): the next batch's plan then starts sooner and overlaps more of the
+        # step (issued before the step graph it measured slower still, C2 44-48)
+        self.native_launch = os.environ.get("CTR_NATIVE_LAUNCH", "0") == "1"
         self._native_launch = lib.ctr_step_launch
         self._ev_start = None
         self.native_steps = 0  # steps issued by ctr_step_launch (tests)
+        self._dw0_fork = os.environ.get("CTR_DW0_FORK", "dx")
+        self._db0_last = os.environ.get("CTR_DB0_LAST", "0") == "1"
         # lookahead (every kind): the next batches' ids are staged and planned on the plan
         # stream, so the step graph starts with no copy and no plan branch, and catches its
         # rows up over the plan's unique rows in one launch. FM: C2 35.5 -> 50.9 M ex/s; C3
@@ -658,7 +664,7 @@ class FusedCTRTrainer:
     def _native_step(self, slot: InputSlot, y, mean_div: float, todo, shape, main):
         """The steady-state step — labels into the staged slot, the slot's step graph, the
         next batches copied into their slots and their plan graphs — in ONE native call
-        (ctr_step_launch: same calls, same order as the Python path below). Returns the
+        (ctr_step_launch: the Python path's calls in its order). Returns the
         loss, or None (nothing done) when this step needs the Python path: a graph not
         captured yet, a step-table re-size, or inputs that need a conversion."""
         if (self.step_table.capacity < self.step_count + 2
@@ -1019,6 +1025,8 @@ class FusedCTRTrainer:
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm_planes(b.dh2p, w1p, False, True, B, H1, H2, out=b.dh1, out_planes=b.dh1p,
                           epi=hip_ops.EPI_GRAD_MASK, aux=b.h1, scale=1.0 / (1.0 - p0))
+        b.ev_dh1 = torch.cuda.Event()
+        b.ev_dh1.record()
         # Linear(F*K,300): dX = dH1 @ W0, the MLP-input gradient the scatter needs
         self._gemm_planes(b.dh1p, w0p, False, True, B, W, H1, out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
@@ -1058,14 +1066,17 @@ class FusedCTRTrainer:
             # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2 (H1's ones column)
             self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B,
                               out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
-            if side is not None:  # from dX on
-                side.wait_event(b.ev_dx)
+            if side is not None:  # from dX on (CTR_DW0_FORK=dh1: from dH1 on, A/B)
+                side.wait_event(b.ev_dh1 if self._dw0_fork == "dh1" else b.ev_dx)
             # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X. The column sum stays here:
             # it lets seg_chunk take the CUs before dW0 does (measured at C3 with db0 moved
             # before the dX fork: dW0 and seg_chunk start together, seg_chunk 38 -> 106 us,
-            # the step +20 us)
-            hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
+            # the step +20 us; CTR_DB0_LAST=1: after dW0, A/B)
+            if not self._db0_last:
+                hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
             self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B, out=gv["mlp.0.weight"])
+            if self._db0_last:
+                hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""
