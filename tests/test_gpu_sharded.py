@@ -63,8 +63,10 @@ def test_sharded_world1_equals_fused_bitwise(cuda, kind, V, K, B):
         losses = [tr.step(xs[i], ys[i], next_x=(xs[i + 1:i + 3] if name != "fused"
                                                  else None)).item()
                   for i in range(len(xs))]
-        if name == "padded":  # the fixed-capacity step replays captured graphs at N = 1
-            assert 1 <= tr.captures <= 6 and len(tr._graphs) == tr.captures
+        if name == "padded":  # the fixed-capacity step replays captured graphs at N = 1;
+            # the capacity only grows, and the buffers / graphs of a smaller one are dropped
+            assert 1 <= tr.captures <= 6 and 1 <= len(tr._graphs) <= tr.captures
+            assert len(tr._xbufs) == 1 and all(k[2] == tr._cap for k in tr._xbufs)
         tr.check_errors()
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         st = tr.optimizer_state_dict()["state"]
