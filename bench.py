@@ -606,8 +606,18 @@ def main():
         roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": nbytes}
-        traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec",
-                                                  "flush": "deferred_flush_tile"}.get(dominant, dominant))
+        if dominant == "plan":  # the plan's launches: per pass a histogram and a scatter
+            passes = -(-max(1, (V - 1).bit_length()) // 8)
+            parts = [("radix_hist_kernel", passes), ("radix_scatter_kernel", passes),
+                     ("seg_count_kernel", 1), ("seg_write_kernel", 1)]
+            got = [(load_traffic(args.config, k), n) for k, n in parts]
+            traffic = (sum(t * n for (t, _), n in got) if all(t for (t, _), _ in got)
+                       else None)
+            src = got[0][0][1] if traffic else None
+        else:
+            traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec",
+                                                      "flush": "deferred_flush_tile"}.get(dominant,
+                                                                                          dominant))
     roofline.update({"traffic": traffic, "traffic_source": src, "avg_launch_ms": launch_ms,
                      "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each launch of this "
