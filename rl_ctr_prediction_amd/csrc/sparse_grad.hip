@@ -213,18 +213,26 @@ __global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
 }
 
 // The combine pass with the deferred Adam apply fused in (float4): a wave takes G = 64/LPR
-// consecutive unique rows. Each of the G rows that spans chunks is first summed by the
-// whole wave exactly as seg_combine_kernel sums it (same partial order, same butterfly:
-// bitwise the same sums) into a wave-private LDS slot; then every lane group applies its
-// own row — the sum from seg_chunk's `out` for a row inside one chunk, from the LDS slot
-// for a spanning one — so the G applies (the memory-heavy part) run side by side. One
-// launch for what the combine and ctr_adam_deferred_rows did in two, and the spanning
-// rows' sums never make the round trip through `out`.
+// consecutive unique rows, lane group g row u0 + g, and every lane group applies its own
+// row — the sum from seg_chunk's `out` for a row inside one chunk — so the G applies (the
+// memory-heavy part) run side by side. One launch for what the combine and
+// ctr_adam_deferred_rows did in two, and the spanning rows' sums never make the round trip
+// through `out`.
+// A spanning row's sum is seg_combine_kernel's, bit for bit: G accumulators, accumulator s
+// the running sum (from zero) of pieces s, s+G, s+2G ... in chunk order, then the pairwise
+// tree over the G accumulators in index order that the xor butterfly forms. A row of at
+// most T pieces (the common case: a few chunks) is summed that way by its own lane group,
+// every piece load in flight at once and all G rows side by side; a row of more pieces (hot
+// Zipf rows) by the whole wave — lane group g accumulator g, then the butterfly — into a
+// wave-private LDS slot, one such row after another. (The whole-wave walk over every
+// spanning row cost a dependent segment-bounds + partials round trip per row, serially.)
 template <int LPR>
 __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
   using VT = float4;
   constexpr int kChunk = seg_chunk<LPR>();
   constexpr int G = kWave / LPR;
+  // most pieces one lane group sums alone (accumulators past T stay zero, still in the tree)
+  constexpr int T = G < 8 ? 8 : (G > 16 ? 16 : G);
   __shared__ VT s_sum[4][kWave];      // [wave][row of the G * lane group column]
   __shared__ float s_lin[4][G];
   const int lane = threadIdx.x & (kWave - 1);
@@ -234,19 +242,33 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
   const int U = *a.num_unique;
   const int step = *a.step_ptr;
+  const VT* __restrict__ part = static_cast<const VT*>(a.part);
   for (int64_t u0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave) * G; u0 < U;
        u0 += waves * G) {
-    for (int j = 0; j < G && u0 + j < U; ++j) {  // rows spanning chunks: the whole wave
-      const int64_t u = u0 + j;
-      const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
-      const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
-      if (fs == ls) continue;  // wave-uniform
-      const int64_t P = ls - fs + 1;
+    const int64_t u = u0 + g;
+    const bool valid = u < U;
+    int32_t off0 = 0, off1 = 1;
+    if (valid) {
+      off0 = a.seg_offsets[u];
+      off1 = a.seg_offsets[u + 1];
+    }
+    const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
+    const int P = (int)(ls - fs + 1);  // pieces: 1 = inside one chunk
+    const int64_t k0 = fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1);  // piece 0's partial slot
+    // rows of more than T pieces: the whole wave, one row after another
+    uint64_t big = __ballot(valid && P > T && c == 0);
+    while (big) {
+      const int src = __builtin_ctzll(big);
+      big &= big - 1;
+      const int j = src / LPR;
+      const int Pj = __shfl(P, src, kWave);
+      const int64_t fsj = __shfl((int)fs, src, kWave);
+      const int64_t k0j = __shfl((int)k0, src, kWave);
       VT acc = VOps<VT>::zero();
       float accl = 0.f;
-      for (int64_t i = g; i < P; i += G) {
-        const int64_t k = i == 0 ? fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1) : (fs + i) * 2;
-        if (col) VOps<VT>::add(acc, static_cast<const VT*>(a.part)[k * a.KV + c]);
+      for (int i = g; i < Pj; i += G) {
+        const int64_t k = i == 0 ? k0j : (fsj + i) * 2;
+        if (col) VOps<VT>::add(acc, part[k * a.KV + c]);
         accl += a.part_lin[k];
       }
 #pragma unroll
@@ -255,26 +277,48 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
         accl += __shfl_xor(accl, o, kWave);
       }
       if (g == 0) {
-        if (a.out_keep) seg_emit<VT>(a, u, c, col, acc, accl);
         s_sum[wib][j * LPR + c] = acc;
         if (c == 0) s_lin[wib][j] = accl;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave-private slots are written
     __builtin_amdgcn_wave_barrier();
-    const int64_t u = u0 + g;  // every lane group applies its own row
-    if (u < U) {
-      const int32_t off0 = a.seg_offsets[u], off1 = a.seg_offsets[u + 1];
-      const bool inside = off0 / kChunk == (off1 - 1) / kChunk;
+    if (valid) {
       VT gr;
       float gl;
-      if (inside) {
+      if (P == 1) {
         gr = col ? static_cast<const VT*>(a.out)[u * a.KV + c] : VOps<VT>::zero();
         gl = a.out_lin ? a.out_lin[u] : 0.f;
+      } else if (P <= T) {
+        VT acc[G];
+        float accl[G];
+#pragma unroll
+        for (int s = 0; s < G; ++s) {
+          acc[s] = VOps<VT>::zero();
+          accl[s] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+          if (i < P) {
+            const int64_t k = i == 0 ? k0 : (fs + i) * 2;
+            if (col) VOps<VT>::add(acc[i % G], part[k * a.KV + c]);
+            accl[i % G] += a.part_lin[k];
+          }
+        }
+#pragma unroll
+        for (int w2 = 1; w2 < G; w2 <<= 1)
+#pragma unroll
+          for (int s = 0; s + w2 < G; s += 2 * w2) {
+            VOps<VT>::add(acc[s], acc[s + w2]);
+            accl[s] += accl[s + w2];
+          }
+        gr = acc[0];
+        gl = accl[0];
       } else {
         gr = s_sum[wib][g * LPR + c];
         gl = s_lin[wib][g];
       }
+      if (P > 1 && a.out_keep) seg_emit<VT>(a, u, c, col, gr, gl);
       deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV, c,
                          col, gr, gl, step, a.tab, a.hp);
     }

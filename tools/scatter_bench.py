@@ -63,6 +63,15 @@ def main():
     res["fm_only_us"] = timed(lambda: H.fm_embedding_grad(plan, F, E, gz, sum_e, None,
                                                           grad_rows=rows, grad_lin=lin), args.reps)
     res["vals_us"] = timed(lambda: H.segment_sum_rows(plan, dx, out=rows), args.reps)
+    # the fused path of the step: sums + the deferred Adam apply of the batch's rows
+    table = (E, torch.zeros_like(E), torch.zeros_like(E), torch.zeros(V, device=dev),
+             torch.zeros(V, device=dev), torch.zeros(V, device=dev),
+             torch.zeros(V, dtype=torch.int32, device=dev))
+    st = H.AdamStepTable(1e-3, (0.9, 0.999), dev)
+    step_dev = torch.ones(1, dtype=torch.int32, device=dev)
+    res["fm_dx_adam_us"] = timed(lambda: H.fm_embedding_grad_adam(
+        plan, F, gz, sum_e, dx, table, step_dev, st, 1, weight_decay=1e-5, grad_rows=rows,
+        grad_lin=lin), args.reps)
     # algorithmic bytes of the FM + dX scatter: per slot 4 index arrays (16 B) + dX row;
     # per unique row the table row read + the gradient row written (+ lin)
     alg = S * (16 + 4 * K) + U * (8 * K + 8) + B * 4 * K
