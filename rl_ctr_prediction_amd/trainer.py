@@ -92,7 +92,7 @@ class InputSlot:
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
     __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "plan_exec",
-                 "done_ev", "stream_i", "cap", "counts")
+                 "done_ev", "stream_i", "stage_stream", "cap", "counts")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -105,6 +105,7 @@ class InputSlot:
         self.plan_exec = None   # its hipGraphExec_t (ctr_step_launch launches it natively)
         self.done_ev = None     # the slot's staging event (one per slot, re-recorded)
         self.stream_i = 0
+        self.stage_stream = None  # the plan stream its last staging ran on
         self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
 
 
@@ -302,6 +303,12 @@ class FusedCTRTrainer:
         # C2 two streams 50.5 / 54.8 / 53.4 vs one 50.5 / 48.9 / 47.3 M ex/s (alternating
         # runs, tools/c2_knobs3.sh); while the host paced the step one stream measured faster
         self.n_plan_streams = int(os.environ.get("CTR_PLAN_STREAMS", "2"))
+        # which plan stream a staged batch's copy + plan run on: "seq" — alternate in staging
+        # order, so two consecutive plans never queue on one stream (with a ring of three
+        # slots, the slot-index rule put slots 0 and 2 on one stream: their plans ran back to
+        # back, two in one step and none in the next); "slot" — the slot's own stream
+        self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "slot")
+        self._stage_seq = 0
         self._extra_plan_streams: list = []
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
@@ -624,7 +631,7 @@ class FusedCTRTrainer:
         stream, concurrently with the step just enqueued (replayed from the slot's own
         plan graph once captured)."""
         s = self._acquire_slot(shape, exclude=current, ahead=True)
-        ps = self._slot_stream(s.stream_i)
+        ps = self._stage_stream(s)
         ps.wait_event(ev_start)
         # torch.cuda.set_stream on the known streams instead of the torch.cuda.stream
         # context manager (~9 us per use: it looks the current stream up again)
@@ -650,6 +657,17 @@ class FusedCTRTrainer:
             torch.cuda.set_stream(main)
         s.ev = ev
         self._staged[key] = s
+
+    def _stage_stream(self, s: InputSlot):
+        """The plan stream of the next staged batch (slot s): see _plan_stream_by. Every
+        slot owns its buffers and plan scratch, so any plan stream may serve it; the slot's
+        readers wait for its staging event, whichever stream recorded it."""
+        if self._plan_stream_by == "slot":
+            s.stage_stream = self._slot_stream(s.stream_i)
+        else:
+            s.stage_stream = self._slot_stream(self._stage_seq % max(1, self.n_plan_streams))
+            self._stage_seq += 1
+        return s.stage_stream
 
     def _slot_event(self, s: InputSlot):
         if s.done_ev is None:
@@ -695,7 +713,7 @@ class FusedCTRTrainer:
             picked.append((n, k, s))
         stages = (StageDesc * max(1, len(picked)))()
         for i, (n, _, s) in enumerate(picked):
-            ps = self._slot_stream(s.stream_i)
+            ps = self._stage_stream(s)
             ev = self._slot_event(s)
             st = stages[i]
             st.src, st.dst, st.bytes = n.data_ptr(), s.ids.data_ptr(), n.numel() * n.element_size()
@@ -707,7 +725,7 @@ class FusedCTRTrainer:
                             slot.y.data_ptr(), B * 4, exec_handle,
                             self._event_handle(start) if picked else None, stages, len(picked))
         for n, _, s in picked:
-            n.record_stream(self._slot_stream(s.stream_i))  # read there until the copy ran
+            n.record_stream(s.stage_stream)  # read there until the copy ran
             s.ev = s.done_ev
         slot.ev = None
         self._bufs.plan = slot.plan
