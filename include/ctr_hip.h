@@ -595,6 +595,102 @@ int ctr_step_launch(ctr_stream_t main_stream, void* wait_event, const void* y_sr
                     int64_t y_bytes, void* step_graph, void* start_event,
                     const ctr_stage* stages, int n_stages);
 
+/* ==== Op-level interface: one POD argument struct per torch.library op ====
+ * ctr_op_<op>(const ctr_<op>_args* a, stream) is the C form of the `ctr::<op>` PyTorch op
+ * (rl_ctr_prediction_amd/torch_ops.py) — what a binding without torch (ctypes, cgo, JNI)
+ * calls. Each composes the entry points above with the same results, bit for bit. (The
+ * `ctr_op_` prefix keeps the names apart from the flat entry points: C has no overloads.)
+ * Scratch: ctr_workspace_bytes(op, dims, n_dims) with the op's dims listed below; the op
+ * carves its plan / partials / row map out of `ws`. Outputs that the reference returns as
+ * fresh tensors (dense gradients) are caller-owned buffers the op zero-fills itself.
+ * `flags`: CTR_OPF_DETERMINISTIC (every op here is deterministic: sums in a fixed order, no
+ * float atomics; the flag is accepted and always honoured). */
+enum ctr_op {
+  CTR_OP_FM_FWD = 1,               /* dims: none                     */
+  CTR_OP_FM_BWD = 2,               /* dims: {B, F, K, V}             */
+  CTR_OP_DEEPFM_GATHER_CONCAT = 3, /* dims: none                     */
+  CTR_OP_EMB_SCATTER_ADD = 4,      /* dims: {n_slots, K, V}          */
+  CTR_OP_ADAM_DENSE = 5,           /* dims: none                     */
+  CTR_OP_ADAM_ROWWISE = 6,         /* dims: {V}                      */
+  CTR_OP_PAIRWISE_FE = 7,          /* dims: none                     */
+  CTR_OP_PG_RETURNS = 8            /* dims: {n}                      */
+};
+enum ctr_op_flags { CTR_OPF_DETERMINISTIC = 1 };
+/* Scratch bytes of op `op` for `dims` (see enum ctr_op); -1 for an unknown op or bad dims. */
+int64_t ctr_workspace_bytes(int op, const int64_t* dims, int n_dims);
+
+/* ctr::fm_fwd — FM.forward logit and the per-example embedding sums its backward needs:
+ * z[B] (the [B,1] logit), sum_e[B,K]. Replaces p_model.py:40-57. */
+typedef struct ctr_fm_fwd_args {
+  const void* idx; int idx_type; int64_t B; int F; int K; int64_t V;
+  const float* emb; const float* lin; const float* bias;
+  float* z; float* sum_e; int32_t* err_flag; int flags;
+} ctr_fm_fwd_args;
+int ctr_op_fm_fwd(const ctr_fm_fwd_args* a, ctr_stream_t stream);
+
+/* ctr::fm_bwd — FM's parameter gradients from dL/dz: dense g_emb[V,K], g_lin[V] (both
+ * zero-filled here, then the batch's rows written: embedding_dense_backward) and g_bias[1]
+ * = sum gz. Replaces autograd through p_model.py:40-57 (all_main/pretrain_main.py:77). */
+typedef struct ctr_fm_bwd_args {
+  const void* idx; int idx_type; int64_t B; int F; int K; int64_t V;
+  const float* emb; const float* sum_e; const float* gz;
+  float* g_emb; float* g_lin; float* g_bias;
+  void* ws; int64_t ws_bytes; int32_t* err_flag; int flags;
+} ctr_fm_bwd_args;
+int ctr_op_fm_bwd(const ctr_fm_bwd_args* a, ctr_stream_t stream);
+
+/* ctr::deepfm_gather_concat — out[B, F*K] = E[x] flattened (DeepFM's MLP input,
+ * p_model.py:320-321). */
+typedef struct ctr_deepfm_gather_concat_args {
+  const void* idx; int idx_type; int64_t B; int F; int K; int64_t V;
+  const float* emb; float* out; int32_t* err_flag; int flags;
+} ctr_deepfm_gather_concat_args;
+int ctr_op_deepfm_gather_concat(const ctr_deepfm_gather_concat_args* a, ctr_stream_t stream);
+
+/* ctr::emb_scatter_add — dense[V,K] (zero-filled here) = embedding_dense_backward of
+ * per-slot gradients grad_slots[n_slots, K] at ids idx[n_slots] (slot order kept per row). */
+typedef struct ctr_emb_scatter_add_args {
+  const void* idx; int idx_type; int64_t n_slots; int K; int64_t V;
+  const float* grad_slots; float* dense;
+  void* ws; int64_t ws_bytes; int32_t* err_flag; int flags;
+} ctr_emb_scatter_add_args;
+int ctr_op_emb_scatter_add(const ctr_emb_scatter_add_args* a, ctr_stream_t stream);
+
+/* ctr::adam_dense — one torch.optim.Adam step (coupled L2) of n elements at step `step`
+ * (1-based; the bias corrections are computed here in double as torch does). Replaces
+ * all_main/pretrain_main.py:78 (optimizer.step) for dense parameters. */
+typedef struct ctr_adam_dense_args {
+  float* p; const float* g; float* m; float* v; int64_t n; int64_t step;
+  double lr; double beta1; double beta2; double eps; double weight_decay; int flags;
+} ctr_adam_dense_args;
+int ctr_op_adam_dense(const ctr_adam_dense_args* a, ctr_stream_t stream);
+
+/* ctr::adam_rowwise — the same Adam step for EVERY row of emb[V,K] (dense semantics), the
+ * gradient of row rows[u] being grad_rows[u,:] and 0 for rows not listed (rows distinct). */
+typedef struct ctr_adam_rowwise_args {
+  float* emb; float* m; float* v; int64_t V; int K;
+  const void* rows; int rows_type; int64_t n_rows; const float* grad_rows; int64_t step;
+  double lr; double beta1; double beta2; double eps; double weight_decay;
+  void* ws; int64_t ws_bytes; int flags;
+} ctr_adam_rowwise_args;
+int ctr_op_adam_rowwise(const ctr_adam_rowwise_args* a, ctr_stream_t stream);
+
+/* ctr::pairwise_fe — Feature_Embedding.forward: [B, F(F-1)/2 + F*K]
+ * (Feature_embedding.py:51-59). */
+typedef struct ctr_pairwise_fe_args {
+  const void* idx; int idx_type; int64_t B; int F; int K; int64_t V;
+  const float* emb; float* out; int32_t* err_flag; int flags;
+} ctr_pairwise_fe_args;
+int ctr_op_pairwise_fe(const ctr_pairwise_fe_args* a, ctr_stream_t stream);
+
+/* ctr::pg_returns — discount_and_norm_rewards: vt (fp64) and its fp32 copy
+ * (PG_model.py:139-154). */
+typedef struct ctr_pg_returns_args {
+  const float* r; int64_t n; double gamma; double* vt; float* vt_f32;
+  void* ws; int64_t ws_bytes; int flags;
+} ctr_pg_returns_args;
+int ctr_op_pg_returns(const ctr_pg_returns_args* a, ctr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

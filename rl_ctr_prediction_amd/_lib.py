@@ -68,6 +68,62 @@ class StageDesc(C.Structure):
                 ("plan_graph", _vp), ("done_event", _vp)]
 
 
+# --- the op-level interface: mirrors of the ctr_<op>_args structs ---------
+CTR_OP_FM_FWD, CTR_OP_FM_BWD, CTR_OP_DEEPFM_GATHER_CONCAT, CTR_OP_EMB_SCATTER_ADD = 1, 2, 3, 4
+CTR_OP_ADAM_DENSE, CTR_OP_ADAM_ROWWISE, CTR_OP_PAIRWISE_FE, CTR_OP_PG_RETURNS = 5, 6, 7, 8
+CTR_OPF_DETERMINISTIC = 1
+_IDXF = [("idx", _vp), ("idx_type", _i32), ("B", _i64), ("F", _i32), ("K", _i32), ("V", _i64)]
+
+
+class FmFwdArgs(C.Structure):
+    _fields_ = _IDXF + [("emb", _vp), ("lin", _vp), ("bias", _vp), ("z", _vp), ("sum_e", _vp),
+                        ("err_flag", _vp), ("flags", _i32)]
+
+
+class FmBwdArgs(C.Structure):
+    _fields_ = _IDXF + [("emb", _vp), ("sum_e", _vp), ("gz", _vp), ("g_emb", _vp),
+                        ("g_lin", _vp), ("g_bias", _vp), ("ws", _vp), ("ws_bytes", _i64),
+                        ("err_flag", _vp), ("flags", _i32)]
+
+
+class DeepfmGatherConcatArgs(C.Structure):
+    _fields_ = _IDXF + [("emb", _vp), ("out", _vp), ("err_flag", _vp), ("flags", _i32)]
+
+
+class EmbScatterAddArgs(C.Structure):
+    _fields_ = [("idx", _vp), ("idx_type", _i32), ("n_slots", _i64), ("K", _i32), ("V", _i64),
+                ("grad_slots", _vp), ("dense", _vp), ("ws", _vp), ("ws_bytes", _i64),
+                ("err_flag", _vp), ("flags", _i32)]
+
+
+class AdamDenseArgs(C.Structure):
+    _fields_ = [("p", _vp), ("g", _vp), ("m", _vp), ("v", _vp), ("n", _i64), ("step", _i64),
+                ("lr", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
+                ("weight_decay", _f64), ("flags", _i32)]
+
+
+class AdamRowwiseArgs(C.Structure):
+    _fields_ = [("emb", _vp), ("m", _vp), ("v", _vp), ("V", _i64), ("K", _i32), ("rows", _vp),
+                ("rows_type", _i32), ("n_rows", _i64), ("grad_rows", _vp), ("step", _i64),
+                ("lr", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
+                ("weight_decay", _f64), ("ws", _vp), ("ws_bytes", _i64), ("flags", _i32)]
+
+
+class PairwiseFeArgs(C.Structure):
+    _fields_ = _IDXF + [("emb", _vp), ("out", _vp), ("err_flag", _vp), ("flags", _i32)]
+
+
+class PgReturnsArgs(C.Structure):
+    _fields_ = [("r", _vp), ("n", _i64), ("gamma", _f64), ("vt", _vp), ("vt_f32", _vp),
+                ("ws", _vp), ("ws_bytes", _i64), ("flags", _i32)]
+
+
+OP_ARGS = {"fm_fwd": FmFwdArgs, "fm_bwd": FmBwdArgs, "deepfm_gather_concat": DeepfmGatherConcatArgs,
+           "emb_scatter_add": EmbScatterAddArgs, "adam_dense": AdamDenseArgs,
+           "adam_rowwise": AdamRowwiseArgs, "pairwise_fe": PairwiseFeArgs,
+           "pg_returns": PgReturnsArgs}
+
+
 # name -> (restype, argtypes); the list is the whole ABI and tests/test_abi.py checks it
 # against the header.
 SIGNATURES = {
@@ -166,6 +222,8 @@ SIGNATURES = {
     "ctr_pg_loss_grad": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _vp, _vp, _vp, _i64, _vp]),
     "ctr_pg_vt_mean": (_i32, [_vp, _i64, _vp, _vp]),
     "ctr_pg_loss_grad_global": (_i32, [_vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp]),
+    "ctr_workspace_bytes": (_i64, [_i32, C.POINTER(_i64), _i32]),
+    **{f"ctr_op_{op}": (_i32, [C.POINTER(st), _vp]) for op, st in OP_ARGS.items()},
 }
 
 

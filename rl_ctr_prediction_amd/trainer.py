@@ -307,7 +307,7 @@ class FusedCTRTrainer:
         # order, so two consecutive plans never queue on one stream (with a ring of three
         # slots, the slot-index rule put slots 0 and 2 on one stream: their plans ran back to
         # back, two in one step and none in the next); "slot" — the slot's own stream
-        self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "slot")
+        self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "seq")
         self._stage_seq = 0
         self._extra_plan_streams: list = []
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)

@@ -1,0 +1,196 @@
+"""The op-level C interface (`ctr_op_<op>(const ctr_<op>_args*, stream)` +
+`ctr_workspace_bytes(op, dims)`, csrc/ops.hip).
+
+CPU: the ctypes mirrors have the header's exact struct layouts (a C program compiled here
+prints sizeof / offsetof), and the workspace query answers without a GPU.
+GPU: every struct-form op gives bitwise the results of its `torch.ops.ctr` twin (the same
+flat kernels composed in the same order) on seeded inputs, int64 and int32 ids."""
+from __future__ import annotations
+
+import ctypes as C
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+STRUCTS = {"ctr_fm_fwd_args": "FmFwdArgs", "ctr_fm_bwd_args": "FmBwdArgs",
+           "ctr_deepfm_gather_concat_args": "DeepfmGatherConcatArgs",
+           "ctr_emb_scatter_add_args": "EmbScatterAddArgs", "ctr_adam_dense_args": "AdamDenseArgs",
+           "ctr_adam_rowwise_args": "AdamRowwiseArgs", "ctr_pairwise_fe_args": "PairwiseFeArgs",
+           "ctr_pg_returns_args": "PgReturnsArgs"}
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="no C compiler")
+def test_struct_mirrors_match_header(tmp_path):
+    from rl_ctr_prediction_amd import _lib as L
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ctr_hip.h"', "int main(void) {"]
+    for cname, pyname in STRUCTS.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in getattr(L, pyname)._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out.splitlines()}
+    for cname, pyname in STRUCTS.items():
+        st = getattr(L, pyname)
+        assert got[(cname, "size")] == C.sizeof(st), cname
+        for f, _ in st._fields_:
+            assert got[(cname, f)] == getattr(st, f).offset, (cname, f)
+
+
+def test_workspace_bytes_query_without_gpu():
+    from rl_ctr_prediction_amd import build_lib
+    try:
+        build_lib.build()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    from rl_ctr_prediction_amd._lib import (CTR_OP_ADAM_DENSE, CTR_OP_ADAM_ROWWISE,
+                                            CTR_OP_EMB_SCATTER_ADD, CTR_OP_FM_BWD,
+                                            CTR_OP_PG_RETURNS, lib)
+
+    def q(op, *dims):
+        arr = (C.c_int64 * max(1, len(dims)))(*dims)
+        return lib.ctr_workspace_bytes(op, arr, len(dims))
+    assert q(CTR_OP_ADAM_DENSE) == 0
+    assert q(CTR_OP_FM_BWD, 4096, 26, 16, 1000) > 4096 * 26 * 16 * 4
+    assert q(CTR_OP_FM_BWD, 4096, 26) == -1  # too few dims
+    assert q(CTR_OP_EMB_SCATTER_ADD, 100, 8, 50) > 0
+    assert q(CTR_OP_ADAM_ROWWISE, 1000) >= 4000
+    assert q(CTR_OP_PG_RETURNS, 4096) > 0
+    assert q(99) == -1
+
+
+# ------------------------------------------------------------------------- GPU ----------
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _ws(op, dims, dev):
+    import torch
+    from rl_ctr_prediction_amd._lib import lib
+    arr = (C.c_int64 * max(1, len(dims)))(*dims)
+    n = lib.ctr_workspace_bytes(op, arr, len(dims))
+    assert n >= 0
+    return torch.empty(max(n, 1), dtype=torch.uint8, device=dev), n
+
+
+def _call(name, **kw):
+    import torch
+    from rl_ctr_prediction_amd._lib import OP_ARGS, lib
+    a = OP_ARGS[name](**kw)
+    getattr(lib, f"ctr_op_{name}")(C.byref(a), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idx_dtype", ["int64", "int32"])
+def test_ops_struct_form_equals_torch_ops(cuda, idx_dtype):
+    import torch
+    from rl_ctr_prediction_amd import torch_ops  # noqa: F401  (registers torch.ops.ctr)
+    from rl_ctr_prediction_amd._lib import (CTR_IDX_I32, CTR_IDX_I64, CTR_OP_ADAM_ROWWISE,
+                                            CTR_OP_EMB_SCATTER_ADD, CTR_OP_FM_BWD,
+                                            CTR_OP_PG_RETURNS, CTR_OPF_DETERMINISTIC)
+    g = torch.Generator(device=cuda).manual_seed(7)
+    B, F, K, V = 300, 26, 16, 5000
+    dt = getattr(torch, idx_dtype)
+    it = CTR_IDX_I64 if idx_dtype == "int64" else CTR_IDX_I32
+    x = torch.randint(0, V, (B, F), device=cuda, generator=g).to(dt)
+    x[:, 0] = 3  # a hot row in every example
+    emb = torch.randn(V, K, device=cuda, generator=g) * 0.1
+    lin = torch.randn(V, 1, device=cuda, generator=g) * 0.1
+    bias = torch.randn(1, device=cuda, generator=g)
+    idxf = dict(idx=_p(x), idx_type=it, B=B, F=F, K=K, V=V, flags=CTR_OPF_DETERMINISTIC)
+
+    # fm_fwd
+    z_ref, s_ref = torch.ops.ctr.fm_fwd(x, emb, lin, bias)
+    z, s = torch.empty(B, device=cuda), torch.empty(B, K, device=cuda)
+    _call("fm_fwd", emb=_p(emb), lin=_p(lin), bias=_p(bias), z=_p(z), sum_e=_p(s), **idxf)
+    assert torch.equal(z, z_ref.view(-1)) and torch.equal(s, s_ref)
+
+    # fm_bwd
+    gz = torch.randn(B, 1, device=cuda, generator=g) * 0.01
+    ge_ref, gl_ref, gb_ref = torch.ops.ctr.fm_bwd(x, emb, s_ref, gz)
+    ge, gl, gb = torch.full((V, K), 7.0, device=cuda), torch.full((V,), 7.0, device=cuda), \
+        torch.empty(1, device=cuda)
+    ws, n = _ws(CTR_OP_FM_BWD, [B, F, K, V], cuda)
+    _call("fm_bwd", emb=_p(emb), sum_e=_p(s_ref), gz=_p(gz), g_emb=_p(ge), g_lin=_p(gl),
+          g_bias=_p(gb), ws=_p(ws), ws_bytes=n, **idxf)
+    assert torch.equal(ge, ge_ref) and torch.equal(gl, gl_ref.view(-1)) and torch.equal(gb, gb_ref)
+
+    # deepfm_gather_concat
+    cat = torch.empty(B, F * K, device=cuda)
+    _call("deepfm_gather_concat", emb=_p(emb), out=_p(cat), **idxf)
+    assert torch.equal(cat, torch.ops.ctr.deepfm_gather_concat(x, emb))
+
+    # emb_scatter_add
+    gs = torch.randn(B * F, K, device=cuda, generator=g)
+    dense = torch.full((V, K), 7.0, device=cuda)
+    ws, n = _ws(CTR_OP_EMB_SCATTER_ADD, [B * F, K, V], cuda)
+    _call("emb_scatter_add", idx=_p(x), idx_type=it, n_slots=B * F, K=K, V=V, grad_slots=_p(gs),
+          dense=_p(dense), ws=_p(ws), ws_bytes=n, flags=CTR_OPF_DETERMINISTIC)
+    assert torch.equal(dense, torch.ops.ctr.emb_scatter_add(x, gs, V))
+
+    # pairwise_fe
+    fe = torch.empty(B, F * (F - 1) // 2 + F * K, device=cuda)
+    _call("pairwise_fe", emb=_p(emb), out=_p(fe), **idxf)
+    assert torch.equal(fe, torch.ops.ctr.pairwise_fe(x, emb))
+
+    # adam_dense (step 3, coupled L2)
+    hp = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-5)
+    p0 = torch.randn(1000, device=cuda, generator=g)
+    gd = torch.randn(1000, device=cuda, generator=g)
+    m0 = torch.randn(1000, device=cuda, generator=g) * 0.1
+    v0 = torch.rand(1000, device=cuda, generator=g) * 0.01
+    pr, mr, vr = p0.clone(), m0.clone(), v0.clone()
+    torch.ops.ctr.adam_dense(pr, gd, mr, vr, 3, hp["lr"], hp["beta1"], hp["beta2"], hp["eps"],
+                             hp["weight_decay"])
+    pa, ma, va = p0.clone(), m0.clone(), v0.clone()
+    _call("adam_dense", p=_p(pa), g=_p(gd), m=_p(ma), v=_p(va), n=1000, step=3, flags=0, **hp)
+    assert torch.equal(pa, pr) and torch.equal(ma, mr) and torch.equal(va, vr)
+
+    # adam_rowwise: rows distinct, every other row decays with g = wd * p
+    rows = torch.randperm(V, device=cuda, generator=g)[:200].to(dt)
+    gr = torch.randn(200, K, device=cuda, generator=g)
+    er, mr2, vr2 = emb.clone(), torch.zeros_like(emb), torch.zeros_like(emb)
+    torch.ops.ctr.adam_rowwise(er, mr2, vr2, rows, gr, 1, hp["lr"], hp["beta1"], hp["beta2"],
+                               hp["eps"], hp["weight_decay"])
+    ea, ma2, va2 = emb.clone(), torch.zeros_like(emb), torch.zeros_like(emb)
+    ws, n = _ws(CTR_OP_ADAM_ROWWISE, [V], cuda)
+    _call("adam_rowwise", emb=_p(ea), m=_p(ma2), v=_p(va2), V=V, K=K, rows=_p(rows), rows_type=it,
+          n_rows=200, grad_rows=_p(gr), step=1, ws=_p(ws), ws_bytes=n, flags=0, **hp)
+    assert torch.equal(ea, er) and torch.equal(ma2, mr2) and torch.equal(va2, vr2)
+
+    # pg_returns
+    r = torch.randn(777, device=cuda, generator=g)
+    vt_ref, vt32_ref = torch.ops.ctr.pg_returns(r, 0.95)
+    vt, vt32 = torch.empty(777, dtype=torch.float64, device=cuda), torch.empty(777, device=cuda)
+    ws, n = _ws(CTR_OP_PG_RETURNS, [777], cuda)
+    _call("pg_returns", r=_p(r), n=777, gamma=0.95, vt=_p(vt), vt_f32=_p(vt32), ws=_p(ws),
+          ws_bytes=n, flags=0)
+    assert torch.equal(vt, vt_ref) and torch.equal(vt32, vt32_ref)
+
+
+def test_ops_struct_form_errors():
+    """Contract violations come back as CTR_ERR_* with a message before any HIP call, so
+    this runs without a GPU."""
+    from rl_ctr_prediction_amd import build_lib
+    try:
+        build_lib.build()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    from rl_ctr_prediction_amd._lib import OP_ARGS, CtrHipError, lib
+    a = OP_ARGS["fm_bwd"](idx=1, idx_type=1, B=4, F=2, K=4, V=10, emb=1, sum_e=1, gz=1, g_emb=1,
+                          g_lin=1, g_bias=1, ws=None, ws_bytes=0, flags=0)
+    with pytest.raises(CtrHipError, match="workspace"):
+        lib.ctr_op_fm_bwd(C.byref(a), None)
+    b = OP_ARGS["adam_rowwise"](emb=1, m=1, v=1, V=10, K=4, rows=1, rows_type=5, n_rows=1,
+                                grad_rows=1, step=1, ws=1, ws_bytes=64, flags=0)
+    with pytest.raises(CtrHipError, match="rows_type"):
+        lib.ctr_op_adam_rowwise(C.byref(b), None)
+    with pytest.raises(CtrHipError, match="null"):
+        lib.ctr_op_fm_fwd(None, None)
