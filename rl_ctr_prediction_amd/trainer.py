@@ -245,6 +245,11 @@ class FusedCTRTrainer:
         self.native_steps = 0  # steps issued by ctr_step_launch (tests)
         self._dw0_fork = os.environ.get("CTR_DW0_FORK", "dx")
         self._db0_last = os.environ.get("CTR_DB0_LAST", "0") == "1"
+        # the weight-gradient side list: "ones" (default) — dW1 alone from the head; from dX
+        # on the column-sum pair (loss, FM bias, mlp.6) then dW0 with db0 as its ones-column
+        # output (the MLP input planes carry a ones column, as H1's do for db1); "colsum" —
+        # the column-sum pair and dW1 from the head, db0 by its own column sum before dW0
+        self._wgrad_order = os.environ.get("CTR_WGRAD_ORDER", "ones")
         # lookahead (every kind): the next batches' ids are staged and planned on the plan
         # stream, so the step graph starts with no copy and no plan branch, and catches its
         # rows up over the plan's unique rows in one launch. FM: C2 35.5 -> 50.9 M ex/s; C3
@@ -479,7 +484,9 @@ class FusedCTRTrainer:
             P = hip_ops.Planes
             # H1 carries a ones column in its padding: dW1 then returns the bias gradient
             # db1 = colsum dH2 as one more output column
-            b.xp, b.h1p = P(B, W, dev), P(B, H1, dev, ones_col=True)
+            # ... and so does the MLP input X (db0 = colsum dH1 from dW0, CTR_WGRAD_ORDER)
+            b.xp = P(B, W, dev, ones_col=self._wgrad_order == "ones")
+            b.h1p = P(B, H1, dev, ones_col=True)
             b.dh2p, b.dh1p = P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
                 b.dslot = e(S, K)
@@ -1073,6 +1080,7 @@ class FusedCTRTrainer:
         H1, H2, W = b.h1.shape[1], b.h2.shape[1], b.dx.shape[1]
         if side is not None:
             side.wait_event(b.ev_head)
+        ones = self._wgrad_order == "ones" and b.xp.ones_col
         with torch.cuda.stream(side) if side is not None else _nullctx():
             jobs = [(b.fm.loss_elem.view(B, 1), None, b.loss, 1.0 / B)]  # batch mean BCE
             if "bias" in gv:  # DeepFM's FM bias: sum gz
@@ -1080,12 +1088,21 @@ class FusedCTRTrainer:
             # Linear(200,1): dW = gz^T H2, db = sum gz
             jobs += [(b.h2, gz, gv["mlp.6.weight"].view(-1)),
                      (gz.view(B, 1), None, gv["mlp.6.bias"].view(1))]
-            hip_ops.colsum_multi(jobs)
+            if not ones:
+                hip_ops.colsum_multi(jobs)
             # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2 (H1's ones column)
             self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B,
                               out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
             if side is not None:  # from dX on (CTR_DW0_FORK=dh1: from dH1 on, A/B)
                 side.wait_event(b.ev_dh1 if self._dw0_fork == "dh1" else b.ev_dx)
+            if ones:
+                # the column-sum pair here, ahead of dW0: seg_chunk takes the CUs before dW0
+                # does (the role db0's own column sum played), and db0 = colsum dH1 comes out
+                # of dW0 as the ones column of X
+                hip_ops.colsum_multi(jobs)
+                self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
+                                  out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
+                return
             # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X. The column sum stays here:
             # it lets seg_chunk take the CUs before dW0 does (measured at C3 with db0 moved
             # before the dX fork: dW0 and seg_chunk start together, seg_chunk 38 -> 106 us,
