@@ -313,6 +313,10 @@ class FusedCTRTrainer:
         # slots, the slot-index rule put slots 0 and 2 on one stream: their plans ran back to
         # back, two in one step and none in the next); "slot" — the slot's own stream
         self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "seq")
+        # stage the next batches (ids copy + plan graph on the plan streams) before the step
+        # graph is enqueued rather than after it: the plan then starts with the step, beside
+        # the catch-up and gather, instead of ~80 us of host time later (A/B knob)
+        self._stage_first = os.environ.get("CTR_STAGE_FIRST", "0") == "1"
         self._stage_seq = 0
         self._extra_plan_streams: list = []
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
@@ -571,14 +575,18 @@ class FusedCTRTrainer:
             slot = self._acquire_slot(shape)
             slot.ids.copy_(x, non_blocking=True)
         slot.y.copy_(y.reshape(-1), non_blocking=True)
+        if self._stage_first:  # the plan streams get their work before the step graph
+            for n, k in todo:
+                self._stage_ahead(n, k, shape, slot, ev_start, main)
         if self.use_graphs and self.timing is None:
             loss = self._graph_step(slot, mean_div, have)
         else:
             self.step_table.ensure(self.step_count + 1)
             loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
             self._after_step()
-        for n, k in todo:
-            self._stage_ahead(n, k, shape, slot, ev_start, main)
+        if not self._stage_first:
+            for n, k in todo:
+                self._stage_ahead(n, k, shape, slot, ev_start, main)
         return loss
 
     def _ring(self, shape) -> list:
