@@ -23,44 +23,14 @@
 
 namespace ctr {
 
-// The replay step of an absent row (g = 0 before weight decay) on four elements, in
-// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two IEEE fp32 operations per
-// lane per instruction, each bitwise the scalar one; sqrt and rcp stay scalar). The
-// flush is VALU-bound at long replays (SQ_ACTIVE_INST_VALU ~95 % of the SIMD quad-cycles
-// at 20 replayed steps, profiles/r02_flush_pmc.txt). Measured on MI355X (tools/ab_flush.sh,
-// C3 table): 4.32 vs 4.42 ms at 20 steps, but 3.06 vs 2.64 ms at 1 step and 21.6 vs 21.5 ms
-// at the C5 shape (10 steps) — packed fp32 issues at about the scalar rate on gfx950, so the
-// scalar form stays the default (CTR_FLUSH_PK=1 selects this one).
-typedef float pf2 __attribute__((ext_vector_type(2)));
-#ifndef CTR_FLUSH_PK
-#define CTR_FLUSH_PK 0
-#endif
-
-__device__ __forceinline__ void adam_replay_pk2(pf2& p, pf2& m, pf2& v, const AdamHP& h) {
-#pragma clang fp contract(off)
-  const pf2 zero = {0.f, 0.f};
-  const pf2 g = __builtin_elementwise_fma((pf2){h.wd, h.wd}, p, zero);        // grad.add(p, wd)
-  m = __builtin_elementwise_fma((pf2){h.w1, h.w1}, g - m, m);                 // lerp_
-  v = __builtin_elementwise_fma((pf2){h.w2, h.w2} * g, g, v * (pf2){h.beta2, h.beta2});
-  const pf2 sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
-  const pf2 den = __builtin_elementwise_fma(sq, (pf2){h.inv_bc2_sqrt, h.inv_bc2_sqrt},
-                                            (pf2){h.eps, h.eps});
-  const pf2 r = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-  p = __builtin_elementwise_fma((pf2){h.neg_step_size, h.neg_step_size} * m, r, p);
-}
-
+// The replay step of an absent row (g = 0 before weight decay) on four elements. Measured
+// and rejected on MI355X (C3 table / C5 shape): an explicit packed-fp32 form (v_pk_fma_f32 /
+// v_pk_mul_f32: 4.32 vs 4.42 ms at 20 replayed steps, 3.06 vs 2.64 at 1 step — hipcc
+// SLP-packs this scalar form already), and one reciprocal per element pair (1/d0 = d1 *
+// rcp(d0*d1): the flush 33.3-34.1 ms either way at C5 — the extra multiplies cancel the saved
+// reciprocal; the replay issues ~7 VALU instructions per element-step whatever their kind).
 __device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v, const AdamHP& h) {
-#if CTR_FLUSH_PK
-  pf2 p0 = {p.x, p.y}, p1 = {p.z, p.w}, m0 = {m.x, m.y}, m1 = {m.z, m.w};
-  pf2 v0 = {v.x, v.y}, v1 = {v.z, v.w};
-  adam_replay_pk2(p0, m0, v0, h);
-  adam_replay_pk2(p1, m1, v1, h);
-  p = make_float4(p0.x, p0.y, p1.x, p1.y);
-  m = make_float4(m0.x, m0.y, m1.x, m1.y);
-  v = make_float4(v0.x, v0.y, v1.x, v1.y);
-#else
   adam_vec(p, make_float4(0.f, 0.f, 0.f, 0.f), m, v, h);
-#endif
 }
 
 // ------------------------------------------------------------------ dense -----------
