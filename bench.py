@@ -305,7 +305,9 @@ def bench_pg(args, cfg, world, rank, dev):
                                "ctr_gemm_f32_ex on the 256-128-A tail)",
                      "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS,
-                     "algorithmic_flops_per_launch": flops, "traffic": None,
+                     "algorithmic_flops_per_launch": flops,
+                     "traffic": load_traffic("c4", "gemm")[0],
+                     "traffic_source": load_traffic("c4", "gemm")[1],
                      "avg_launch_ms": launch_ms, "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each GEMM launch over "
                                "un-timed learn() calls before the timed region"},
