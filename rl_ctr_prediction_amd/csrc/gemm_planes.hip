@@ -727,6 +727,9 @@ static bool pl_ks_ok(const PlDef& d, int64_t Kp, int64_t kps) {
   return d.ks == 1 || (Kp % 64 == 0 && kps % 64 == 0);
 }
 
+#ifndef CTR_PL_DX_TILE
+#define CTR_PL_DX_TILE 19  // (A/B builds: 7, the 4-wave 64 x 64 tiling)
+#endif
 #ifndef CTR_PL_FWD0_TILE
 #define CTR_PL_FWD0_TILE 8  // (A/B builds: 30, the direct-A 128 x 80 tiling)
 #endif
@@ -762,7 +765,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   if (!a_rc && !b_rc && M >= 2048 && N > 256 && N <= 320) return mk(CTR_PL_FWD0_TILE, 1);
   if (!a_rc && !b_rc && M >= 2048 && N <= 256) return mk(17, 1);
   if (!a_rc && b_rc && M >= 2048 && N >= 1024) {
-    PlCfg c = mk(19, 1);
+    PlCfg c = mk(CTR_PL_DX_TILE, 1);
     c.xg = 2;  // dX: each XCD's half of the weight stays L2-resident
     return c;
   }
