@@ -727,8 +727,12 @@ static bool pl_ks_ok(const PlDef& d, int64_t Kp, int64_t kps) {
   return d.ks == 1 || (Kp % 64 == 0 && kps % 64 == 0);
 }
 
+// dX (dH1 . W0: M = B, N = 1664, K = 300) on the 4-wave 64 x 64 tiling, three blocks per CU:
+// in the step it runs 64.3 us (median of 93 launches, rocprofv3) against 74.8 on the 8-wave
+// tiling 19 that standalone timing had picked (70.7 vs 74.3 us alone), C3 12.51 / 12.49 /
+// 12.81 vs 12.30 / 12.44 / 12.53 M ex/s alternating (profiles/r03_dx_tiling.txt)
 #ifndef CTR_PL_DX_TILE
-#define CTR_PL_DX_TILE 19  // (A/B builds: 7, the 4-wave 64 x 64 tiling)
+#define CTR_PL_DX_TILE 7  // (A/B builds: 19, the 8-wave 64 x 64 tiling)
 #endif
 #ifndef CTR_PL_FWD0_TILE
 #define CTR_PL_FWD0_TILE 8  // (A/B builds: 30, the direct-A 128 x 80 tiling)
