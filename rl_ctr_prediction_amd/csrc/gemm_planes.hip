@@ -746,6 +746,24 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     }
     return c;
   };
+  // per-shape override for in-step A/B (tuning only): CTR_GEMM_PLANES_SHAPE_CFG =
+  // "M,N,Kp,a_rc,b_rc=tile,splits,xg;..." (Kp: the 32-padded k extent)
+  if (const char* env = getenv("CTR_GEMM_PLANES_SHAPE_CFG")) {
+    const char* q = env;
+    while (q && *q) {
+      long long m, n, k;
+      int ar, br, ti = -1, sp = 1, xg = 1, used = 0;
+      if (sscanf(q, "%lld,%lld,%lld,%d,%d=%d,%d,%d%n", &m, &n, &k, &ar, &br, &ti, &sp, &xg,
+                 &used) >= 8 && m == M && n == N && k == Kp && ar == (int)a_rc &&
+          br == (int)b_rc && ti >= 0 && ti < kNumPl && sp >= 1 && pl_valid(ti, a_rc, b_rc)) {
+        PlCfg c = mk(ti, sp);
+        c.xg = xg == 2 || xg == 4 || xg == 8 ? xg : 1;
+        if (pl_ks_ok(kPl[ti], Kp, c.kps)) return c;
+      }
+      q = strchr(q, ';');
+      if (q) ++q;
+    }
+  }
   if (const char* env = getenv("CTR_GEMM_PLANES_CFG")) {
     int ti = -1, sp = 1, xg = 1;
     if (sscanf(env, "%d,%d,%d", &ti, &sp, &xg) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
