@@ -3,8 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline]
 
 N>1 is launched by the driver as `python -m torch.distributed.run --nproc-per-node N ...`:
-one process per GPU, RCCL over xGMI, data parallel with replicated tables (weak scaling:
-every rank trains its own B-example batches; value = all ranks' examples / max time).
+one process per GPU, RCCL over xGMI, data parallel with row-sharded embedding tables
+(ShardedCTRTrainer: ids / rows / row gradients by all-to-all, dense gradients all-reduced;
+--sharding replicated keeps full replicas with a sparse all-gather). Weak scaling: every
+rank trains its own B-example batches; value = all ranks' examples / max time.
 
 Workload (default c3 = BASELINE configs[2], the north-star target shape): DeepFM, 26
 fields, 10M-id vocabulary, embed_dim 64, batch 8192 per GPU, synthetic Criteo-shape ids
@@ -79,11 +81,13 @@ def adam_bytes(V, K, U):
     return 24 * V * (K + 1) + 4 * V + U * (4 * K + 8)
 
 
-def gather_bytes(S, K, B, deep):
+def gather_bytes(S, K, B, deep, planes=True):
     """fm_forward: int64 ids (8 B/slot), the gathered row (4K B) and linear weight (4 B)
-    per slot, the per-example sums written (4K B/example), and for DeepFM the flat MLP
-    input written (4K B/slot)."""
-    return S * (8 + 4 * K + 4) + B * 4 * K + (S * 4 * K if deep else 0) + B * 16
+    per slot, the per-example sums written (4K B/example), and for DeepFM the MLP input
+    written — as its three bf16 planes (6K B/slot, fm_forward_planes: the default) or fp32
+    (4K B/slot)."""
+    x_bytes = (6 if planes else 4) * K
+    return S * (8 + 4 * K + 4) + B * 4 * K + (S * x_bytes if deep else 0) + B * 16
 
 
 def ipnn_gather_bytes(S, K, B, F):
@@ -124,10 +128,27 @@ def flush_bytes(V, K, lin=True):
     return 24 * V * K + (24 * V if lin else 0) + 8 * V
 
 
+def host_threads() -> tuple[int, str]:
+    """Every core this process may run on (torch.set_num_threads(cpu count)):
+    the CPU affinity set, capped by a cgroup CPU quota when one is set (a quota of Q cores
+    runs at most Q threads at once; more would only time-slice)."""
+    n = len(os.sched_getaffinity(0))
+    note = f"sched_getaffinity: {n} cores"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            note += f"; cgroup cpu.max quota {int(quota) / int(period):g} cores"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, note
+
+
 def cpu_baseline(cfg, batches, max_seconds=25.0):
     """The oracle (torch-CPU restatement, pinned to the reference) on this host."""
     from oracle import ctr_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, thread_note = host_threads()
     torch.set_num_threads(threads)
     t0 = time.perf_counter()
     params = O.init_params(cfg["kind"], cfg["V"], cfg["F"], cfg["K"], seed=1)
@@ -135,19 +156,21 @@ def cpu_baseline(cfg, batches, max_seconds=25.0):
     init_s = time.perf_counter() - t0
     xs = [torch.from_numpy(x) for x, _ in batches]
     ys = [torch.from_numpy(y) for _, y in batches]
-    O.train_step(cfg["kind"], params, opt, xs[0], ys[0])  # warm-up (allocates dense grads)
-    n, t = 0, 0.0
+    for i in range(2):  # warm-up (allocates the dense grads), BASELINE.md protocol
+        O.train_step(cfg["kind"], params, opt, xs[i % len(xs)], ys[i % len(ys)])
+    n, t, split = 0, 0.0, {}
     while n < 1 or (t < max_seconds and n < 10):
         s = time.perf_counter()
-        O.train_step(cfg["kind"], params, opt, xs[n % len(xs)], ys[n % len(ys)])
+        O.train_step(cfg["kind"], params, opt, xs[n % len(xs)], ys[n % len(ys)], split=split)
         t += time.perf_counter() - s
         n += 1
         if t > max_seconds / 2 and n >= 3:
             break
     eps = n * cfg["B"] / t
     return {"value": eps, "unit": "examples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"{n} timed steps (+1 warm-up) of the same workload and batches on the "
+            "cpu_model": cpu_model(), "threads_note": thread_note,
+            "split_ms_per_step": {k: v / n * 1e3 for k, v in split.items()},
+            "sample": f"{n} timed steps (+2 warm-up) of the same workload and batches on the "
                       f"host CPU, oracle/ctr_oracle.py train_step (torch-CPU ops as the "
                       f"reference: dense nn.Embedding grads, torch.optim.Adam); "
                       f"{t / n * 1e3:.0f} ms/step; param init {init_s:.1f} s untimed"}
@@ -156,7 +179,7 @@ def cpu_baseline(cfg, batches, max_seconds=25.0):
 def cpu_baseline_pg(cfg, episodes, max_seconds=25.0):
     """PolicyGradient.learn restated on torch-CPU (oracle.pg_learn) on this host."""
     from oracle import ctr_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, thread_note = host_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(1)
     V, F, K, A = cfg["V"], cfg["F"], cfg["K"], cfg["A"]
@@ -172,7 +195,7 @@ def cpu_baseline_pg(cfg, episodes, max_seconds=25.0):
         t += time.perf_counter() - s
         n += 1
     return {"value": n * cfg["B"] / t, "unit": "transitions/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "threads_note": thread_note,
             "sample": f"{n} timed learn() calls (+1 warm-up) on the same episodes, "
                       f"oracle/ctr_oracle.py pg_learn (torch-CPU: FE state, policy MLP, "
                       f"loss_func, Adam); {t / n * 1e3:.0f} ms per episode"}
@@ -400,6 +423,9 @@ def main():
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
+    ap.add_argument("--no-driver-loop", action="store_true",
+                    help="skip the driver-loop measurement (pretrain_main.run_epoch over K "
+                         "batches after the timed region)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch every step eagerly (no HIP-graph replay): the host-paced "
                          "launch path that N > 1 row sharding takes without CTR_SHARDED_GRAPHS")
@@ -469,7 +495,7 @@ def main():
         i = seq[0]
         seq[0] += 1
         nxt = [xs[(i + j) % len(xs)] for j in range(1, args.lookahead + 1)]
-        return trainer.step(xs[i % len(xs)], ys[i % len(ys)], next_x=nxt)
+        trainer.step(xs[i % len(xs)], ys[i % len(ys)], next_x=nxt, return_loss=False)
 
     for i in range(args.warmup):
         step(i)
@@ -533,6 +559,40 @@ def main():
     torch.cuda.synchronize()
     timing = trainer.timing
     trainer.timing = None
+
+    # the driver's own loop (pretrain_main.train -> run_epoch: lookahead steps, the loss
+    # summed on the device and read once), and the reference's per-step `.item()` loop for
+    # comparison, each over K batches + the flush, N = 1 (pretrain_main is one process)
+    driver = None
+    if world == 1 and not args.no_driver_loop:
+        from rl_ctr_prediction_amd.pretrain_main import run_epoch
+        base = seq[0]
+        dl = [(xs[(base + j) % len(xs)], ys[(base + j) % len(ys)]) for j in range(args.steps)]
+        trainer.flush()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mean_loss = run_epoch(trainer, dl)
+        trainer.flush()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        tot = 0.0
+        for j, (x_j, y_j) in enumerate(dl):
+            nxt = [b[0] for b in dl[j + 1:j + 3]]
+            tot += trainer.step(x_j, y_j, next_x=nxt).item()
+        trainer.flush()
+        torch.cuda.synchronize()
+        dt_item = time.perf_counter() - t0
+        driver = {"value": B * args.steps / dt, "unit": "examples/s",
+                  "ms_per_step": dt / args.steps * 1e3, "mean_loss": mean_loss,
+                  "item_per_step": {"value": B * args.steps / dt_item,
+                                    "ms_per_step": dt_item / args.steps * 1e3,
+                                    "mean_loss": tot / args.steps},
+                  "what": "pretrain_main.run_epoch (the driver's train() loop: step() with the "
+                          "next two batches' plans built ahead, each step's loss added to a "
+                          "device float64 sum, read once) over K batches + the flush; "
+                          "item_per_step: the same steps with the reference's per-step "
+                          "`total_loss += loss.item()` host sync (all_main/pretrain_main.py:79)"}
 
     U = trainer._bufs.plan.num_unique_host()
     S = B * F
@@ -659,6 +719,7 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
         "host_ms_per_step": host_s / args.steps * 1e3,  # inside step(): the enqueue cost
+        "driver_loop": driver,
         "gather_scatter": {
             "gather_kernel": g_kernel, "gather_ms": gather_ms,
             "gather_GBps": g_bytes / (gather_ms * 1e-3) / 1e9,

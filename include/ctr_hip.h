@@ -451,17 +451,24 @@ int ctr_segment_sum_rows_adam(const ctr_sparse_plan* plan, int K, const float* v
  *   finished before ctr_step_end. table_steps = entries of step_table (its capacity). */
 int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream);
 int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream);
+/* ctr_step_end_loss: ctr_step_end, and loss_sum[0] += (double)loss[0] — the driver's epoch
+ *   loss accumulated on the device (fp64, in step order: bitwise the reference's Python
+ *   `total_loss += train_loss.item()`, all_main/pretrain_main.py:79, with no host sync per
+ *   step). */
+int ctr_step_end_loss(int32_t* step_ctr, const float* loss, double* loss_sum,
+                      ctr_stream_t stream);
 /* ctr_fm_step_tail: the FM step's dense tail (one process) in one launch —
  *   loss_out[0] = loss_scale * sum(loss_elem[:B]), bias_grad[0] = sum(gz[:B]) (bitwise
  *   ctr_sum_f32), Adam on the flat dense vector (p, g, m, v)[:n] at step ctr[1] (bitwise
- *   ctr_adam_dense; bias_grad may point into g), then ctr_step_end(step_ctr).
+ *   ctr_adam_dense; bias_grad may point into g), then ctr_step_end(step_ctr); loss_sum
+ *   (may be NULL): loss_sum[0] += (double)loss_out[0], as ctr_step_end_loss.
  *   Replaces: all_main/pretrain_main.py:74-78 (loss.backward's bias gradient, the batch
  *   loss, optimizer.step() on the FM bias) at the end of a step. */
 int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t B, float loss_scale,
                      float* loss_out, float* bias_grad, float* p, const float* g, float* m,
                      float* v, int64_t n, const float* step_table, int32_t* step_ctr,
                      double beta1, double beta2, double eps, double weight_decay,
-                     ctr_stream_t stream);
+                     double* loss_sum, ctr_stream_t stream);
 int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                             float* v_lin, int64_t V, int K, int32_t* last,
                             const int32_t* step_ctr, int n_slices, const float* step_table,
@@ -666,12 +673,14 @@ typedef struct ctr_adam_dense_args {
 int ctr_op_adam_dense(const ctr_adam_dense_args* a, ctr_stream_t stream);
 
 /* ctr::adam_rowwise — the same Adam step for EVERY row of emb[V,K] (dense semantics), the
- * gradient of row rows[u] being grad_rows[u,:] and 0 for rows not listed (rows distinct). */
+ * gradient of row rows[u] being grad_rows[u,:] and 0 for rows not listed (rows distinct).
+ * A listed row outside [0, V) is not applied and raises CTR_EFLAG_INDEX in *err_flag (may
+ * be NULL: then such a row is dropped silently), as the torch op's index_copy_ raises. */
 typedef struct ctr_adam_rowwise_args {
   float* emb; float* m; float* v; int64_t V; int K;
   const void* rows; int rows_type; int64_t n_rows; const float* grad_rows; int64_t step;
   double lr; double beta1; double beta2; double eps; double weight_decay;
-  void* ws; int64_t ws_bytes; int flags;
+  void* ws; int64_t ws_bytes; int32_t* err_flag; int flags;
 } ctr_adam_rowwise_args;
 int ctr_op_adam_rowwise(const ctr_adam_rowwise_args* a, ctr_stream_t stream);
 

@@ -155,15 +155,24 @@ def make_optimizer(params: dict, lr: float, weight_decay: float):
 
 
 def train_step(kind: str, params: dict, opt, x: torch.Tensor, y: torch.Tensor,
-               drop_p: float = 0.2) -> float:
+               drop_p: float = 0.2, split: dict | None = None) -> float:
     """One reference step: forward, BCE, zero_grad, backward (dense embedding grads),
-    Adam.step, loss.item()  (all_main/pretrain_main.py:72-79)."""
+    Adam.step, loss.item()  (all_main/pretrain_main.py:72-79). split: accumulates the
+    seconds of the forward (+ BCE), backward and optimizer phases (BASELINE.md protocol)."""
+    import time
+    t0 = time.perf_counter()
     p = forward(kind, params, x, drop_p, True)
     loss = bce(p, y.reshape(-1, 1).to(p.dtype))
+    t1 = time.perf_counter()
     for t in params.values():
         t.grad = None
     loss.backward()
+    t2 = time.perf_counter()
     opt.step()
+    t3 = time.perf_counter()
+    if split is not None:
+        for k, d in (("fwd", t1 - t0), ("bwd", t2 - t1), ("adam", t3 - t2)):
+            split[k] = split.get(k, 0.0) + d
     return loss.item()
 
 

@@ -106,7 +106,8 @@ class AdamRowwiseArgs(C.Structure):
     _fields_ = [("emb", _vp), ("m", _vp), ("v", _vp), ("V", _i64), ("K", _i32), ("rows", _vp),
                 ("rows_type", _i32), ("n_rows", _i64), ("grad_rows", _vp), ("step", _i64),
                 ("lr", _f64), ("beta1", _f64), ("beta2", _f64), ("eps", _f64),
-                ("weight_decay", _f64), ("ws", _vp), ("ws_bytes", _i64), ("flags", _i32)]
+                ("weight_decay", _f64), ("ws", _vp), ("ws_bytes", _i64), ("err_flag", _vp),
+                ("flags", _i32)]
 
 
 class PairwiseFeArgs(C.Structure):
@@ -196,8 +197,9 @@ SIGNATURES = {
                                                _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_step_begin": (_i32, [_vp, _vp]),
     "ctr_step_end": (_i32, [_vp, _vp]),
+    "ctr_step_end_loss": (_i32, [_vp, _vp, _vp, _vp]),
     "ctr_fm_step_tail": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
-                                _vp, _f64, _f64, _f64, _f64, _vp]),
+                                _vp, _f64, _f64, _f64, _f64, _vp, _vp]),
     "ctr_adam_deferred_sweep": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32,
                                        _vp, _i64, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_flush": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp,

@@ -409,10 +409,14 @@ __global__ __launch_bounds__(256) void deferred_catchup_wave(
 // Within a step, ctr[0] stays at t-1 (catch-up, sweep and dropout read it) and ctr[1] = t
 // (the Adam apply reads it), so work on several streams never sees the counter move.
 __global__ void step_begin_kernel(int32_t* ctr) { ctr[1] = ctr[0] + 1; }
-__global__ void step_end_kernel(int32_t* ctr) {
+// loss_sum (optional): the driver's epoch loss, accumulated on the device in double —
+// adding the fp32 batch loss widened exactly, in step order, is bitwise the reference's
+// Python `total_loss += loss.item()` (all_main/pretrain_main.py:79)
+__global__ void step_end_kernel(int32_t* ctr, const float* loss, double* loss_sum) {
   const int32_t t = ctr[1];
   ctr[0] = t;
   ctr[1] = t + 1;  // the next step's: ctr_step_begin is then a no-op
+  if (loss_sum) loss_sum[0] += (double)loss[0];
 }
 
 // The FM step's dense tail in one launch (single process): the batch loss and the FM
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(1024) void fm_step_tail_kernel(
     const float* __restrict__ loss_elem, const float* __restrict__ gz, int64_t B,
     float loss_scale, float* __restrict__ loss_out, float* bias_grad, float* __restrict__ p,
     const float* g, float* __restrict__ m, float* __restrict__ v, int64_t n, AdamHP h,
-    const float* __restrict__ tab, int32_t* ctr) {
+    const float* __restrict__ tab, int32_t* ctr, double* loss_sum) {
   __shared__ float sh[2][16];
   const int t = threadIdx.x;
   float al = 0.f, ag = 0.f;
@@ -447,7 +451,9 @@ __global__ __launch_bounds__(1024) void fm_step_tail_kernel(
       rl += sh[0][w2];
       rg += sh[1][w2];
     }
-    loss_out[0] = rl * loss_scale;
+    const float L = rl * loss_scale;
+    loss_out[0] = L;
+    if (loss_sum) loss_sum[0] += (double)L;
     bias_grad[0] = rg * 1.0f;
   }
   __syncthreads();  // the bias gradient (an element of g) is visible to the block
@@ -1253,7 +1259,15 @@ extern "C" int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream) {
 
 extern "C" int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream) {
   CTR_REQUIRE(step_ctr, "ctr_step_end: null pointer");
-  hipLaunchKernelGGL(step_end_kernel, 1, 1, 0, as_stream(stream), step_ctr);
+  hipLaunchKernelGGL(step_end_kernel, 1, 1, 0, as_stream(stream), step_ctr, nullptr, nullptr);
+  CTR_LAUNCH_CHECK("step_end_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_step_end_loss(int32_t* step_ctr, const float* loss, double* loss_sum,
+                                 ctr_stream_t stream) {
+  CTR_REQUIRE(step_ctr && loss && loss_sum, "ctr_step_end_loss: null pointer");
+  hipLaunchKernelGGL(step_end_kernel, 1, 1, 0, as_stream(stream), step_ctr, loss, loss_sum);
   CTR_LAUNCH_CHECK("step_end_kernel");
   return CTR_OK;
 }
@@ -1263,13 +1277,14 @@ extern "C" int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t
                                 const float* g, float* m, float* v, int64_t n,
                                 const float* step_table, int32_t* step_ctr, double beta1,
                                 double beta2, double eps, double weight_decay,
-                                ctr_stream_t stream) {
+                                double* loss_sum, ctr_stream_t stream) {
   CTR_REQUIRE(loss_elem && gz && loss_out && bias_grad && step_table && step_ctr && B >= 0,
               "ctr_fm_step_tail: bad arguments");
   CTR_REQUIRE(n >= 0 && (n == 0 || (p && g && m && v)), "ctr_fm_step_tail: bad dense vector");
   const AdamHP h = make_hp(0.0, 1.0, beta1, beta2, eps, weight_decay);
   hipLaunchKernelGGL(fm_step_tail_kernel, 1, 1024, 0, as_stream(stream), loss_elem, gz, B,
-                     loss_scale, loss_out, bias_grad, p, g, m, v, n, h, step_table, step_ctr);
+                     loss_scale, loss_out, bias_grad, p, g, m, v, n, h, step_table, step_ctr,
+                     loss_sum);
   CTR_LAUNCH_CHECK("fm_step_tail_kernel");
   return CTR_OK;
 }

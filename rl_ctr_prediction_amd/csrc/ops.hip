@@ -212,10 +212,10 @@ extern "C" int ctr_op_adam_rowwise(const ctr_adam_rowwise_args* a, ctr_stream_t 
     const unsigned g = (unsigned)ceil_div(a->n_rows, 256);
     if (a->rows_type == CTR_IDX_I64)
       hipLaunchKernelGGL(rowmap_set_kernel<int64_t>, g, 256, 0, st,
-                         static_cast<const int64_t*>(a->rows), a->n_rows, a->V, rowmap, nullptr);
+                         static_cast<const int64_t*>(a->rows), a->n_rows, a->V, rowmap, a->err_flag);
     else
       hipLaunchKernelGGL(rowmap_set_kernel<int32_t>, g, 256, 0, st,
-                         static_cast<const int32_t*>(a->rows), a->n_rows, a->V, rowmap, nullptr);
+                         static_cast<const int32_t*>(a->rows), a->n_rows, a->V, rowmap, a->err_flag);
     CTR_LAUNCH_CHECK("rowmap_set_kernel");
   }
   double ss, bc2s;

@@ -421,7 +421,9 @@ __global__ __launch_bounds__(256) void shard_runs_copy_kernel(
     const VT* __restrict__ src, VT* __restrict__ dst, int64_t W, int64_t C,
     const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets) {
   const int j = blockIdx.y;
-  const int64_t cnt = counts[j], off = offsets[j];
+  // a run longer than the capacity (CTR_EFLAG_CAPACITY raised by the pack) is cut to C
+  // rows both ways: never a read past run j's padded block
+  const int64_t cnt = min<int64_t>(counts[j], C), off = offsets[j];
   const int64_t n = (PACK ? C : cnt) * W;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x) {

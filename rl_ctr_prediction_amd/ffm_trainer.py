@@ -98,6 +98,11 @@ class FusedFFMTrainer:
         self.step_done, self.step_cur = self.step_ctr[0:1], self.step_ctr[1:2]
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        # own scratch and capture stream (hip_ops.Workspace: no captured graph shares
+        # scratch with another object's launches)
+        self._scratch = hip_ops.Workspace()
+        self._capture_stream = torch.cuda.Stream(device=dev)
         self.step_count = 0
         self._dirty = False
         flush_hooks(model, self)
@@ -194,10 +199,22 @@ class FusedFFMTrainer:
         return b
 
     # ------------------------------------------------------------------------ step ----
-    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def step(self, x: torch.Tensor, y: torch.Tensor, return_loss: bool = True):
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1); returns the mean
-        BCE as the trainer's persistent 1-element loss buffer for this batch shape (valid
-        until the next step with the same shape; no host sync)."""
+        BCE as a fresh 1-element device tensor (no host sync), or None with
+        return_loss=False. Every step adds its loss to ``loss_sum`` (float64, on the device;
+        read_loss_sum / reset_loss_sum, as FusedCTRTrainer)."""
+        with self._scratch.scope():
+            loss = self._step(x, y)
+            return loss.clone() if return_loss else None
+
+    def reset_loss_sum(self) -> None:
+        self.loss_sum.zero_()
+
+    def read_loss_sum(self) -> float:
+        return float(self.loss_sum.item())
+
+    def _step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         B, F = x.shape
         if F != self.F:
             raise ValueError(f"FusedFFMTrainer: batch has {F} fields, model {self.F}")
@@ -240,7 +257,7 @@ class FusedFFMTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool):
+                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
                     self._launch(xs, ys)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1
@@ -294,5 +311,5 @@ class FusedFFMTrainer:
                            self.betas, self.eps, self.weight_decay, step_dev=self.step_cur,
                            table=self.step_table)
         hip_ops.tensor_sum(fwd["loss_elem"], scale=1.0 / B, out=b.loss)
-        hip_ops.step_end(self.step_ctr)
+        hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss

@@ -6,7 +6,9 @@ an error, never a silent fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -66,25 +68,63 @@ def _idx(t: torch.Tensor, name: str = "idx") -> tuple[torch.Tensor, int]:
 
 
 class Workspace:
-    """Grow-only scratch buffer, one per (device, stream); kernels on one stream are
-    ordered, so consecutive ops can share it. A buffer outgrown is retired, never freed:
-    HIP graphs captured earlier still hold its address."""
+    """Grow-only scratch buffers of ONE owner, one per (device, stream) inside it: kernels
+    on one stream are ordered, so consecutive ops of the owner can share a buffer. A buffer
+    outgrown is retired, never freed: HIP graphs captured earlier still hold its address.
 
-    _pool: dict = {}
-    _retired: list = []
+    Every trainer (and PolicyGradient) owns a Workspace and enters it (``with ws.scope():``)
+    around the launches it enqueues or captures, so no captured graph references scratch
+    that another object's launches also use — two objects' streams may share a HIP handle
+    (torch hands streams out of a small pool round-robin) without sharing scratch. Calls
+    made outside any scope (one-off op calls, tests) use the process-wide default owner."""
+
+    _default: "Workspace | None" = None
+    _tls = threading.local()
+
+    def __init__(self):
+        self._pool: dict = {}
+        self._retired: list = []
+
+    @contextlib.contextmanager
+    def scope(self):
+        stack = getattr(Workspace._tls, "stack", None)
+        if stack is None:
+            stack = Workspace._tls.stack = []
+        stack.append(self)
+        try:
+            yield self
+        finally:
+            stack.pop()
 
     @classmethod
-    def get(cls, nbytes: int, device: torch.device) -> torch.Tensor | None:
+    def current(cls) -> "Workspace":
+        stack = getattr(cls._tls, "stack", None)
+        if stack:
+            return stack[-1]
+        if cls._default is None:
+            cls._default = Workspace()
+        return cls._default
+
+    def buffer(self, nbytes: int, device: torch.device) -> torch.Tensor | None:
         if nbytes <= 0:
             return None
         key = (device.index, _stream())
-        buf = cls._pool.get(key)
+        buf = self._pool.get(key)
         if buf is None or buf.numel() < nbytes:
             if buf is not None:
-                cls._retired.append(buf)
+                self._retired.append(buf)
             buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-            cls._pool[key] = buf
+            self._pool[key] = buf
         return buf
+
+    def buffers(self) -> list:
+        """Every buffer this owner holds (tests: owners never share one)."""
+        return list(self._pool.values()) + list(self._retired)
+
+    @classmethod
+    def get(cls, nbytes: int, device: torch.device) -> torch.Tensor | None:
+        """Scratch of nbytes on the current stream, from the current owner."""
+        return cls.current().buffer(nbytes, device)
 
 
 def check_index_error(err_flag: torch.Tensor) -> None:
@@ -742,18 +782,29 @@ def step_begin(step_ctr: torch.Tensor) -> None:
     lib.ctr_step_begin(_p(step_ctr), _stream())
 
 
-def step_end(step_ctr: torch.Tensor) -> None:
-    """ctr[0] = ctr[1] on the device."""
-    lib.ctr_step_end(_p(step_ctr), _stream())
+def step_end(step_ctr: torch.Tensor, loss: torch.Tensor | None = None,
+             loss_sum: torch.Tensor | None = None) -> None:
+    """ctr[0] = ctr[1] on the device; with loss / loss_sum (fp32 [1] / fp64 [1]) also
+    loss_sum += loss in double (the driver's epoch loss, no host sync per step)."""
+    if loss_sum is None:
+        lib.ctr_step_end(_p(step_ctr), _stream())
+        return
+    _f32(loss, "loss")
+    if loss_sum.dtype != torch.float64 or not loss_sum.is_cuda:
+        raise TypeError("step_end: loss_sum must be a float64 device tensor")
+    lib.ctr_step_end_loss(_p(step_ctr), _p(loss), _p(loss_sum), _stream())
 
 
 def fm_step_tail(loss_elem: torch.Tensor, gz: torch.Tensor, loss_scale: float,
                  loss_out: torch.Tensor, bias_grad: torch.Tensor, p, g, m, v,
                  table: AdamStepTable, step: int, step_ctr: torch.Tensor, betas=(0.9, 0.999),
-                 eps=1e-8, weight_decay=0.0) -> None:
+                 eps=1e-8, weight_decay=0.0, loss_sum: torch.Tensor | None = None) -> None:
     """The FM step's dense tail in one launch: loss_out = loss_scale * sum(loss_elem),
     bias_grad = sum(gz) (bitwise tensor_sum), the Adam step of the flat dense vector p at
-    step ctr[1] (bitwise adam_dense), then step_end(step_ctr)."""
+    step ctr[1] (bitwise adam_dense), then step_end(step_ctr) (and loss_sum += loss_out
+    in double when given)."""
+    if loss_sum is not None and (loss_sum.dtype != torch.float64 or not loss_sum.is_cuda):
+        raise TypeError("fm_step_tail: loss_sum must be a float64 device tensor")
     for t, n in ((loss_elem, "loss_elem"), (gz, "gz"), (p, "param"), (g, "grad"),
                  (m, "exp_avg"), (v, "exp_avg_sq")):
         _f32(t, n)
@@ -766,7 +817,8 @@ def fm_step_tail(loss_elem: torch.Tensor, gz: torch.Tensor, loss_scale: float,
     lib.ctr_fm_step_tail(_p(loss_elem), _p(gz), B, float(loss_scale), _p(loss_out),
                          _p(bias_grad), _p(p), _p(g), _p(m), _p(v), p.numel(), _p(tab),
                          _p(step_ctr), float(betas[0]), float(betas[1]), float(eps),
-                         float(weight_decay), _stream())
+                         float(weight_decay), _p(loss_sum) if loss_sum is not None else None,
+                         _stream())
 
 
 def adam_deferred_sweep(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step_ctr: torch.Tensor,

@@ -151,6 +151,11 @@ class PolicyGradient:
         self.use_graphs = True
         self._graphs: dict = {}
         self._graph_pool = torch.cuda.graph_pool_handle()
+        # the learn graphs are captured on a stream of this object's own (not torch's shared
+        # default capture stream) and every launch takes scratch from its own Workspace: no
+        # captured graph shares a scratch buffer with another object's launches
+        self._scratch = hip_ops.Workspace()
+        self._capture_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self._graph_tab_version = self._step_table.version
         self._lbufs: dict = {}
         # the layers whose GEMMs run on pre-split bf16 planes (csrc/gemm_planes.hip, the
@@ -231,6 +236,10 @@ class PolicyGradient:
         return d64.cpu().numpy().reshape(-1, 1)
 
     def learn(self):
+        with self._scratch.scope():  # this object's own scratch (hip_ops.Workspace)
+            return self._learn()
+
+    def _learn(self):
         rank, ws = world()
         if ws == 1 and self.use_graphs and self._ep_states and all(
                 t.device == self._flat.device for t in self._ep_states + self._ep_as):
@@ -324,7 +333,7 @@ class PolicyGradient:
             loss = self._fused_learn(b["x"], b["a"], b["vt"])  # the real learn
             self._step += 1
             g = torch.cuda.CUDAGraph()
-            with graph_capture(g, pool=self._graph_pool):
+            with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
                 static = self._fused_learn(b["x"], b["a"], b["vt"])  # captured, not executed
             self._graphs[key] = (g, static)
             return loss

@@ -123,22 +123,40 @@ class DeviceBatches:
 
 
 def train(model, optimizer, data_loader, loss, device):
-    """One epoch (all_main/pretrain_main.py:67-83); `optimizer` is the FusedCTRTrainer."""
+    """One epoch (all_main/pretrain_main.py:67-83); `optimizer` is the fused trainer.
+
+    The reference reads every batch loss on the host (``total_loss += train_loss.item()``,
+    line 79): a full sync per step. The fused trainers add each step's loss to a float64
+    accumulator on the device inside the step's last launch, and the epoch reads it once —
+    the same fp32 values added in the same order in double: bitwise the reference's Python
+    float sum (tests/test_gpu_models.py::test_driver_epoch_loss_bitwise)."""
     model.train()
-    total_loss = 0.0
-    log_intervals = 0
     batches = list(data_loader)  # views of the device-resident data: nothing is copied
+    return run_epoch(optimizer, batches)
+
+
+def run_epoch(optimizer, batches) -> float:
+    """Mean train loss of one pass of `optimizer` over `batches` [(features, labels)] in
+    order (the body of train(); bench.py --driver-loop times it)."""
+    if not batches:
+        raise ZeroDivisionError("float division by zero")  # the reference's empty epoch
     lookahead = isinstance(optimizer, FusedCTRTrainer)
+    device_sum = hasattr(optimizer, "read_loss_sum")
+    total_loss = 0.0
+    if device_sum:
+        optimizer.reset_loss_sum()
     for i, (features, labels) in enumerate(batches):
         if lookahead:  # the next two batches' sparse plans are built during this step
             nxt = [b[0] for b in batches[i + 1:i + 3]]
-            train_loss = optimizer.step(features, labels, next_x=nxt)
-        else:
-            train_loss = optimizer.step(features, labels)
-        total_loss += train_loss.item()
-        log_intervals += 1
+            optimizer.step(features, labels, next_x=nxt, return_loss=False)
+        elif device_sum:
+            optimizer.step(features, labels, return_loss=False)
+        else:  # AutogradTrainer: the reference's per-step host read
+            total_loss += optimizer.step(features, labels).item()
+    if device_sum:
+        total_loss = optimizer.read_loss_sum()
     optimizer.check_errors()
-    return total_loss / log_intervals
+    return total_loss / len(batches)
 
 
 def _predict(model, data_loader, loss):

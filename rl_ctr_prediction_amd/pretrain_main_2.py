@@ -34,13 +34,9 @@ def train(model, optimizer, train_data, loss, device, len_train, batch):
     device once)."""
     model.train()
     data = train_data.to(device)
-    total_loss, log_intervals = 0.0, 0
-    for i in range(0, len_train, batch):
-        features, labels = data[i:i + batch, 1:], data[i:i + batch, 0]
-        total_loss += optimizer.step(features, labels.float()).item()
-        log_intervals += 1
-    optimizer.check_errors()
-    return total_loss / log_intervals
+    batches = [(data[i:i + batch, 1:], data[i:i + batch, 0].float())
+               for i in range(0, len_train, batch)]
+    return _pm.run_epoch(optimizer, batches)  # the loss summed on the device, read once
 
 
 def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, learning_rate,

@@ -88,9 +88,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     target), never the whole table. The model may be built on the host (the reference's own
     init: ``get_model(...)`` then ``.to(device)``, all_main/pretrain_main.py:137), so a
     vocabulary larger than one GPU is never materialised on any device.
-    ``model.state_dict()`` (every rank together: it gathers) and gather_tables() assemble
-    the full tables; the sharded model's own forward needs them and refuses to run on a
-    shard (N > 1)."""
+    ``model.state_dict()`` is local (no collective): this rank's rows of the tables and the
+    replicated dense parameters, so ``if rank == 0: torch.save(model.state_dict())`` never
+    blocks, and every rank resumes from its own file with ``model.load_state_dict`` (a
+    full-size table in the loaded dict is cut to the rank's rows). full_state_dict() and
+    gather_tables() — collectives, every rank calls them — assemble the full tables; the
+    sharded model's own forward needs them and refuses to run on a shard (N > 1)."""
 
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None,
@@ -174,17 +177,20 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                    "tables; assemble them with trainer.gather_tables() (or "
                                    "model.state_dict() on every rank) for inference")
 
-            def full_tables(module, state_dict, prefix, local_metadata):
+            def load_rows(state_dict, prefix, local_metadata, strict, missing, unexpected,
+                          errors):
+                """A full-size table in the loaded dict (a checkpoint of the unsharded model
+                or of full_state_dict()) is cut to this rank's rows; a shard-size one (this
+                rank's own model.state_dict()) loads as it is."""
                 t = ref()
                 if t is None:
-                    return state_dict
-                E_full, w_full = t.gather_tables()
-                state_dict[prefix + "feature_embedding.weight"] = E_full
-                if w_full is not None:
-                    state_dict[prefix + "linear.weight"] = w_full.view(-1, 1)
-                return state_dict
+                    return
+                for name in ("feature_embedding.weight", "linear.weight"):
+                    v = state_dict.get(prefix + name)
+                    if v is not None and v.dim() >= 1 and v.shape[0] == t._V_full != t.V_tab:
+                        state_dict[prefix + name] = v[t.row_lo:t.row_hi]
             model.register_forward_pre_hook(no_forward)
-            model._register_state_dict_hook(full_tables)
+            model._register_load_state_dict_pre_hook(load_rows)
 
     def _vocab_size(self, E) -> int:
         return self._V_full
@@ -211,16 +217,30 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         return lo, min(lo + self.shard_rows, self.V)
 
     def optimizer_state_dict(self) -> dict:
+        """The shard's moments (the spare row is internal): only the table parameters'
+        entries are trimmed, picked by name — a dense parameter whose length happens to be
+        V_tab + 1 keeps every element."""
         st = super().optimizer_state_dict()
-        for s in st["state"].values():  # the shard's rows (the spare row is internal)
-            for k in ("exp_avg", "exp_avg_sq"):
-                if s[k].dim() >= 1 and s[k].shape[0] == self.V_tab + 1:
+        names = [n for n, _ in self.model.named_parameters()]
+        for i, s in st["state"].items():
+            if names[i] in ("feature_embedding.weight", "linear.weight"):
+                for k in ("exp_avg", "exp_avg_sq"):
                     s[k] = s[k][:self.V_tab]
         return st
 
+    def full_state_dict(self, device=None) -> dict:
+        """model.state_dict() with the full tables assembled from every rank's shard — a
+        collective: EVERY rank calls it (device="cpu" for a table larger than one GPU)."""
+        sd = self.model.state_dict()
+        E_full, w_full = self.gather_tables(device=device)
+        sd["feature_embedding.weight"] = E_full
+        if w_full is not None:
+            sd["linear.weight"] = w_full.view(-1, 1)
+        return sd
+
     # ------------------------------------------------------------------ the step ------
-    def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-             next_x=None) -> torch.Tensor:
+    def _step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
+              next_x=None) -> torch.Tensor:
         """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches are
         staged and their plans and per-owner run maxima built on the plan stream during this
         step. Purely local (the capacity agreement is made when a batch's step comes), so
@@ -421,7 +441,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("adam", t)
         self._adam_dense(step_hint)
         self._join_sweep()
-        hip_ops.step_end(self.step_ctr)
+        hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss
 
     def _sharded_fwd_bwd(self, ids, y, b, T, T_lin, bias, mean_div, F):
@@ -563,7 +583,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._dirty = True
         self._adam_dense(self.step_count)
         self._join_sweep()
-        hip_ops.step_end(self.step_ctr)
+        hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         for n in ahead:  # the next batches' plans and counts, concurrent with this step
             k = self._xkey(n)
             if k in self._pending:

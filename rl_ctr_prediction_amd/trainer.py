@@ -277,6 +277,9 @@ class FusedCTRTrainer:
         # share scratch while running concurrently (the step graphs are captured on the
         # trainer's own capture stream for the same reason, not on torch's global one)
         self._own_streams: list = []
+        # scratch owned by this trainer alone: its captured graphs reference no buffer that
+        # another object's launches use (hip_ops.Workspace)
+        self._scratch = hip_ops.Workspace()
         self._capture_stream = self._new_stream()
         self._side = self._new_stream() if self.deferred and self._vec_ok else None
         # the weight-gradient work shares the plan's side stream (it starts after the head,
@@ -324,6 +327,8 @@ class FusedCTRTrainer:
         if self.deferred:  # nothing may read a table with rows still owed steps
             flush_hooks(model, self)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # every step's mean loss added in float64 by its last launch (the driver's epoch sum)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.step_count = 0
         self._bufs: _Bufs | None = None
         self._bufsets: dict = {}
@@ -506,9 +511,10 @@ class FusedCTRTrainer:
 
     # ------------------------------------------------------------------------ step ----
     def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-             next_x=None) -> torch.Tensor:
+             next_x=None, return_loss: bool = True) -> torch.Tensor | None:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
-        batch's mean BCE as a 1-element device tensor (no host sync).
+        batch's mean BCE as a fresh 1-element device tensor (no host sync), or None with
+        return_loss=False (no copy launch; the loss still goes into ``loss_sum``).
 
         Single process: x and y are copied into a fixed input slot of their shape
         (InputSlot; one D2D copy of the ids and labels) and the slot's step graph — the
@@ -528,9 +534,27 @@ class FusedCTRTrainer:
         before this call: its contents must stay valid until this call's work has run; a
         step with other ids builds its plan as usual.
 
-        The returned tensor is the trainer's persistent loss buffer for this batch shape
-        (a captured HIP graph writes it in place): it is valid until the next step() with
-        the same shape. Keep a value with ``loss.item()`` or ``loss.clone()``."""
+        Every step also adds its loss (fp64) to the device accumulator ``loss_sum`` inside
+        the step's last launch — the driver's epoch loss without a host sync per step
+        (read_loss_sum / reset_loss_sum)."""
+        with self._scratch.scope():  # this trainer's own scratch (hip_ops.Workspace)
+            loss = self._step(x, y, global_batch, next_x)
+            return loss.clone() if return_loss else None
+
+    def reset_loss_sum(self) -> None:
+        """Zero the device loss accumulator (on the current stream, in step order)."""
+        self.loss_sum.zero_()
+
+    def read_loss_sum(self) -> float:
+        """The sum of every step's mean loss since reset_loss_sum(), accumulated on the
+        device in float64 in step order: bitwise the reference's per-step
+        ``total_loss += loss.item()`` (all_main/pretrain_main.py:79). Syncs once."""
+        return float(self.loss_sum.item())
+
+    def _step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
+              next_x=None) -> torch.Tensor:
+        """step() without the copy of the loss: returns the persistent loss buffer of the
+        batch shape (the captured graph writes it in place)."""
         B, F = x.shape
         rank, ws = world()
         mean_div = float(global_batch if global_batch is not None else B * ws)
@@ -957,7 +981,7 @@ class FusedCTRTrainer:
             hip_ops.fm_step_tail(b.fm.loss_elem, gz, 1.0 / B, b.loss, gv["bias"].view(1),
                                  self.flat, self.flat_grad, self.m_flat, self.v_flat,
                                  self.step_table, step_hint, self.step_ctr, self.betas,
-                                 self.eps, self.weight_decay)
+                                 self.eps, self.weight_decay, loss_sum=self.loss_sum)
             self._span("adam", t)
             return b.loss
         wg = self._wgrad_stream if ws == 1 else None
@@ -967,7 +991,7 @@ class FusedCTRTrainer:
             self._adam_dense(step_hint)
         self._join_wgrad()
         self._join_sweep()
-        hip_ops.step_end(self.step_ctr)
+        hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss
 
     def _adam_dense(self, step_hint: int) -> None:

@@ -119,8 +119,21 @@ def _rank_main(rank, world, port, kind, V, F, K, B, steps, q, drop=0.0, exchange
             nxt = [d[0] for d in data[i + 1:i + 3]] if rank == 1 else None
             losses.append(tr.step(xs, ys, next_x=nxt).item())
         E, w = tr.gather_tables()
-        sd = m.state_dict()  # every rank: the full tables are gathered into it
+        sd = tr.full_state_dict()  # every rank: the full tables are gathered into it
         assert torch.equal(sd["feature_embedding.weight"], E)
+        # model.state_dict() is local (no collective): rank 0 alone may save it, and every
+        # rank resumes from its own dict or from the full one (cut to its rows)
+        local = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        assert local["feature_embedding.weight"].shape[0] == rows
+        if rank == 0:
+            import io
+            torch.save(m.state_dict(), io.BytesIO())
+        dist.barrier()
+        m.load_state_dict(local)
+        m.load_state_dict(sd)
+        after = m.state_dict()
+        for k in local:
+            assert torch.equal(after[k], local[k]), k
         Ec, wc = tr.gather_tables(device="cpu")  # shard by shard, into host memory
         assert torch.equal(Ec, E.cpu())
         if w is not None:
