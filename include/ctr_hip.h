@@ -547,6 +547,13 @@ int ctr_ffm_keys(const void* idx, int idx_type, int64_t B, int F, int64_t V, int
 int ctr_ipnn_forward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
                      const float* emb, float* cat, int64_t ldc, int32_t* err_flag,
                      ctr_stream_t stream);
+/* ctr_ipnn_forward_planes: ctr_ipnn_forward writing cat as its three bf16 planes (the
+ *   split-bf16 MLP GEMMs' operand) — cat itself may then be NULL (no fp32 copy, no split
+ *   pass); with both, both are written. */
+int ctr_ipnn_forward_planes(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
+                            const float* emb, float* cat, int64_t ldc,
+                            const ctr_planes* cat_planes, int32_t* err_flag,
+                            ctr_stream_t stream);
 int ctr_ipnn_backward(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
                       const float* emb, const float* dcat, int64_t ldd, float* dslot,
                       ctr_stream_t stream);

@@ -217,6 +217,8 @@ SIGNATURES = {
     "ctr_csv_to_bin": (_i32, [C.c_char_p, C.c_char_p, _vp, _vp, _vp]),
     "ctr_bin_info": (_i32, [C.c_char_p, _vp, _vp, _vp, _vp]),
     "ctr_ipnn_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "ctr_ipnn_forward_planes": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _i64,
+                                       _planes_p, _vp, _vp]),
     "ctr_ipnn_backward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _i64, _vp, _vp]),
     "ctr_softmax_rows": (_i32, [_vp, _i64, _i32, _vp, _vp]),
     "ctr_pg_workspace_bytes": (_i64, [_i64]),

@@ -25,12 +25,17 @@ __device__ __forceinline__ int pair_index(int i, int j, int F) {
   return i * (2 * F - i - 1) / 2 + (j - i - 1);
 }
 
+// xpl (optional): the MLP input written as its three bf16 planes (the split-bf16 GEMMs'
+// operand, csrc/gemm_planes.hip) — flat part from the staged tile, pair part as computed —
+// so no fp32 copy of cat and no split pass; cat may then be NULL.
 template <typename IdxT>
 __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restrict__ idx,
                                                            int64_t B, int F, int K, int64_t V,
                                                            const float* __restrict__ emb,
                                                            float* __restrict__ cat, int64_t ldc,
-                                                           int32_t* err) {
+                                                           int32_t* err,
+                                                           uint16_t* __restrict__ xpl,
+                                                           int64_t xpl_ld, int64_t xpl_ps) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x / kWave;
   const int lane = threadIdx.x & (kWave - 1);
@@ -38,12 +43,12 @@ __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restric
   if (b >= B) return;  // wave-uniform; the tile is wave-private (no block barrier)
   const int ld = K + 1;
   float* tile = lds + (int64_t)wave * F * ld;
-  float* ob = cat + b * ldc;
+  float* ob = cat ? cat + b * ldc : nullptr;
   stage_rows_wave(idx, b, F, K, V, emb, tile, ld, ob, err, lane);
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores are done
   __builtin_amdgcn_wave_barrier();
   const int P = F * (F - 1) / 2;
-  float* op = ob + (int64_t)F * K;
+  uint16_t* xb = xpl ? xpl + b * xpl_ld : nullptr;
   // lane -> pairs p = lane, lane + 64, ...; (i, j) walked incrementally
   int i = 0, rem = lane;
   for (int p = lane; p < P; p += kWave) {
@@ -59,8 +64,31 @@ __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restric
 #pragma clang fp contract(off)
       for (int k = 0; k < K; ++k) acc += ei[k] * ej[k];  // torch.mul, then torch.sum
     }
-    op[p] = acc;
+    if (ob) ob[(int64_t)F * K + p] = acc;
+    if (xb) {
+      uint16_t h3[3];
+      psplit1(acc, h3);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) xb[q * xpl_ps + (int64_t)F * K + p] = h3[q];
+    }
     rem += kWave;
+  }
+  if (xb) {  // the flat part's planes (columns 0 .. F*K), 4 consecutive elements per lane
+    if ((K & 3) == 0 && (xpl_ld & 3) == 0) {
+      for (int t = 4 * lane; t < F * K; t += 4 * kWave) {
+        const int f = t / K, k = t - f * K;
+        const float* r = tile + f * ld + k;
+        store_planes4_at(xb + t, xpl_ps, make_float4(r[0], r[1], r[2], r[3]));
+      }
+    } else {
+      for (int t = lane; t < F * K; t += kWave) {
+        const int f = t / K, k = t - f * K;
+        uint16_t h3[3];
+        psplit1(tile[f * ld + k], h3);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xb[q * xpl_ps + t] = h3[q];
+      }
+    }
   }
 }
 
@@ -106,9 +134,90 @@ __global__ __launch_bounds__(256) void ipnn_backward_kernel(const IdxT* __restri
   }
 }
 
+// The backward with the example's rows held in registers (lane = column k; FMAX >= F
+// fields, KC columns per lane): ONE walk over the pairs in row-major order, each pair's
+// dcat read once (an LDS broadcast) and applied to both its fields,
+//   g_i += dp(i,j) * e_j,  g_j += dp(i,j) * e_i.
+// For a field f the pairs (j, f), j < f, come before (f, j), j > f, in that walk, so g_f
+// receives its terms in ascending j — the same operations in the same order as
+// ipnn_backward_kernel (bitwise equal; tests/test_gpu_kernels.py), with one LDS read per
+// pair instead of two per term, and no row staging in LDS.
+template <typename IdxT, int FMAX, int KC>
+__global__ __launch_bounds__(256) void ipnn_backward_reg(const IdxT* __restrict__ idx,
+                                                         int64_t B, int F, int K, int64_t V,
+                                                         const float* __restrict__ emb,
+                                                         const float* __restrict__ dcat,
+                                                         int64_t ldd,
+                                                         float* __restrict__ dslot) {
+#pragma clang fp contract(off)  // torch.mul, then the index_put accumulation: rounded apart
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
+  if (b >= B) return;  // wave-uniform; the LDS slice is wave-private
+  const int P = F * (F - 1) / 2;
+  float* dp = lds + (int64_t)wave * (FMAX * (FMAX - 1) / 2);
+  const float* db = dcat + b * ldd;
+  for (int p = lane; p < P; p += kWave) dp[p] = db[(int64_t)F * K + p];
+  const long long my_row = lane < F ? (long long)load_row(idx, b * F + lane, V, (int32_t*)nullptr)
+                                    : 0ll;
+  float e[FMAX][KC], g[FMAX][KC];
+#pragma unroll
+  for (int j = 0; j < FMAX; ++j) {
+    const long long row = __shfl(my_row, j < F ? j : 0, kWave);
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int k = lane + kWave * c;
+      const bool ok = j < F && k < K;
+      e[j][c] = ok ? emb[(int64_t)row * K + k] : 0.f;
+      g[j][c] = ok ? db[(int64_t)j * K + k] : 0.f;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's dp stores are done
+  __builtin_amdgcn_wave_barrier();
+  int p = 0;
+#pragma unroll
+  for (int i = 0; i < FMAX - 1; ++i) {
+#pragma unroll
+    for (int j = i + 1; j < FMAX; ++j) {
+      if (j < F) {  // wave-uniform
+        const float d = dp[p++];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          g[i][c] += d * e[j][c];
+          g[j][c] += d * e[i][c];
+        }
+      }
+    }
+  }
+  float* out = dslot + b * (int64_t)F * K;
+#pragma unroll
+  for (int f = 0; f < FMAX; ++f)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int k = lane + kWave * c;
+      if (f < F && k < K) out[(int64_t)f * K + k] = g[f][c];
+    }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
+
+// CTR_IPNN_BWD=lds selects the LDS-tile kernel (A/B runs); default: the register kernel
+// where F <= 32 and K <= 64 (one column per lane; wider rows take the LDS-tile kernel)
+template <typename IdxT>
+static bool launch_ipnn_backward_reg(const IdxT* idx, int64_t B, int F, int K, int64_t V,
+                                     const float* emb, const float* dcat, int64_t ldd,
+                                     float* dslot, hipStream_t st) {
+  const char* env = getenv("CTR_IPNN_BWD");
+  if ((env && env[0] == 'l') || F > 32 || K > 64) return false;
+  constexpr int FM = 32;
+  hipLaunchKernelGGL((ipnn_backward_reg<IdxT, FM, 1>), (unsigned)ceil_div(B, 4), 256,
+                     4 * (FM * (FM - 1) / 2) * sizeof(float), st, idx, B, F, K, V, emb, dcat,
+                     ldd, dslot);
+  return true;
+}
 
 static int ipnn_check(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
                       size_t per_wave_floats) {
@@ -119,26 +228,45 @@ static int ipnn_check(const void* idx, int idx_type, int64_t B, int F, int K, in
   return CTR_OK;
 }
 
-extern "C" int ctr_ipnn_forward(const void* idx, int idx_type, int64_t B, int F, int K,
-                                int64_t V, const float* emb, float* cat, int64_t ldc,
-                                int32_t* err_flag, ctr_stream_t stream) {
+extern "C" int ctr_ipnn_forward_planes(const void* idx, int idx_type, int64_t B, int F, int K,
+                                       int64_t V, const float* emb, float* cat, int64_t ldc,
+                                       const ctr_planes* cat_planes, int32_t* err_flag,
+                                       ctr_stream_t stream) {
   const size_t per_wave = (size_t)F * (K + 1);
   int rc = ipnn_check(idx, idx_type, B, F, K, V, per_wave);
   if (rc != CTR_OK) return rc;
-  CTR_REQUIRE(emb && cat && ldc >= (int64_t)F * K + F * (F - 1) / 2,
+  const int64_t W = (int64_t)F * K + F * (F - 1) / 2;
+  CTR_REQUIRE(emb && (cat || cat_planes) && (!cat || ldc >= W),
               "ctr_ipnn_forward: bad output");
+  CTR_REQUIRE(!cat_planes || (cat_planes->data && cat_planes->rows >= B && cat_planes->cols >= W &&
+                              cat_planes->ld >= W && (uintptr_t)cat_planes->data % 8 == 0 &&
+                              cat_planes->plane_stride >= cat_planes->rows * cat_planes->ld),
+              "ctr_ipnn_forward_planes: planes smaller than cat [B, %lld]", (long long)W);
   if (B == 0) return CTR_OK;
+  uint16_t* xpl = cat_planes ? static_cast<uint16_t*>(cat_planes->data) : nullptr;
+  const int64_t xld = cat_planes ? cat_planes->ld : 0;
+  const int64_t xps = cat_planes ? cat_planes->plane_stride : 0;
   const size_t lds = 4 * per_wave * sizeof(float);
   const unsigned grid = (unsigned)ceil_div(B, 4);
   hipStream_t st = as_stream(stream);
   if (idx_type == CTR_IDX_I64)
     hipLaunchKernelGGL(ipnn_forward_kernel<int64_t>, grid, 256, lds, st,
-                       static_cast<const int64_t*>(idx), B, F, K, V, emb, cat, ldc, err_flag);
+                       static_cast<const int64_t*>(idx), B, F, K, V, emb, cat, ldc, err_flag,
+                       xpl, xld, xps);
   else
     hipLaunchKernelGGL(ipnn_forward_kernel<int32_t>, grid, 256, lds, st,
-                       static_cast<const int32_t*>(idx), B, F, K, V, emb, cat, ldc, err_flag);
+                       static_cast<const int32_t*>(idx), B, F, K, V, emb, cat, ldc, err_flag,
+                       xpl, xld, xps);
   CTR_LAUNCH_CHECK("ctr_ipnn_forward");
   return CTR_OK;
+}
+
+extern "C" int ctr_ipnn_forward(const void* idx, int idx_type, int64_t B, int F, int K,
+                                int64_t V, const float* emb, float* cat, int64_t ldc,
+                                int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(cat, "ctr_ipnn_forward: null output");
+  return ctr_ipnn_forward_planes(idx, idx_type, B, F, K, V, emb, cat, ldc, nullptr, err_flag,
+                                 stream);
 }
 
 extern "C" int ctr_ipnn_backward(const void* idx, int idx_type, int64_t B, int F, int K,
@@ -153,12 +281,19 @@ extern "C" int ctr_ipnn_backward(const void* idx, int idx_type, int64_t B, int F
   const size_t lds = 4 * per_wave * sizeof(float);
   const unsigned grid = (unsigned)ceil_div(B, 4);
   hipStream_t st = as_stream(stream);
-  if (idx_type == CTR_IDX_I64)
-    hipLaunchKernelGGL(ipnn_backward_kernel<int64_t>, grid, 256, lds, st,
-                       static_cast<const int64_t*>(idx), B, F, K, V, emb, dcat, ldd, dslot);
-  else
-    hipLaunchKernelGGL(ipnn_backward_kernel<int32_t>, grid, 256, lds, st,
-                       static_cast<const int32_t*>(idx), B, F, K, V, emb, dcat, ldd, dslot);
+  const bool reg = idx_type == CTR_IDX_I64
+      ? launch_ipnn_backward_reg(static_cast<const int64_t*>(idx), B, F, K, V, emb, dcat, ldd,
+                                 dslot, st)
+      : launch_ipnn_backward_reg(static_cast<const int32_t*>(idx), B, F, K, V, emb, dcat, ldd,
+                                 dslot, st);
+  if (!reg) {
+    if (idx_type == CTR_IDX_I64)
+      hipLaunchKernelGGL(ipnn_backward_kernel<int64_t>, grid, 256, lds, st,
+                         static_cast<const int64_t*>(idx), B, F, K, V, emb, dcat, ldd, dslot);
+    else
+      hipLaunchKernelGGL(ipnn_backward_kernel<int32_t>, grid, 256, lds, st,
+                         static_cast<const int32_t*>(idx), B, F, K, V, emb, dcat, ldd, dslot);
+  }
   CTR_LAUNCH_CHECK("ctr_ipnn_backward");
   return CTR_OK;
 }

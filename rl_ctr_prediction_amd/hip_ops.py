@@ -865,14 +865,23 @@ def feature_embedding(idx: torch.Tensor, emb: torch.Tensor, err_flag=None,
 
 
 def ipnn_forward(idx: torch.Tensor, emb: torch.Tensor, out: torch.Tensor | None = None,
-                 err_flag=None) -> torch.Tensor:
+                 err_flag=None, planes: "Planes | None" = None) -> torch.Tensor | None:
     """InnerPNN MLP input [B, F*K + F(F-1)/2]: flat embeddings, then the pairwise inner
-    products in row-major pair order (p_model.py:187-195)."""
+    products in row-major pair order (p_model.py:187-195). planes: also (or, with
+    out=None, only) written as its three bf16 planes — the MLP GEMMs' operand, no split
+    pass; returns out (None when only the planes are written)."""
     idx, it = _idx(idx)
     _f32(emb, "feature_embedding.weight")
     B, F = idx.shape
     V, K = emb.shape
     W = F * K + F * (F - 1) // 2
+    if planes is not None:
+        if planes.rows < B or planes.cols < W:
+            raise ValueError(f"ipnn_forward: planes [{planes.rows}, {planes.cols}] < [{B}, {W}]")
+        lib.ctr_ipnn_forward_planes(_p(idx), it, B, F, K, V, _p(emb), _p(out),
+                                    out.stride(0) if out is not None else 0, planes.desc,
+                                    _p(err_flag), _stream())
+        return out
     if out is None:
         out = torch.empty(B, W, dtype=torch.float32, device=emb.device)
     elif out.dtype != torch.float32 or out.shape[0] < B or out.shape[1] < W or out.stride(1) != 1:

@@ -479,7 +479,7 @@ class FusedCTRTrainer:
         deep = self.kind in _MLP_KINDS
         W = F * K + (F * (F - 1) // 2 if self.kind == "IPNN" else 0)  # MLP input width
         # DeepFM writes its MLP input straight as planes (b.xp): no fp32 copy of X
-        x_fp32 = deep and not (self.kind == "DeepFM" and hip_ops.fm_forward_planes_ok(K, F))
+        x_fp32 = deep and not (self.kind == "IPNN" or hip_ops.fm_forward_planes_ok(K, F))
         fm = hip_ops.FMForward(z=e(B), sum_e=e(B, K), emb_out=e(B, W) if x_fp32 else None,
                                p=None, loss_elem=e(B), gz=e(B))
         S = B * F
@@ -1051,8 +1051,8 @@ class FusedCTRTrainer:
         off1 = rank * B * H1
         off2 = ws * B * H1 + rank * B * H2
         t = self._mark("gather")
-        if self.kind == "IPNN":  # cat = flat(E[x]) ++ pairwise inner products
-            X = hip_ops.ipnn_forward(x, E, out=b.fm.emb_out, err_flag=self.err)
+        if self.kind == "IPNN":  # cat = flat(E[x]) ++ pairwise inner products, as planes
+            X = hip_ops.ipnn_forward(x, E, out=None, err_flag=self.err, planes=b.xp)
             z_fm = b.zero
         elif b.fm.emb_out is None:  # gather + FM, the MLP input written as its planes
             hip_ops.fm_forward_planes(x, E, w, bias, b.xp, b.fm.z, b.fm.sum_e, err_flag=self.err)

@@ -382,6 +382,34 @@ def test_ipnn_forward_and_backward_vs_oracle(cuda, F, K, B):
     assert ((ds - e.grad).abs() <= 1e-5 * bound + 1e-30).all()
 
 
+@pytest.mark.parametrize("F,K,B", [(2, 1, 3), (8, 16, 64), (26, 64, 300), (5, 3, 7),
+                                   (32, 64, 33), (33, 8, 9), (22, 128, 50)])
+def test_ipnn_planes_and_register_backward_bitwise(cuda, F, K, B, monkeypatch):
+    """ipnn_forward writing the MLP input's planes directly == split_planes of the fp32
+    forward, bit for bit (with and without the fp32 copy); the register backward (F <= 32,
+    K <= 64) == the LDS-tile backward (CTR_IPNN_BWD=lds), bit for bit."""
+    H = _hip()
+    g = torch.Generator().manual_seed(F + 7 * K + B)
+    V = 500
+    E = torch.randn(V, K, generator=g).to(cuda)
+    x = torch.randint(0, V, (B, F), generator=g).to(cuda)
+    W = F * K + F * (F - 1) // 2
+    cat = H.ipnn_forward(x, E)
+    want = H.split_planes(cat)
+    for keep in (False, True):
+        pl = H.Planes(B, W, cuda)
+        out = torch.empty_like(cat) if keep else None
+        H.ipnn_forward(x, E, out=out, planes=pl)
+        assert torch.equal(pl.t, want.t)
+        if keep:
+            assert torch.equal(out, cat)
+    dcat = torch.randn(B, W, generator=g).to(cuda)
+    reg = H.ipnn_backward(x, E, dcat)
+    monkeypatch.setenv("CTR_IPNN_BWD", "lds")
+    lds = H.ipnn_backward(x, E, dcat)
+    assert torch.equal(reg, lds)
+
+
 # ------------------------------------------------------------------------ REINFORCE ---
 def test_pg_discount_norm_vs_golden(cuda, golden):
     H = _hip()
