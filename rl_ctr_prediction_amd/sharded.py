@@ -9,8 +9,9 @@ per step:
   1. sparse plan of the local batch (global ids), built on the plan stream (ahead of the
      step with next_x); its unique rows are ascending, hence grouped by owner;
   2. the exchange capacity C: the largest per-owner run over every rank's batch (one
-     all-reduce MAX of a scalar on the plan stream, read by the host: the step's only host
-     read, and with next_x a read of work finished long before); the capacity in use only
+     all-reduce MAX of a scalar on a capacity stream that waits for the batch's plan only,
+     read by the host: the step's only host read, which never waits for the main stream's
+     queued steps — with next_x the plan finished long before); the capacity in use only
      grows — past a batch that exceeds it, to that run + 1/32, rounded up to 1024 rows — so
      after the first few steps every batch fits one capacity (one set of buffers, one
      graph per input slot);
@@ -136,6 +137,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                  "(dist.new_group is collective over the whole world)")
             self._count_group = dist.new_group()
         self._ahead_counts: dict = {}
+        self._cap_stream = None  # the capacity agreement's stream (_agree_capacity)
+        self.cap_reads = 0
         self._xbufs: dict = {}
         self._cap = 0  # the exchange capacity in use (rows per (requester, owner) pair)
         # graph replay of the fixed-capacity step: at one process always (no collective), at
@@ -281,14 +284,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             finally:
                 torch.cuda.set_stream(main)
         slot.y.copy_(y.reshape(-1), non_blocking=True)
-        # the capacity: every rank's largest run, agreed on the plan stream (host waits there)
+        # the capacity: every rank's largest run, agreed on a stream of its own that waits for
+        # this slot's plan only (built one or two steps ahead with next_x) — never for the
+        # main stream — so the host's read waits for the all-reduce alone while the GPU still
+        # runs the steps already enqueued
         t = self._mark("plan")
-        with torch.cuda.stream(ps):
-            if ws > 1:
-                dist.all_reduce(slot.cap, op=dist.ReduceOp.MAX, group=self._count_group)
-            cmax = int(slot.cap.item())
-            ev_plan = torch.cuda.Event()
-            ev_plan.record(ps)
+        cmax = self._agree_capacity(slot)
         self._span("plan", t)
         if cmax > self._cap:  # grows only (every rank sees the same cmax: the same C)
             grown = cmax + cmax // 32  # headroom: a later, slightly larger batch still fits
@@ -299,7 +300,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 self._xbufs = {k: v for k, v in self._xbufs.items() if k[2] == C}
             self._cap = C
         C = self._cap
-        main.wait_event(ev_plan)
+        main.wait_event(slot.ev)  # the slot's ids copy, plan and per-owner runs
         if self.use_graphs and self._graph_ok and self.timing is None:
             loss = self._sharded_graph_step(slot, mean_div, C)
         else:
@@ -319,6 +320,26 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 torch.cuda.set_stream(main)
             self._staged[k] = s
         return loss
+
+    def _agree_capacity(self, slot: InputSlot) -> int:
+        """The largest per-owner run of this step's batches over every rank (an all-reduce
+        MAX over the count group), read by the host. On the capacity stream: it waits for
+        the slot's plan event only, so the read never waits for the main stream's work (the
+        previous steps), and the all-reduce result travels to pinned host memory."""
+        if self._cap_stream is None:
+            self._cap_stream = self._new_stream()
+            self._cap_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._cap_ev = torch.cuda.Event()
+        cs = self._cap_stream
+        cs.wait_event(slot.ev)
+        with torch.cuda.stream(cs):
+            if self.world_size > 1:
+                dist.all_reduce(slot.cap, op=dist.ReduceOp.MAX, group=self._count_group)
+            self._cap_host.copy_(slot.cap, non_blocking=True)
+            self._cap_ev.record(cs)
+        self._cap_ev.synchronize()
+        self.cap_reads += 1
+        return int(self._cap_host[0])
 
     def _slot_stream(self, stream_i: int):
         return self._plan_stream  # every slot is copied and planned on the one plan stream
