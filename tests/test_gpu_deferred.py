@@ -251,27 +251,35 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
                 assert torch.equal(st[i][k], out[0][2][i][k]), (i, k)
 
 
-@pytest.mark.parametrize("K", [64, 16, 8, 128, 10])
-def test_flush_variants_bitwise(cuda, K, monkeypatch):
-    """The software-pipelined flush (CTR_FLUSH_PIPE=1 / 2) == the single-buffered tile
-    kernel, bitwise, on rows of mixed staleness (current, 1 step, up to the full region)
-    and a table whose row count is not a multiple of 64."""
+@pytest.mark.parametrize("K,V,T,lin", [(64, 100_003, 23, True), (16, 100_003, 23, True),
+                                       (8, 100_003, 23, True), (128, 100_003, 23, True),
+                                       (10, 100_003, 23, True), (64, 37, 5, True),
+                                       (32, 70_001, 300, False), (256, 4_099, 9, True)])
+def test_flush_variants_bitwise(cuda, K, V, T, lin, monkeypatch):
+    """The LDS-DMA flush (the default for K % 4 == 0, 16 <= K <= 256) and the
+    software-pipelined register flush (CTR_FLUSH_PIPE=1 / 2) == the single-buffered tile
+    kernel (CTR_FLUSH_DMA=0), bitwise, on rows of mixed staleness (current, 1 step, up to
+    the full region), a row count that is not a multiple of 64 (and one below 64), steps
+    older than any LDS window (T = 300) and a table without linear weights."""
     from rl_ctr_prediction_amd import hip_ops as H
-    V, T = 100_003, 23
-    g = torch.Generator(device=cuda).manual_seed(K)
+    g = torch.Generator(device=cuda).manual_seed(K + V)
     E0 = torch.randn(V, K, device=cuda, generator=g) * 0.05
     m0 = torch.randn(V, K, device=cuda, generator=g) * 1e-4
     v0 = torch.rand(V, K, device=cuda, generator=g) * 1e-8
     w0 = torch.randn(V, device=cuda, generator=g) * 0.05
     last0 = torch.randint(0, T + 1, (V,), device=cuda, generator=g, dtype=torch.int32)
-    last0[:640] = T  # whole tiles already current
+    last0[:min(640, V // 2)] = T  # whole tiles already current
     tab = H.AdamStepTable(1e-3, (0.9, 0.999), cuda)
     out = []
-    for variant in ("0", "1", "2"):
-        monkeypatch.setenv("CTR_FLUSH_PIPE", variant)
+    for dma, pipe in (("0", "0"), ("1", "0"), ("1", "1"), ("1", "2")):
+        monkeypatch.setenv("CTR_FLUSH_DMA", dma)
+        monkeypatch.setenv("CTR_FLUSH_PIPE", pipe)
         E, m, v, w = E0.clone(), m0.clone(), v0.clone(), w0.clone()
         mw, vw, last = torch.zeros_like(w), torch.zeros_like(w), last0.clone()
-        H.adam_deferred_flush(E, m, v, w, mw, vw, last, T, tab, weight_decay=1e-5)
+        if lin:
+            H.adam_deferred_flush(E, m, v, w, mw, vw, last, T, tab, weight_decay=1e-5)
+        else:
+            H.adam_deferred_flush(E, m, v, None, None, None, last, T, tab, weight_decay=1e-5)
         out.append((E, m, v, w, mw, vw, last))
     for o in out[1:]:
         for a, b in zip(out[0], o):
