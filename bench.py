@@ -415,8 +415,6 @@ def main():
     ap.add_argument("--sharding", default="auto", choices=["auto", "rows", "replicated"],
                     help="N>1: row-sharded tables with all-to-all (auto) or replicated tables "
                          "with a sparse all-gather")
-    ap.add_argument("--sweep-slices", type=int, default=0,
-                    help="deferred mode: background sweep of 1/N of the rows per step (0 = off)")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="sparse plans built this many batches ahead, concurrently with the "
                          "step (FusedCTRTrainer next_x); 0 = every plan in its own step")
@@ -480,7 +478,6 @@ def main():
     else:
         trainer = FusedCTRTrainer(model, lr=1e-3, weight_decay=1e-5, seed=1234,
                                   optimizer_mode=args.optimizer)
-    trainer.sweep_slices = args.sweep_slices
     if args.no_graphs:
         trainer.use_graphs = False
     if args.flush_every is not None:
@@ -508,7 +505,7 @@ def main():
 
     # breakdown pass (NOT timed): every kernel group bracketed by HIP events, to find the
     # dominant kernel and report the per-kernel table
-    keys = ("adam", "catchup", "gather", "plan", "scatter", "flush", "gemm", "exchange", "sweep")
+    keys = ("adam", "catchup", "gather", "plan", "scatter", "flush", "gemm", "exchange")
     trainer.flush()
     trainer.timing = {k: [] for k in keys}
     for i in range(n_bd):
@@ -618,7 +615,6 @@ def main():
         "sparse plan (radix sort + scan)": {"ms_per_step": per_step["plan"]},
         "scatter (fm_embedding_grad segmented sums)": {"ms_per_step": per_step["scatter"]},
         "exchange (RCCL collectives + row gathers, N>1)": {"ms_per_step": per_step["exchange"]},
-        "sweep (deferred_sweep_vec, background stream)": {"ms_per_step": per_step["sweep"]},
     }
     spans = timing[dominant]
     launch_ms = avg_ms(spans)

@@ -393,23 +393,6 @@ int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_emb, float*
                                   const int32_t* step_ptr, const float* step_table, double beta1,
                                   double beta2, double eps, double weight_decay,
                                   ctr_stream_t stream);
-/* Catch-up AHEAD of the next batch (FusedCTRTrainer.step(next_x=...)): while the current
- * batch's step runs, the next batch's rows that the current batch does NOT touch are
- * brought to *step_ptr (the step in flight: it gives them g = wd*p, which it would) — those
- * rows are disjoint from everything the current step reads or writes, so the two run
- * concurrently, and the next step needs no catch-up. `tag` is a caller-owned int32[V]
- * scratch (no initialisation), `tag_value` a negative value never passed before with this
- * tag array (the current batch's rows are tagged with it and skipped). Needs K % 4 == 0 and
- * (K/4) | 64.
- * Replaces: part of optimizer.step (all_main/pretrain_main.py:78) for the rows of the
- * next batch, moved ahead in time (deferred-exact: same arithmetic, same order per row). */
-int ctr_adam_deferred_catchup_ahead(float* emb, float* m_emb, float* v_emb, float* lin,
-                                    float* m_lin, float* v_lin, int64_t V, int K, int32_t* last,
-                                    const void* idx_cur, int idx_type_cur, int64_t S_cur,
-                                    const void* idx_next, int idx_type_next, int64_t S_next,
-                                    int32_t* tag, int32_t tag_value, const int32_t* step_ptr,
-                                    const float* step_table, double beta1, double beta2,
-                                    double eps, double weight_decay, ctr_stream_t stream);
 /* Fused scatter + deferred Adam (ws == 1, deferred mode): the segmented row sums of
  * ctr_fm_embedding_grad / ctr_segment_sum_rows with ctr_adam_deferred_rows(the sums,
  * step = *step_ptr) folded into the pass that finishes the rows spanning several chunks —
@@ -444,11 +427,7 @@ int ctr_segment_sum_rows_adam(const ctr_sparse_plan* plan, int K, const float* v
  * ctr_step_begin: ctr[1] = ctr[0] + 1;  ctr_step_end: ctr[0] = ctr[1], ctr[1] += 1. A
  * counter initialised to {0, 1} therefore needs no ctr_step_begin (one launch less per
  * step); within a step both values are constant, so kernels on several streams can read
- * them: the catch-up, the sweep and the dropout stream read ctr[0], the Adam apply ctr[1].
- * ctr_adam_deferred_sweep: bring rows [s*ceil(V/n), (s+1)*ceil(V/n)), s = ctr[0] % n_slices,
- *   up to step ctr[0] — a background share of the flush, run concurrently with a step
- *   after its catch-up (it skips the batch's rows, which are current to ctr[0]) and
- *   finished before ctr_step_end. table_steps = entries of step_table (its capacity). */
+ * them: the catch-up and the dropout stream read ctr[0], the Adam apply ctr[1]. */
 int ctr_step_begin(int32_t* step_ctr, ctr_stream_t stream);
 int ctr_step_end(int32_t* step_ctr, ctr_stream_t stream);
 /* ctr_step_end_loss: ctr_step_end, and loss_sum[0] += (double)loss[0] — the driver's epoch
@@ -469,11 +448,6 @@ int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t B, float l
                      float* v, int64_t n, const float* step_table, int32_t* step_ctr,
                      double beta1, double beta2, double eps, double weight_decay,
                      double* loss_sum, ctr_stream_t stream);
-int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
-                            float* v_lin, int64_t V, int K, int32_t* last,
-                            const int32_t* step_ctr, int n_slices, const float* step_table,
-                            int64_t table_steps, double beta1, double beta2, double eps,
-                            double weight_decay, ctr_stream_t stream);
 
 /* ------------------------------------------------ A7: Feature_Embedding -------------
  * out[b] = [ <E[x_bi],E[x_bj]> for i<j in row-major pair order ] ++ flat(E[x_b]),
@@ -584,30 +558,6 @@ int ctr_pg_loss_grad_global(const float* probs, const int64_t* acts, int64_t B, 
                             const float* vt_mean, float grad_scale, float* loss_out,
                             float* dlogits, ctr_stream_t stream);
 
-/* ---- step launch (host-side sequence of one single-process training step) ------------
- * Replaces the host side of the reference's per-batch loop body (all_main/pretrain_main.py:
- * 71-78: forward, loss, backward and optimizer.step issued once per batch) once that body is
- * a captured HIP graph per input slot: in ONE call,
- *   1. if n_stages > 0: record start_event on main_stream (everything enqueued before this
- *      step — the last readers of the slots the stages overwrite);
- *   2. if wait_event: main_stream waits for it (the slot's ids staged and planned ahead);
- *   3. copy y_bytes from y_src to y_dst on main_stream (the batch's labels into the slot);
- *   4. launch step_graph (a hipGraphExec_t) on main_stream;
- *   5. for each stage: its stream waits for start_event, `bytes` are copied src -> dst on it
- *      (the next batch's ids into its slot), plan_graph (its sparse plan build, or NULL) is
- *      launched there and done_event recorded after.
- * Device-to-device copies only; events, streams and graph execs are the caller's. */
-typedef struct ctr_stage {
-  const void* src;
-  void* dst;
-  int64_t bytes;
-  ctr_stream_t stream;
-  void* plan_graph; /* hipGraphExec_t or NULL */
-  void* done_event; /* hipEvent_t */
-} ctr_stage;
-int ctr_step_launch(ctr_stream_t main_stream, void* wait_event, const void* y_src, void* y_dst,
-                    int64_t y_bytes, void* step_graph, void* start_event,
-                    const ctr_stage* stages, int n_stages);
 
 /* ==== Op-level interface: one POD argument struct per torch.library op ====
  * ctr_op_<op>(const ctr_<op>_args* a, stream) is the C form of the `ctr::<op>` PyTorch op

@@ -62,12 +62,6 @@ class PlaneViewDesc(C.Structure):
     _fields_ = [("offset", _i64), ("rows", _i64), ("cols", _i64), ("planes", PlanesDesc)]
 
 
-class StageDesc(C.Structure):
-    """Mirror of ``ctr_stage`` (include/ctr_hip.h)."""
-    _fields_ = [("src", _vp), ("dst", _vp), ("bytes", _i64), ("stream", _vp),
-                ("plan_graph", _vp), ("done_event", _vp)]
-
-
 # --- the op-level interface (SURVEY.md §8b): mirrors of the ctr_<op>_args structs ---------
 CTR_OP_FM_FWD, CTR_OP_FM_BWD, CTR_OP_DEEPFM_GATHER_CONCAT, CTR_OP_EMB_SCATTER_ADD = 1, 2, 3, 4
 CTR_OP_ADAM_DENSE, CTR_OP_ADAM_ROWWISE, CTR_OP_PAIRWISE_FE, CTR_OP_PG_RETURNS = 5, 6, 7, 8
@@ -171,7 +165,6 @@ SIGNATURES = {
     "ctr_ids_add": (_i32, [_vp, _i64, _i32, _vp]),
     "ctr_shard_pack_ids": (_i32, [_plan_p, _i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "ctr_shard_runs_copy": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _vp]),
-    "ctr_step_launch": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, C.POINTER(StageDesc), _i32]),
     "ctr_segment_workspace_bytes": (_i64, [_i64, _i32]),
     "ctr_fm_embedding_grad": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _i64, _vp]),
@@ -192,16 +185,11 @@ SIGNATURES = {
     "ctr_adam_deferred_catchup_ids": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
                                              _i32, _i64, _vp, _vp, _vp, _f64, _f64, _f64, _f64,
                                              _vp]),
-    "ctr_adam_deferred_catchup_ahead": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp,
-                                               _vp, _i32, _i64, _vp, _i32, _i64, _vp, _i32, _vp,
-                                               _vp, _f64, _f64, _f64, _f64, _vp]),
     "ctr_step_begin": (_i32, [_vp, _vp]),
     "ctr_step_end": (_i32, [_vp, _vp]),
     "ctr_step_end_loss": (_i32, [_vp, _vp, _vp, _vp]),
     "ctr_fm_step_tail": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                 _vp, _f64, _f64, _f64, _f64, _vp, _vp]),
-    "ctr_adam_deferred_sweep": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32,
-                                       _vp, _i64, _f64, _f64, _f64, _f64, _vp]),
     "ctr_adam_deferred_flush": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp,
                                        _f64, _f64, _f64, _f64, _vp]),
     "ctr_feature_embedding_forward": (_i32, [_vp, _i32, _i64, _i32, _i32, _i64, _vp, _vp, _vp,

@@ -22,7 +22,7 @@ LIB = PKG / "libctr_hip.so"
 ARCH = os.environ.get("CTR_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["abi.cpp", "fm_forward.hip", "sparse_plan.hip", "sparse_grad.hip", "adam.hip",
-           "gemm.hip", "gemm_sb16.hip", "gemm_planes.hip", "reduce_pg.hip", "pnn.hip", "io.cpp", "runner.cpp", "ensemble.hip", "ffm.hip",
+           "gemm.hip", "gemm_sb16.hip", "gemm_planes.hip", "reduce_pg.hip", "pnn.hip", "io.cpp", "ensemble.hip", "ffm.hip",
            "layout.hip", "ops.hip"]
 INCLUDE_DIRS = [CSRC, ROOT / "include"]
 

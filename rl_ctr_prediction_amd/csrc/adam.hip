@@ -254,71 +254,6 @@ __global__ __launch_bounds__(256) void deferred_mark_kernel(const IdxT* __restri
     owner[load_row(idx, s, V, nullptr)] = (int32_t)s;
 }
 
-// Catch-up AHEAD (ctr_adam_deferred_catchup_ahead): the next batch's rows that the current
-// batch does not touch, brought to the current step while it runs. `tag` (int32[V], caller
-// scratch, no initialisation) first gets a per-call negative value at the current batch's
-// rows, then every next-batch slot whose row does not carry it stores its index there (one
-// survives, as in deferred_mark_kernel); the surviving slot replays the row. Slot indices are
-// >= 0 and the tag value < 0, so rows of the current batch are never replayed here (they get
-// their gradient at this step), and stale tags of earlier calls never match.
-template <typename IdxT>
-__global__ __launch_bounds__(256) void deferred_tag_kernel(const IdxT* __restrict__ idx,
-                                                           int64_t S, int64_t V,
-                                                           int32_t* __restrict__ tag,
-                                                           int32_t value) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
-       s += (int64_t)gridDim.x * blockDim.x)
-    tag[load_row(idx, s, V, nullptr)] = value;
-}
-
-template <typename IdxT>
-__global__ __launch_bounds__(256) void deferred_mark_excl_kernel(const IdxT* __restrict__ idx,
-                                                                 int64_t S, int64_t V,
-                                                                 int32_t* __restrict__ tag,
-                                                                 int32_t exclude) {
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = load_row(idx, s, V, nullptr);
-    if (tag[r] != exclude) tag[r] = (int32_t)s;
-  }
-}
-
-template <typename IdxT, int K4>
-__global__ __launch_bounds__(256) void deferred_catchup_ids_vec(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
-    int32_t* __restrict__ last, const IdxT* __restrict__ idx, int64_t S, int64_t V,
-    const int32_t* __restrict__ owner, const int32_t* __restrict__ step_ptr,
-    const float* __restrict__ tab, AdamHP h) {
-  const int c = threadIdx.x % K4;
-  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
-  const int step = *step_ptr;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t s = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; s < S; s += groups) {
-    const int64_t r = load_row(idx, s, V, nullptr);
-    if (owner[r] != (int32_t)s) continue;
-    const int from = last[r];
-    if (from >= step) continue;
-    const int64_t e = r * K4 + c;
-    float4 pp = E[e], mm = mE[e], vv = vE[e];
-    const bool own_lin = w && c == 0;
-    float pw = 0.f, mws = 0.f, vws = 0.f;
-    if (own_lin) {
-      pw = w[r]; mws = mw[r]; vws = vw[r];
-    }
-    for (int t = from + 1; t <= step; ++t) {
-      load_step(h, tab, t);
-      adam_vec(pp, z4, mm, vv, h);
-      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
-    }
-    E[e] = pp; mE[e] = mm; vE[e] = vv;
-    if (own_lin) {
-      w[r] = pw; mw[r] = mws; vw[r] = vws;
-    }
-    if (c == 0) last[r] = step;
-  }
-}
-
 // The same catch-up with one LANE per slot for the ownership / staleness test and the
 // replay done by lane groups over a compacted per-wave list: the test for all 64 slots of a
 // wave issues together (idx -> owner -> last, three dependent loads for 64 slots at once
@@ -406,7 +341,7 @@ __global__ __launch_bounds__(256) void deferred_catchup_wave(
 }
 
 // Device step counters of a trainer: ctr[0] = completed steps, ctr[1] = the step in flight.
-// Within a step, ctr[0] stays at t-1 (catch-up, sweep and dropout read it) and ctr[1] = t
+// Within a step, ctr[0] stays at t-1 (catch-up and dropout read it) and ctr[1] = t
 // (the Adam apply reads it), so work on several streams never sees the counter move.
 __global__ void step_begin_kernel(int32_t* ctr) { ctr[1] = ctr[0] + 1; }
 // loss_sum (optional): the driver's epoch loss, accumulated on the device in double —
@@ -469,62 +404,6 @@ __global__ __launch_bounds__(1024) void fm_step_tail_kernel(
     const int32_t s = ctr[1];
     ctr[0] = s;
     ctr[1] = s + 1;
-  }
-}
-
-// Background sweep (deferred Adam): bring one slice of the rows — slice ctr[0] % n_slices —
-// up to the completed step ctr[0], while a training step runs on other streams. Rows of the
-// step's own batch are current to ctr[0] after its catch-up (from >= target: skipped), so
-// the sweep never touches a row the step reads or updates. Lane 0 of a row's lane group
-// also owns the row's linear weight. The per-step scalars are staged in LDS (lds_steps
-// entries; larger targets read them from global memory).
-template <int K4>
-__global__ __launch_bounds__(256) void deferred_sweep_vec(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
-    int32_t* __restrict__ last, const int32_t* __restrict__ ctr, int n_slices, int lds_steps,
-    const float* __restrict__ tab, AdamHP h) {
-  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
-  const int target = ctr[0];
-  const bool use_lds = target < lds_steps;
-  if (use_lds) {
-    for (int i = threadIdx.x; i <= target; i += blockDim.x)
-      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
-    __syncthreads();
-  }
-  if (target <= 0) return;
-  const int64_t per = (V + n_slices - 1) / n_slices;
-  const int64_t lo = (int64_t)(target % n_slices) * per;
-  const int64_t hi = min(V, lo + per);
-  const int c = threadIdx.x % K4;
-  const bool own_lin = w && c == 0;
-  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t r = lo + (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; r < hi; r += groups) {
-    const int from = last[r];
-    if (from >= target) continue;
-    const int64_t e = r * K4 + c;
-    float4 pp = E[e], mm = mE[e], vv = vE[e];
-    float pw = 0.f, mws = 0.f, vws = 0.f;
-    if (own_lin) {
-      pw = w[r]; mws = mw[r]; vws = vw[r];
-    }
-    for (int s = from + 1; s <= target; ++s) {
-      if (use_lds) {
-        const float2 t = s_tab[s];
-        h.neg_step_size = t.x;
-        h.inv_bc2_sqrt = t.y;
-      } else {
-        load_step(h, tab, s);
-      }
-      adam_vec(pp, z4, mm, vv, h);
-      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
-    }
-    E[e] = pp; mE[e] = mm; vE[e] = vv;
-    if (own_lin) {
-      w[r] = pw; mw[r] = mws; vw[r] = vws;
-    }
-    if (c == 0) last[r] = target;
   }
 }
 
@@ -625,93 +504,6 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
   }
 }
 
-// The background sweep, tiled like deferred_flush_tile: slice ctr[0] % n_slices of the rows
-// (slices of whole 64-row tiles) brought to the completed step ctr[0] (read on the device:
-// the sweep is a node of the captured step graph, forked after the catch-up so it never
-// touches the step's rows — those are current to ctr[0] and skipped). Every step sweeps one
-// slice, so no row is ever more than n_slices steps behind and no separate flush pass is
-// needed; the replay (VALU) runs beside the step's GEMMs (matrix pipe) on a bounded grid.
-template <int K4, int UNR>
-__global__ __launch_bounds__(256) void deferred_sweep_tile(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
-    int32_t* __restrict__ last, const int32_t* __restrict__ ctr, int n_slices, int lds_steps,
-    const float* __restrict__ tab, AdamHP h) {
-  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
-  const int step = ctr[0];
-  const bool use_lds = step < lds_steps;
-  if (use_lds) {
-    for (int i = threadIdx.x; i <= step; i += blockDim.x)
-      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
-    __syncthreads();
-  }
-  if (step <= 0) return;
-  constexpr int RPI = kWave / K4;
-  constexpr int ITERS = K4;
-  static_assert(ITERS % UNR == 0, "batches of UNR instructions");
-  const int64_t n_tiles_all = (V + kWave - 1) / kWave;
-  const int64_t per = (n_tiles_all + n_slices - 1) / n_slices;  // tiles per slice
-  const int64_t t_lo = (int64_t)(step % n_slices) * per;
-  const int64_t t_hi = min(n_tiles_all, t_lo + per);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int c = lane % K4, r_in = lane / K4;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-  auto set_step = [&](int t) {
-    if (use_lds) {
-      const float2 v = s_tab[t];
-      h.neg_step_size = v.x;
-      h.inv_bc2_sqrt = v.y;
-    } else {
-      load_step(h, tab, t);
-    }
-  };
-  for (int64_t tile = t_lo + (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-       tile < t_hi; tile += waves) {
-    const int64_t base = tile * kWave;
-    const int64_t my = base + lane;
-    const bool ok = my < V;
-    const int from_l = ok ? last[my] : step;
-    if (__all(from_l >= step)) continue;
-    if (w && from_l < step) {
-      float pp = w[my], mm = mw[my], vv = vw[my];
-      for (int s = from_l + 1; s <= step; ++s) {
-        set_step(s);
-        adam_elem(pp, 0.f, mm, vv, h);
-      }
-      w[my] = pp; mw[my] = mm; vw[my] = vv;
-    }
-#pragma unroll 1
-    for (int it0 = 0; it0 < ITERS; it0 += UNR) {
-      float4 pp[UNR], mm[UNR], vv[UNR];
-      int from[UNR];
-      int64_t e[UNR];
-      int f0 = step;
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int r = (it0 + u) * RPI + r_in;
-        from[u] = __shfl(from_l, r, kWave);
-        e[u] = (base + r) * K4 + c;
-        f0 = min(f0, from[u]);
-        if (from[u] < step) {
-          pp[u] = E[e[u]]; mm[u] = mE[e[u]]; vv[u] = vE[e[u]];
-        }
-      }
-      for (int s = f0 + 1; s <= step; ++s) {
-        set_step(s);
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-          if (s > from[u]) adam_replay_vec(pp[u], mm[u], vv[u], h);
-      }
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        if (from[u] < step) {
-          E[e[u]] = pp[u]; mE[e[u]] = mm[u]; vE[e[u]] = vv[u];
-        }
-    }
-    if (from_l < step) last[my] = step;
-  }
-}
-
 // The tiled flush with its loads on LDS-DMA, one batch ahead (CTR_FLUSH_DMA, default):
 // a wave walks its items — (64-row tile, batch of UNR wave-instructions of float4 columns)
 // — and for each: waits for that item's DMA, moves it LDS -> registers, issues the NEXT
@@ -719,10 +511,9 @@ __global__ __launch_bounds__(256) void deferred_sweep_tile(
 // and stores it. So every wave keeps its next batch's 3 * UNR KiB in flight under its own
 // replay: HBM and VALU work overlap inside each wave, where the register-staged kernels
 // ran their waves in phase (all load, then all replay: the flush cost the SUM of its HBM
-// pass and its replay). Waits are counted explicitly (asm s_waitcnt, LDS reads as asm:
-// hipcc would drain every load in flight before a C++ LDS read after an LDS-DMA); every
-// VMEM instruction issues with a full exec mask — rows past V load a clamped row and store
-// through a buffer descriptor bounded at V, which drops them — so the counts are exact.
+// pass and its replay). The LDS reads are asm (hipcc would drain every load in flight
+// before a C++ LDS read after an LDS-DMA) behind an explicit wait; rows past V load a
+// clamped row and store through a buffer descriptor bounded at V, which drops them.
 // Same rows, same steps, same adam_elem: bitwise deferred_flush_tile.
 __device__ __forceinline__ float4 lds_read4(const char* p) {
   float4 v;
@@ -790,20 +581,15 @@ __global__ __launch_bounds__(256) void deferred_flush_dma(
       __builtin_amdgcn_global_load_lds((const void*)(vE + e), (__attribute__((address_space(3))) void*)(slot + (2 * UNR + u) * 1024), 16, 0, 0);
     }
   };
-  constexpr int TILE_LD = 4;  // per-row state pieces (last, w, m_w, v_w): 1 or 4
-  (void)TILE_LD;
-  const int tile_pieces = lin ? 4 : 1;
   int from_l = step;  // the lane's row of the current tile: its last[] (rows past V: step)
-  int stores_prev = 0;  // VMEM stores issued by the previous item (counted waits below)
   issue(0);
 #pragma unroll 1
   for (int64_t j = 0; j < n_items; ++j) {
     asm volatile("" ::: "memory");
-    // item j's DMA has landed: only the previous item's stores may still be in flight
-    if (stores_prev == 0) CTR_VMWAIT(0);
-    else if (stores_prev == 3 * UNR) CTR_VMWAIT(3 * UNR);
-    else if (stores_prev == 3 * UNR + 1) CTR_VMWAIT(3 * UNR + 1);
-    else CTR_VMWAIT(3 * UNR + 4);
+    // item j's DMA has landed (and the previous item's stores: loads and stores retire out
+    // of order on vmcnt, so no counted wait can tell them apart; the store latency of one
+    // wave hides under the other waves' replays)
+    CTR_VMWAIT(0);
     const int64_t tile = tile0 + (j / NB) * waves;
     const int64_t base = tile * kWave;
     const int bi = (int)(j % NB);
@@ -856,7 +642,6 @@ __global__ __launch_bounds__(256) void deferred_flush_dma(
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, mm[u]), rM, off, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vv[u]), rV, off, 0, 0);
     }
-    stores_prev = 3 * UNR;
     if (bi == 0) {  // the tile's linear weights (lane = row) and last[]
       if (lin && from_l < step) {
         for (int s = from_l + 1; s <= step; ++s) {
@@ -875,7 +660,6 @@ __global__ __launch_bounds__(256) void deferred_flush_dma(
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mws), rmw, lane * 4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vws), rvw, lane * 4, 0, 0);
       }
-      stores_prev += tile_pieces;
     }
   }
   CTR_VMWAIT(0);
@@ -1354,55 +1138,6 @@ extern "C" int ctr_adam_deferred_catchup_ids(float* emb, float* m_emb, float* v_
                              owner, step_ptr, step_table, h, st);
 }
 
-extern "C" int ctr_adam_deferred_catchup_ahead(
-    float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin, float* v_lin, int64_t V,
-    int K, int32_t* last, const void* idx_cur, int idx_type_cur, int64_t S_cur,
-    const void* idx_next, int idx_type_next, int64_t S_next, int32_t* tag, int32_t tag_value,
-    const int32_t* step_ptr, const float* step_table, double beta1, double beta2, double eps,
-    double weight_decay, ctr_stream_t stream) {
-  CTR_REQUIRE(emb && m_emb && v_emb && last && tag && step_ptr && step_table &&
-                  (idx_cur || S_cur == 0) && (idx_next || S_next == 0),
-              "ctr_adam_deferred_catchup_ahead: null pointer");
-  CTR_REQUIRE(tag_value < 0, "ctr_adam_deferred_catchup_ahead: tag_value must be negative");
-  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && K > 0 && S_cur >= 0 && S_next >= 0 &&
-                  S_cur < (int64_t(1) << 31) && S_next < (int64_t(1) << 31),
-              "ctr_adam_deferred_catchup_ahead: bad sizes");
-  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
-              "ctr_adam_deferred_catchup_ahead: linear table pointers must be all set or all NULL");
-  CTR_REQUIRE((idx_type_cur == CTR_IDX_I32 || idx_type_cur == CTR_IDX_I64) &&
-                  (idx_type_next == CTR_IDX_I32 || idx_type_next == CTR_IDX_I64),
-              "ctr_adam_deferred_catchup_ahead: bad idx_type");
-  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, nullptr),
-              "ctr_adam_deferred_catchup_ahead: needs K %% 4 == 0, (K/4) | 64 and 16-B rows");
-  if (S_next == 0) return CTR_OK;
-  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
-  hipStream_t st = as_stream(stream);
-  if (S_cur > 0) {
-    const unsigned gc = (unsigned)std::min<int64_t>(ceil_div(S_cur, 256), 256);
-    if (idx_type_cur == CTR_IDX_I64)
-      hipLaunchKernelGGL(deferred_tag_kernel<int64_t>, gc, 256, 0, st,
-                         static_cast<const int64_t*>(idx_cur), S_cur, V, tag, tag_value);
-    else
-      hipLaunchKernelGGL(deferred_tag_kernel<int32_t>, gc, 256, 0, st,
-                         static_cast<const int32_t*>(idx_cur), S_cur, V, tag, tag_value);
-    CTR_LAUNCH_CHECK("deferred_tag_kernel");
-  }
-  const unsigned gn = (unsigned)std::min<int64_t>(ceil_div(S_next, 256), 256);
-  if (idx_type_next == CTR_IDX_I64)
-    hipLaunchKernelGGL(deferred_mark_excl_kernel<int64_t>, gn, 256, 0, st,
-                       static_cast<const int64_t*>(idx_next), S_next, V, tag, tag_value);
-  else
-    hipLaunchKernelGGL(deferred_mark_excl_kernel<int32_t>, gn, 256, 0, st,
-                       static_cast<const int32_t*>(idx_next), S_next, V, tag, tag_value);
-  CTR_LAUNCH_CHECK("deferred_mark_excl_kernel");
-  // a small grid: the replay trickles along beside the step's kernels instead of taking
-  // every CU ahead of them (CTR_CATCHUP_AHEAD_BLOCKS for A/B runs)
-  int64_t cap = 64;
-  if (const char* env = getenv("CTR_CATCHUP_AHEAD_BLOCKS")) cap = std::max(1, atoi(env));
-  return launch_catchup_wave(emb, m_emb, v_emb, lin, m_lin, v_lin, V, K, last, idx_next,
-                             idx_type_next, S_next, tag, step_ptr, step_table, h, st, cap);
-}
-
 static int launch_catchup_wave(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                                float* v_lin, int64_t V, int K, int32_t* last, const void* idx,
                                int idx_type, int64_t S, const int32_t* owner,
@@ -1474,70 +1209,5 @@ extern "C" int ctr_fm_step_tail(const float* loss_elem, const float* gz, int64_t
                      loss_scale, loss_out, bias_grad, p, g, m, v, n, h, step_table, step_ctr,
                      loss_sum);
   CTR_LAUNCH_CHECK("fm_step_tail_kernel");
-  return CTR_OK;
-}
-
-extern "C" int ctr_adam_deferred_sweep(float* emb, float* m_emb, float* v_emb, float* lin,
-                                       float* m_lin, float* v_lin, int64_t V, int K,
-                                       int32_t* last, const int32_t* step_ctr, int n_slices,
-                                       const float* step_table, int64_t table_steps,
-                                       double beta1, double beta2, double eps,
-                                       double weight_decay, ctr_stream_t stream) {
-  CTR_REQUIRE(emb && m_emb && v_emb && last && step_ctr && step_table,
-              "ctr_adam_deferred_sweep: null pointer");
-  CTR_REQUIRE(V > 0 && K > 0 && n_slices > 0 && table_steps > 0,
-              "ctr_adam_deferred_sweep: bad sizes");
-  CTR_REQUIRE((lin && m_lin && v_lin) || (!lin && !m_lin && !v_lin),
-              "ctr_adam_deferred_sweep: linear table pointers must be all set or all NULL");
-  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, nullptr),
-              "ctr_adam_deferred_sweep: needs K %% 4 == 0, (K/4) | 64 and 16-B rows");
-  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
-  hipStream_t st = as_stream(stream);
-  const int lds_steps = (int)std::min<int64_t>(table_steps + 1, kMaxLdsSteps);
-  const size_t lds_bytes = (size_t)lds_steps * sizeof(float2);
-  const int K4 = K / 4;
-  const int64_t rows = ceil_div(V, n_slices);
-  // the tiled sweep on a bounded grid (CTR_SWEEP_BLOCKS, default 256: one 4-wave block per
-  // CU beside the step's kernels); CTR_SWEEP_TILE=0: the row-per-lane-group kernel (A/B)
-  const char* te = getenv("CTR_SWEEP_TILE");
-  if (!(te && te[0] == '0') && K4 >= 4) {
-    const char* be = getenv("CTR_SWEEP_BLOCKS");
-    const long bl = be ? atol(be) : 256;
-    const int64_t tiles = ceil_div(ceil_div(V, (int64_t)kWave), n_slices);
-    const unsigned g2 = (unsigned)std::max<int64_t>(
-        1, std::min<int64_t>(ceil_div(tiles, 4), bl >= 1 && bl <= 65536 ? bl : 256));
-#define CTR_SWEEPT(K4_, UNR_)                                                                   \
-  hipLaunchKernelGGL((deferred_sweep_tile<K4_, UNR_>), g2, 256, lds_bytes, st,                  \
-                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
-                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, step_ctr,    \
-                     n_slices, lds_steps, step_table, h)
-    switch (K4) {
-      case 4: CTR_SWEEPT(4, 4); break;
-      case 8: CTR_SWEEPT(8, 4); break;
-      case 16: CTR_SWEEPT(16, 4); break;
-      case 32: CTR_SWEEPT(32, 4); break;
-      case 64: CTR_SWEEPT(64, 4); break;
-    }
-#undef CTR_SWEEPT
-    CTR_LAUNCH_CHECK("deferred_sweep_tile");
-    return CTR_OK;
-  }
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows * K4, 256), 4096));
-#define CTR_SWEEP(K4_)                                                                          \
-  hipLaunchKernelGGL((deferred_sweep_vec<K4_>), grid, 256, lds_bytes, st,                       \
-                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
-                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, step_ctr,    \
-                     n_slices, lds_steps, step_table, h)
-  switch (K4) {
-    case 1: CTR_SWEEP(1); break;
-    case 2: CTR_SWEEP(2); break;
-    case 4: CTR_SWEEP(4); break;
-    case 8: CTR_SWEEP(8); break;
-    case 16: CTR_SWEEP(16); break;
-    case 32: CTR_SWEEP(32); break;
-    case 64: CTR_SWEEP(64); break;
-  }
-#undef CTR_SWEEP
-  CTR_LAUNCH_CHECK("deferred_sweep_vec");
   return CTR_OK;
 }

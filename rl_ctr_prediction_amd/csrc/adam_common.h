@@ -38,7 +38,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 // (v_pk_fma_f32 / v_pk_mul_f32, bitwise the same results) measured slower on MI355X — the
 // apply pass 2-4x (deferred_rows_vec<APPLY>: 7.3 -> 32.6 us at C2, 33.5 -> 59.7 us at C3)
 // and within a few % on the VALU-bound flush (packed fp32 issues at about the scalar rate on
-// gfx950: csrc/adam.hip CTR_FLUSH_PK).
+// gfx950).
 __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4& v,
                                          const AdamHP& h) {
   adam_elem(p.x, g.x, m.x, v.x, h);

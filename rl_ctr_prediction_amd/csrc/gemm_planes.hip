@@ -39,14 +39,6 @@ typedef float pf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
 
-// CTR_PL_SPREAD = 1: the LDS-DMA pieces of stage t+NS-1 are issued between the MFMA groups
-// of stage t (one group per accumulator column) instead of all together right after the
-// stage's barrier, where their issue cost (~100-185 cycles per 1 KiB piece beside MFMAs,
-// MI355X_MICROARCH.md) held every wave's MFMAs back at the same moment
-#ifndef CTR_PL_SPREAD
-#define CTR_PL_SPREAD 0
-#endif
-
 struct PlaneSrc {
   const uint16_t* p;  // plane 0 (bf16 bits); planes `ps` elements apart
   int64_t ld;         // elements per storage row
@@ -280,14 +272,7 @@ __device__ __forceinline__ int64_t planes_tile_index(int64_t gn, int g) {
 // MFMAs of stages t .. t+NS-2.
 // KS: 32-deep MFMA k-steps per ring stage (1 or 2): KS = 2 halves the barriers per k
 // (the guide's BK 32 -> 64) at twice the LDS per stage.
-//
-// A_DIR (KC A operand only): the A fragments skip LDS — each wave loads its own rows'
-// 16x16x32 fragments straight into registers (a KC fragment is one 16-B run of k per lane,
-// i.e. one global_load_dwordx4 per plane), NS-1 stages ahead in a register ring beside the
-// LDS ring that now carries B alone. Every DMA piece of A and every LDS fragment read of A
-// disappear; the A bytes a wave needs come through its vector L1 instead.
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool A_RC, bool B_RC, int NS, int KS = 1,
-          bool A_DIR = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool A_RC, bool B_RC, int NS, int KS = 1>
 __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(PlanesArgs a) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -295,14 +280,13 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile in 16x16 MFMA blocks");
   static_assert(!A_RC || BM == 128 || BM % 64 == 0, "RC operand tiles of 128 or 64 * n");
   static_assert(!B_RC || BN == 128 || BN % 64 == 0, "RC operand tiles of 128 or 64 * n");
-  static_assert(!A_DIR || !A_RC, "direct A fragments need k-contiguous rows");
   constexpr int RA = rc_img<BM>(), RB = rc_img<BN>();  // RC image widths
   static_assert(NS >= 2 && NS <= 7, "2- to 7-deep LDS ring");
   static_assert(KS == 1 || KS == 2, "1 or 2 MFMA k-steps per stage");
-  constexpr int A_PL = A_DIR ? 0 : BM * kPBK * 2, B_PL = BN * kPBK * 2;  // bytes per plane image
+  constexpr int A_PL = BM * kPBK * 2, B_PL = BN * kPBK * 2;  // bytes per plane image
   constexpr int SUB = 3 * (A_PL + B_PL);                     // one 32-deep k-step's images
   constexpr int STAGE = KS * SUB;
-  constexpr int NIA1 = A_DIR ? 0 : 3 * BM / 16, NIB1 = 3 * BN / 16;  // 1 KiB pieces per k-step
+  constexpr int NIA1 = 3 * BM / 16, NIB1 = 3 * BN / 16;  // 1 KiB pieces per k-step
   constexpr int NIA = KS * NIA1, NIB = KS * NIB1;        // ... per stage
   constexpr int EPI = NW * 16 * (WN + 4) * 4;
   constexpr int LDS = NS * STAGE > EPI ? NS * STAGE : EPI;
@@ -349,12 +333,12 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   // t * (32 k) to the base.
   constexpr int IPWA = (NIA + NW - 1) / NW, IPWB = (NIB + NW - 1) / NW;
   const PlaneSrc SA = a.A, SB = a.B;
-  uint32_t offA[IPWA > 0 ? IPWA : 1], offB[IPWB];
-  int ldsA[IPWA > 0 ? IPWA : 1], ldsB[IPWB];
+  uint32_t offA[IPWA], offB[IPWB];
+  int ldsA[IPWA], ldsB[IPWB];
 #pragma unroll
   for (int j = 0; j < IPWA; ++j) {
     const int ins = min(wave + NW * j, NIA - 1);
-    const int ks = NIA1 > 0 ? ins / NIA1 : 0, r = NIA1 > 0 ? ins % NIA1 : 0;
+    const int ks = ins / NIA1, r = ins % NIA1;
     const int plane = r / (BM / 16), c = r % (BM / 16);
     ldsA[j] = ks * SUB + plane * A_PL + c * 1024;
     const int64_t k0 = kb + ks * kPBK;
@@ -375,37 +359,6 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   }
   const int64_t stepA = 2 * (A_RC ? kPBK * KS * SA.ld : kPBK * KS);  // bytes per stage along k
   const int64_t stepB = 2 * (B_RC ? kPBK * KS * SB.ld : kPBK * KS);
-  // direct A: byte offset (plane 0, the split's first k) of the lane's fragment run per
-  // 16-row block of the wave; plane p adds p * psA, stage t adds t * stepA
-  constexpr int IPA = A_DIR ? KS * TM * 3 : 0;  // direct loads per wave per stage
-  int64_t offAd[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    int64_t row = m0 + wm0 + 16 * i + (lane & 15);
-    row = row < SA.rows ? row : SA.rows - 1;  // clamped rows only feed never-stored outputs
-    offAd[i] = (row * SA.ld + kb + 8 * (lane >> 4)) * 2;
-  }
-  const int64_t psA = SA.ps * 2;
-  pbf16x8 areg[A_DIR ? NS : 1][KS][TM][3];
-  auto issue_a = [&](pbf16x8 (&dst)[KS][TM][3], int t_) {
-    const char* base = (const char*)SA.p + (int64_t)t_ * stepA;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          // asm: invisible to the compiler's wait pass, which otherwise drains every load
-          // in flight (vmcnt(0)) at the unrolled loop's head; the stage waits below are the
-          // ones that order these loads before their MFMAs
-          const void* src = base + offAd[i] + p * psA + ks * kPBK * 2;
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[ks][i][p]) : "v"(src));
-        }
-  };
-  (void)issue_a;
-  // (the source is passed as `const void*`: with a type-dependent `const char*` argument the
-  // host-side pass of hipcc 7.2 fails substitution on this builtin and silently drops the
-  // kernel's launch stub)
 #define CTR_PL_ISSUE(t_)                                                                       \
   do {                                                                                         \
     char* st_ = smem + ((t_) % NS) * STAGE;                                                    \
@@ -416,21 +369,6 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     _Pragma("unroll") for (int j_ = 0; j_ < IPWB; ++j_)                                        \
         __builtin_amdgcn_global_load_lds((const void*)(bb_ + offB[j_]), (CTR_LDS void*)(st_ + ldsB[j_]), 16, 0, 0); \
   } while (0)
-
-  constexpr int IPW_ALL = IPWA + IPWB;
-  constexpr int PER = (IPW_ALL + TN - 1) / TN;  // pieces issued after each column group
-  auto issue_piece = [&](int t_, int j) {
-    char* st_ = smem + (t_ % NS) * STAGE;
-    if (j < IPWA) {
-      const char* ba_ = (const char*)SA.p + (int64_t)t_ * stepA;
-      __builtin_amdgcn_global_load_lds((const void*)(ba_ + offA[j]), (CTR_LDS void*)(st_ + ldsA[j]), 16, 0, 0);
-    } else {
-      const char* bb_ = (const char*)SB.p + (int64_t)t_ * stepB;
-      __builtin_amdgcn_global_load_lds((const void*)(bb_ + offB[j - IPWA]),
-                                       (CTR_LDS void*)(st_ + ldsB[j - IPWA]), 16, 0, 0);
-    }
-  };
-  (void)issue_piece;
 
   int aoff[TM][2], boff[TN][2];
 #pragma unroll
@@ -444,15 +382,14 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     boff[i][1] = B_RC ? frag_rc_img_off<RB>(wn0 + 16 * i, lane, 1) : 0;
   }
 
-  auto compute_sub = [&](const char* st, int t_issue, const pbf16x8 (&ad)[TM][3]) {
+  auto compute_sub = [&](const char* st) {
     pbf16x8 af[TM][3];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const char* img = st + p * A_PL;
-        if constexpr (A_DIR) af[i][p] = ad[i][p];
-        else af[i][p] = A_RC ? frag_rc_at(img + aoff[i][0], img + aoff[i][1]) : frag_kc_at(img + aoff[i][0]);
+        af[i][p] = A_RC ? frag_rc_at(img + aoff[i][0], img + aoff[i][1]) : frag_kc_at(img + aoff[i][0]);
       }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -476,60 +413,14 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
         lo[i][tn] = v;
         acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[0], acc[i][tn], 0, 0, 0);
       }
-      if (CTR_PL_SPREAD && t_issue >= 0) {
-#pragma unroll
-        for (int q = 0; q < PER; ++q)
-          if (tn * PER + q < IPW_ALL) issue_piece(t_issue, tn * PER + q);
-      }
     }
   };
-  auto compute = [&](int slot, int t_issue, const pbf16x8 (&ad)[KS][TM][3]) {
+  auto compute = [&](int slot) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      compute_sub(smem + slot * STAGE + ks * SUB, ks == 0 ? t_issue : -1, ad[ks]);
+    for (int ks = 0; ks < KS; ++ks) compute_sub(smem + slot * STAGE + ks * SUB);
   };
 
-  constexpr int IPW = IPWA + IPWB + IPA;
-#define CTR_PL_WAIT_STAGE(t_)                                                               \
-  do {                                                                                      \
-    const int q = min(nt - 1 - (t_), NS - 2);                                               \
-    if (q <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
-    if constexpr (NS - 2 >= 1) { if (q == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * 1) : "memory"); } \
-    if constexpr (NS - 2 >= 2) { if (q == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * 2) : "memory"); } \
-    if constexpr (NS - 2 >= 3) { if (q == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * 3) : "memory"); } \
-    if constexpr (NS - 2 >= 4) { if (q == 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * 4) : "memory"); } \
-    if constexpr (NS - 2 >= 5) { if (q == 5) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * 5) : "memory"); } \
-  } while (0)
-  if constexpr (A_DIR) {
-    // the loop unrolled by NS so that every register-ring slot is a compile-time index
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-      if (s < nt) {
-        CTR_PL_ISSUE(s);
-        issue_a(areg[s], s);
-      }
-    for (int t0 = 0; t0 < nt; t0 += NS) {
-#pragma unroll
-      for (int u = 0; u < NS; ++u) {
-        const int t = t0 + u;
-        if (t < nt) {
-          CTR_PL_WAIT_STAGE(t);
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-          if (t + NS - 1 < nt) {
-            CTR_PL_ISSUE(t + NS - 1);
-            issue_a(areg[(u + NS - 1) % NS], t + NS - 1);
-          }
-          // the LDS slot laundered into a run-time value: with the constant slot offsets of
-          // the unrolled loop hipcc proves a pending LDS-DMA may alias one slot's reads and
-          // drains every load in flight (vmcnt(0)) there
-          int slot = u;
-          asm volatile("" : "+s"(slot));
-          compute(slot, -1, areg[u]);
-        }
-      }
-    }
-  } else {
+  constexpr int IPW = IPWA + IPWB;
   // prologue: stages 0 .. NS-2 in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -547,15 +438,9 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     // ... and every wave's (and every wave is done reading the slot refilled next)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (CTR_PL_SPREAD) {
-      compute(t % NS, t + NS - 1 < nt ? t + NS - 1 : -1, areg[0]);
-    } else {
-      if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
-      compute(t % NS, -1, areg[0]);
-    }
+    if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
+    compute(t % NS);
   }
-  }
-#undef CTR_PL_WAIT_STAGE
 #undef CTR_PL_ISSUE
   __syncthreads();  // every stage read before the epilogue reuses the LDS
 #pragma unroll
@@ -662,7 +547,6 @@ struct PlDef {
   int occ;     // blocks resident per CU (LDS bound)
   double eff;  // sustained fraction of the per-CU bf16 MFMA peak (model only)
   int ks = 1;  // 32-deep k-steps per ring stage
-  bool dir = false;  // A fragments loaded straight into registers (KC A only)
 };
 static const PlDef kPl[] = {
     {64, 160, 2, 2, 3, 1, 0.60},   // 0: fwd0 / dH1-shaped (N = 300 -> 320), 256 blocks at B = 8192
@@ -701,13 +585,6 @@ static const PlDef kPl[] = {
     {256, 64, 4, 2, 2, 1, 0.60},   // 26: 120 KB (dW1: M = 200)
     {192, 64, 4, 2, 2, 1, 0.60},   // 27: 96 KB
     {320, 64, 2, 2, 2, 1, 0.60},   // 28: 144 KB, 4 waves (TM 10)
-    // direct A fragments (A_DIR): the LDS ring holds B only
-    {64, 160, 4, 2, 3, 1, 0.70, 1, true},   // 29: fwd0-shaped, A rows shared by 2 N-waves
-    {128, 80, 8, 1, 4, 1, 0.70, 1, true},   // 30: 8 waves x 16 rows x 80
-    {128, 80, 4, 1, 4, 1, 0.70, 1, true},   // 31: 4 waves x 32 rows x 80
-    {128, 64, 8, 1, 3, 1, 0.65, 1, true},   // 32: dX / dH1 (k-strided B of 64)
-    {128, 128, 8, 1, 3, 1, 0.65, 1, true},  // 33
-    {64, 160, 4, 1, 3, 1, 0.70, 1, true},   // 34: 4 waves x 16 rows x 160
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -719,7 +596,7 @@ struct PlCfg {
 
 static bool pl_valid(int ti, bool a_rc, bool b_rc) {
   const PlDef& d = kPl[ti];
-  return (!d.dir || !a_rc) && (!d.dir || !b_rc || d.bn == 128 || d.bn % 64 == 0) && (!a_rc || d.bm == 128 || d.bm % 64 == 0) && (!b_rc || d.bn == 128 || d.bn % 64 == 0);
+  return (!a_rc || d.bm == 128 || d.bm % 64 == 0) && (!b_rc || d.bn == 128 || d.bn % 64 == 0);
 }
 
 // a KS = 2 tiling needs every split's k range in whole 64-deep stages
@@ -738,7 +615,7 @@ static bool pl_ks_ok(const PlDef& d, int64_t Kp, int64_t kps) {
 #define CTR_PL_DX_XG 1
 #endif
 #ifndef CTR_PL_FWD0_TILE
-#define CTR_PL_FWD0_TILE 8  // (A/B builds: 30, the direct-A 128 x 80 tiling)
+#define CTR_PL_FWD0_TILE 8
 #endif
 static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   auto mk = [&](int ti, int s) {
@@ -782,11 +659,9 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   // products with a k-strided B (the dH1 / dX backward) on 64x64 x3 blocks per CU, the
   // transposed weight gradients (both operands k-strided, long K) on 64x64 with split-K
   // sized to ~2 blocks per CU
-  // fwd0 (N = 300) stays on the 64 x 160 LDS tiling (8): the direct-A 128 x 80 tiling (30:
-  // A fragments straight into registers, the LDS ring carries the weight tile alone) is
-  // faster standalone (59.1 vs 65.2 us, profiles/r03_gemm_direct_a.txt) but not in the step,
-  // where it reads the X planes 4 times instead of 2 beside the plan kernels (C3 12.44 /
-  // 12.63 vs 12.60 / 12.76 M ex/s, alternating)
+  // fwd0 (N = 300) on the 64 x 160 tiling (8): a direct-to-register A variant (round 3,
+  // removed) was faster standalone (59.1 vs 65.2 us, profiles/r03_gemm_direct_a.txt) but not
+  // in the step, where it read the X planes 4 times instead of 2
   if (!a_rc && !b_rc && M >= 2048 && N > 256 && N <= 320) return mk(CTR_PL_FWD0_TILE, 1);
   if (!a_rc && !b_rc && M >= 2048 && N <= 256) return mk(17, 1);
   if (!a_rc && b_rc && M >= 2048 && N >= 1024) {
@@ -838,7 +713,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   PlCfg best = mk(0, 1);
   double best_t = 1e30;
   for (int ti = 0; ti < kNumPl; ++ti) {
-    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1 || kPl[ti].dir) continue;  // the model: KS = 1 only
+    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1) continue;  // the model: KS = 1 only
     const PlDef& d = kPl[ti];
     const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
     for (int s = 1; s <= 32; ++s) {
@@ -866,12 +741,6 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
 #define CTR_PL_K(BM, BN, WMW, WNW, NS, AR, BR, KS)                                        \
   hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WMW, WNW, AR, BR, NS, KS>), grid,             \
                      64 * WMW * WNW, 0, st, a)
-#define CTR_PL_KD(BM, BN, WMW, WNW, NS, BR)                                                    \
-  hipLaunchKernelGGL((gemm_planes_kernel<BM, BN, WMW, WNW, false, BR, NS, 1, true>), grid,     \
-                     64 * WMW * WNW, 0, st, a)
-#define CTR_PL_DIR(BM, BN, WMW, WNW, NS)                 \
-  if (!b_rc) CTR_PL_KD(BM, BN, WMW, WNW, NS, false);     \
-  else CTR_PL_KD(BM, BN, WMW, WNW, NS, true);
 #define CTR_PL_ALL4K(BM, BN, WMW, WNW, NS, KS)                          \
   if (!a_rc && !b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false, KS); \
   else if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, true, KS);      \
@@ -914,17 +783,9 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 26: CTR_PL_ALL4(256, 64, 4, 2, 2) break;
     case 27: CTR_PL_ALL4(192, 64, 4, 2, 2) break;
     case 28: CTR_PL_ALL4(320, 64, 2, 2, 2) break;
-    case 29: CTR_PL_KD(64, 160, 4, 2, 3, false); break;
-    case 30: CTR_PL_KD(128, 80, 8, 1, 4, false); break;
-    case 31: CTR_PL_KD(128, 80, 4, 1, 4, false); break;
-    case 32: CTR_PL_DIR(128, 64, 8, 1, 3) break;
-    case 33: CTR_PL_DIR(128, 128, 8, 1, 3) break;
-    case 34: CTR_PL_KD(64, 160, 4, 1, 3, false); break;
   }
 }
 #undef CTR_PL_AONLY
-#undef CTR_PL_DIR
-#undef CTR_PL_KD
 #undef CTR_PL_ALL4
 #undef CTR_PL_ALL4K
 #undef CTR_PL_K

@@ -43,9 +43,6 @@ struct RadixPass {
   uint32_t* keys_out;
   int32_t* vals_out;
   int32_t* hist;       // [n_tiles][bins]
-  int32_t* hist_next;  // scatter: the next pass's per-tile histograms, accumulated here
-  int32_t* zero_hist;  // first histogram launch: zero_count arrays [n_tiles][bins] to clear
-  int zero_count;
   int64_t S;
   int n_tiles;
   int shift;
@@ -77,10 +74,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(RadixPass a) {
   }
   __syncthreads();
   for (int d = t; d < R; d += kSortThreads) a.hist[(int64_t)blockIdx.x * R + d] = h[d];
-  // the later passes' histograms are accumulated by the scatters (atomics): start at zero
-  for (int z = 0; z < a.zero_count; ++z)
-    for (int d = t; d < R; d += kSortThreads)
-      a.zero_hist[((int64_t)z * a.n_tiles + blockIdx.x) * R + d] = 0;
 }
 
 // Exclusive scan of one value per thread over the 256-thread block (4 waves).
@@ -195,7 +188,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
 #pragma unroll
   for (int g0 = 0; g0 < IPT; g0 += G) {
     int rank[G];
-    uint64_t peer[G];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       const int64_t e = base + (g0 + i) * kSortThreads + t;
@@ -208,7 +200,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
         peers &= ((d >> b) & 1u) ? m : ~m;
       }
       rank[i] = __popcll(peers & lt);
-      peer[i] = peers;
       if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
     }
     __syncthreads();
@@ -235,25 +226,6 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(RadixPass a
       const bool ok = e < a.S;
       const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
       pos[g0 + i] = ok ? s_base[d] + s_pre[i][w][d] + rank[i] : -1;
-      if constexpr (!LAST) {
-        // the next pass's histogram of the tile this key lands in: lanes of the peer group
-        // (same digit: consecutive positions, so at most two output tiles, told apart by
-        // parity) with the same next digit add their count with one atomic
-        if (a.hist_next) {
-          const uint32_t nd = (key[g0 + i] >> (a.shift + BITS)) & (R - 1);
-          const int ot = ok ? (int)(pos[g0 + i] / (kSortThreads * IPT)) : 0;
-          uint64_t same = peer[i];
-#pragma unroll
-          for (int b = 0; b < BITS; ++b) {
-            const uint64_t m = __ballot((nd >> b) & 1u);
-            same &= ((nd >> b) & 1u) ? m : ~m;
-          }
-          const uint64_t mo = __ballot(ot & 1);
-          same &= (ot & 1) ? mo : ~mo;
-          if (ok && (same & lt) == 0)
-            atomicAdd(&a.hist_next[(int64_t)ot * R + nd], (int32_t)__popcll(same));
-        }
-      }
     }
   }
 #pragma unroll
@@ -492,22 +464,11 @@ static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
     L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
     L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
   }
-  // histograms sized for the widest digit (the plan's buffers do not know V), one per pass
-  // (the scatters accumulate the next pass's; up to 4 passes of 8 bits)
-  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles * 4));
+  // histograms sized for the widest digit (the plan's buffers do not know V)
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles));
   L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
   L->total = off;
   return off;
-}
-
-// CTR_PLAN_FUSED_HIST=1 (A/B runs): the scatters accumulate the next pass's per-tile
-// histograms (peer-group-aggregated device atomics) instead of a histogram launch before
-// every pass — bit-exact, two launches fewer, but measured slower on MI355X (per plan C2 67
-// vs 55 us, C3 80 vs 65, C5 96 vs 77: the extra ballots and cross-XCD atomics cost more
-// than the launches they save)
-static bool plan_fused_hist() {
-  const char* env = getenv("CTR_PLAN_FUSED_HIST");
-  return env && env[0] == '1';
 }
 
 template <int IPT, int BITS>
@@ -515,22 +476,17 @@ static int run_passes(RadixPass a, int passes, const ctr_sparse_plan* plan, Plan
                       hipStream_t st) {
   const unsigned grid = (unsigned)a.n_tiles;
   constexpr int R = Radix<BITS>::kBins;
-  const bool fused = plan_fused_hist() && passes <= 4;
-  const int64_t hsz = (int64_t)a.n_tiles * R;
   for (int p = 0; p < passes; ++p) {
     const bool first = p == 0, last = p == passes - 1;
     a.shift = p * BITS;
-    a.hist = fused ? L.hist + p * hsz : L.hist;
-    a.hist_next = (fused && !last) ? L.hist + (p + 1) * hsz : nullptr;
-    a.zero_hist = (fused && first) ? L.hist + hsz : nullptr;
-    a.zero_count = (fused && first) ? passes - 1 : 0;
+    a.hist = L.hist;
     a.keys_in = first ? nullptr : L.keys[(p - 1) & 1];
     a.vals_in = first ? nullptr : L.vals[(p - 1) & 1];
     a.keys_out = last ? reinterpret_cast<uint32_t*>(plan->sorted_rows) : L.keys[p & 1];
     a.vals_out = last ? plan->sorted_slots : L.vals[p & 1];
     if (first)
       hipLaunchKernelGGL((radix_hist_kernel<IPT, true, BITS>), grid, kSortThreads, 0, st, a);
-    else if (!fused)
+    else
       hipLaunchKernelGGL((radix_hist_kernel<IPT, false, BITS>), grid, kSortThreads, 0, st, a);
     CTR_LAUNCH_CHECK("radix_hist_kernel");
     if (first && last)

@@ -23,7 +23,7 @@ __all__ = [
     "fm_embedding_grad_adam", "segment_sum_rows_adam",
     "rows_to_dense", "adam_dense", "fm_step_tail", "adam_embedding", "adam_scalars", "feature_embedding",
     "AdamStepTable", "adam_deferred_rows", "adam_deferred_flush", "adam_deferred_catchup_ids",
-    "step_begin", "step_end", "adam_deferred_sweep", "ids_add_", "shard_pack_ids", "shard_runs_copy",
+    "step_begin", "step_end", "ids_add_", "shard_pack_ids", "shard_runs_copy",
     "softmax_rows", "pg_discount_norm", "pg_loss_grad", "pg_vt_mean", "pg_loss_grad_global", "check_index_error", "Workspace",
     "EPI_NONE", "EPI_BIAS", "EPI_BIAS_RELU", "EPI_BIAS_RELU_DROP", "EPI_GRAD_MASK",
 ]
@@ -757,26 +757,6 @@ def adam_deferred_catchup_ids(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx: t
                                       float(eps), float(weight_decay), _stream())
 
 
-def adam_deferred_catchup_ahead(emb, m_emb, v_emb, lin, m_lin, v_lin, last, idx_cur: torch.Tensor,
-                                idx_next: torch.Tensor, tag: torch.Tensor, tag_value: int,
-                                step_dev: torch.Tensor, table: AdamStepTable, step_hint: int,
-                                betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0) -> None:
-    """Bring the rows of idx_next that idx_cur does not hold to the step in step_dev (device
-    int32) — the catch-up of the next step, run while the current one executes. tag: an
-    int32[V] scratch; tag_value: negative, never reused with this tag array."""
-    V, K = emb.shape
-    ic, itc = _idx(idx_cur)
-    inx, itn = _idx(idx_next)
-    if tag.dtype != torch.int32 or tag.numel() < V:
-        raise ValueError("adam_deferred_catchup_ahead: tag must be int32[V]")
-    tab = table.ensure(max(step_hint, 1))
-    lib.ctr_adam_deferred_catchup_ahead(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin),
-                                        _p(v_lin), V, K, _p(last), _p(ic), itc, ic.numel(),
-                                        _p(inx), itn, inx.numel(), _p(tag), int(tag_value),
-                                        _p(step_dev), _p(tab), float(betas[0]), float(betas[1]),
-                                        float(eps), float(weight_decay), _stream())
-
-
 def step_begin(step_ctr: torch.Tensor) -> None:
     """ctr[1] = ctr[0] + 1 on the device (int32[2]: completed steps, step in flight)."""
     lib.ctr_step_begin(_p(step_ctr), _stream())
@@ -819,17 +799,6 @@ def fm_step_tail(loss_elem: torch.Tensor, gz: torch.Tensor, loss_scale: float,
                          _p(step_ctr), float(betas[0]), float(betas[1]), float(eps),
                          float(weight_decay), _p(loss_sum) if loss_sum is not None else None,
                          _stream())
-
-
-def adam_deferred_sweep(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step_ctr: torch.Tensor,
-                        n_slices: int, table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8,
-                        weight_decay=0.0) -> None:
-    """Bring slice ctr[0] % n_slices of the rows up to the completed step ctr[0]."""
-    V, K = emb.shape
-    lib.ctr_adam_deferred_sweep(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), V,
-                                K, _p(last), _p(step_ctr), int(n_slices), _p(table.tab),
-                                int(table.capacity), float(betas[0]), float(betas[1]),
-                                float(eps), float(weight_decay), _stream())
 
 
 def adam_deferred_flush(emb, m_emb, v_emb, lin, m_lin, v_lin, last, step: int,

@@ -417,7 +417,6 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                           self.step_done, self.step_table, step_hint,
                                           self.betas, self.eps, self.weight_decay)
         self._span("catchup", t)
-        self._fork_sweep()
         t = self._mark("exchange")
         hip_ops.embedding_gather(self.E_tab, xb.recv_ids, out=xb.rows_out)
         alltoall_equal(xb.rows_in, xb.rows_out, self.group)
@@ -461,7 +460,6 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                    step_dev=self.step_cur)
         self._span("adam", t)
         self._adam_dense(step_hint)
-        self._join_sweep()
         hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss
 
@@ -568,7 +566,6 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                           self.step_table, self.step_count + 1, self.betas,
                                           self.eps, self.weight_decay)
         self._span("catchup", t)
-        self._fork_sweep()
         t = self._mark("exchange")
         rows = hip_ops.embedding_gather(self.E_tab, req)
         T = alltoallv(rows, recv_c, send_c, self.group)
@@ -603,7 +600,6 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("adam", t)
         self._dirty = True
         self._adam_dense(self.step_count)
-        self._join_sweep()
         hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         for n in ahead:  # the next batches' plans and counts, concurrent with this step
             k = self._xkey(n)

@@ -36,7 +36,7 @@ import torch
 import torch.nn as nn
 
 from . import hip_ops
-from ._lib import StageDesc, lib
+from ._lib import lib
 from .distributed import allgather_sparse_rows, allreduce_sum_, world
 from .p_model import FM, DeepFM, InnerPNN
 
@@ -91,7 +91,7 @@ class InputSlot:
     passes through the slot, so a stream of fresh batches replays the same graphs (the
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
-    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph", "plan_exec",
+    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph",
                  "done_ev", "stream_i", "stage_stream", "cap", "counts")
 
     def __init__(self, shape, index: int, device):
@@ -102,7 +102,6 @@ class InputSlot:
         self.plan = hip_ops.SparsePlanBuffers(B * F, device)
         self.ev = None          # staged ahead: the copy + plan on the plan stream recorded here
         self.plan_graph = None  # the plan build of this slot, captured on its plan stream
-        self.plan_exec = None   # its hipGraphExec_t (ctr_step_launch launches it natively)
         self.done_ev = None     # the slot's staging event (one per slot, re-recorded)
         self.stream_i = 0
         self.stage_stream = None  # the plan stream its last staging ran on
@@ -206,10 +205,6 @@ class FusedCTRTrainer:
         # initialised to {0, 1}: ctr_step_end advances both, so no step-begin launch is needed
         self.step_ctr = torch.tensor([0, 1], dtype=torch.int32, device=self.device)
         self.step_done, self.step_cur = self.step_ctr[0:1], self.step_ctr[1:2]
-        # optional background sweep: each step brings 1/sweep_slices of the rows up to date on
-        # its own stream. Off by default: measured on MI355X (C3) it slows the concurrent
-        # GEMMs by more than it saves at flush() (8.6 vs 9.9 M ex/s at K=30)
-        self.sweep_slices = 0
         # fused scatter + Adam apply (one process, deferred mode); keep_grads keeps every
         # row's gradient sum in b.grad_rows / b.grad_lin (tests read them)
         self.fuse_apply = os.environ.get("CTR_FUSE_APPLY", "1") != "0"
@@ -233,16 +228,7 @@ class FusedCTRTrainer:
         self._staged: dict = {}    # ids key of a batch staged ahead -> its InputSlot
         self.max_slots = 8
         self.captures = 0          # step graphs captured (tests: bounded, batch-independent)
-        # the steady-state single-process step issued by one native call (ctr_step_launch)
-        # instead of ~10 torch calls from Python: opt-in (CTR_NATIVE_LAUNCH=1). It frees
-        # host time but measured no faster on MI355X boxes, where the step is GPU-bound
-        # (C2 50.6 / 49.7 vs 51.5 / 51.9 and 50.0 / 50.7 vs 49.8 / 53.2 M ex/s Python; C3
-        # within noise): the next batch's plan then starts sooner and overlaps more of the
-        # step (issued before the step graph it measured slower still, C2 44-48)
-        self.native_launch = os.environ.get("CTR_NATIVE_LAUNCH", "0") == "1"
-        self._native_launch = lib.ctr_step_launch
         self._ev_start = None
-        self.native_steps = 0  # steps issued by ctr_step_launch (tests)
         self._dw0_fork = os.environ.get("CTR_DW0_FORK", "dx")
         self._db0_last = os.environ.get("CTR_DB0_LAST", "0") == "1"
         # the weight-gradient side list: "ones" (default) — dW1 alone from the head; from dX
@@ -301,7 +287,6 @@ class FusedCTRTrainer:
                              hip_ops.Planes(*w1.shape, self.device))
         # created on first use: every HIP stream takes one of the process's few hardware
         # queues (GPU_MAX_HW_QUEUES = 4), and streams beyond that share queues in order
-        self._sweep_stream = None
         self._plan_stream = None
         if self._side is not None:
             self._plan_stream = self._new_stream()
@@ -316,10 +301,6 @@ class FusedCTRTrainer:
         # slots, the slot-index rule put slots 0 and 2 on one stream: their plans ran back to
         # back, two in one step and none in the next); "slot" — the slot's own stream
         self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "seq")
-        # stage the next batches (ids copy + plan graph on the plan streams) before the step
-        # graph is enqueued rather than after it: the plan then starts with the step, beside
-        # the catch-up and gather, instead of ~80 us of host time later (A/B knob)
-        self._stage_first = os.environ.get("CTR_STAGE_FIRST", "0") == "1"
         self._stage_seq = 0
         self._extra_plan_streams: list = []
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
@@ -437,9 +418,8 @@ class FusedCTRTrainer:
 
     def _bound_staleness(self) -> None:
         """Flush once `flush_every` steps have passed since the last flush: no row is then
-        more than that many steps behind when a batch reads it (with the background sweep
-        on, the sweep bounds the staleness instead)."""
-        if (self.deferred and self.flush_every > 0 and not self.sweep_slices
+        more than that many steps behind when a batch reads it."""
+        if (self.deferred and self.flush_every > 0
                 and self.step_count - self._flushed_at >= self.flush_every):
             self.flush()
 
@@ -584,10 +564,6 @@ class FusedCTRTrainer:
                 main.wait_event(self._staged.pop(k).ev)  # its plan-stream writes come first
         todo = [(n, k) for n, k in nk if k not in self._staged]
         have = slot is not None
-        if have and self.native_launch and self.use_graphs and self.timing is None:
-            loss = self._native_step(slot, y, mean_div, todo, shape, main)
-            if loss is not None:
-                return loss
         ev_start = None
         if todo:  # everything enqueued before this step (the last users of the slots)
             ev_start = self._start_event()
@@ -599,18 +575,14 @@ class FusedCTRTrainer:
             slot = self._acquire_slot(shape)
             slot.ids.copy_(x, non_blocking=True)
         slot.y.copy_(y.reshape(-1), non_blocking=True)
-        if self._stage_first:  # the plan streams get their work before the step graph
-            for n, k in todo:
-                self._stage_ahead(n, k, shape, slot, ev_start, main)
         if self.use_graphs and self.timing is None:
             loss = self._graph_step(slot, mean_div, have)
         else:
             self.step_table.ensure(self.step_count + 1)
             loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
             self._after_step()
-        if not self._stage_first:
-            for n, k in todo:
-                self._stage_ahead(n, k, shape, slot, ev_start, main)
+        for n, k in todo:
+            self._stage_ahead(n, k, shape, slot, ev_start, main)
         return loss
 
     def _ring(self, shape) -> list:
@@ -688,7 +660,7 @@ class FusedCTRTrainer:
                     g = torch.cuda.CUDAGraph()
                     with graph_capture(g, pool=self._graph_pool, stream=ps):
                         s.plan.build(s.ids, self.V)  # captured, not executed
-                    s.plan_graph, s.plan_exec = g, g.raw_cuda_graph_exec()
+                    s.plan_graph = g
             self._span("plan", t)
             ev = self._slot_event(s)
             ev.record(ps)
@@ -717,67 +689,6 @@ class FusedCTRTrainer:
         if self._ev_start is None:
             self._ev_start = torch.cuda.Event()
         return self._ev_start
-
-    def _native_step(self, slot: InputSlot, y, mean_div: float, todo, shape, main):
-        """The steady-state step — labels into the staged slot, the slot's step graph, the
-        next batches copied into their slots and their plan graphs — in ONE native call
-        (ctr_step_launch: the Python path's calls in its order). Returns the
-        loss, or None (nothing done) when this step needs the Python path: a graph not
-        captured yet, a step-table re-size, or inputs that need a conversion."""
-        if (self.step_table.capacity < self.step_count + 2
-                or self._graph_tab_version != self.step_table.version):
-            return None
-        mlp = getattr(self.model, "mlp", None)
-        drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
-        hit = self._graphs.get((slot.shape, slot.index, mean_div, self.model.training, drops,
-                                True))
-        if hit is None:
-            return None
-        B, _, dtype = shape
-        if not (y.is_cuda and y.dtype == torch.float32 and y.is_contiguous()
-                and y.numel() == B and y.device == self.device):
-            return None
-        for n, _ in todo:
-            if not (n.is_cuda and n.dtype == dtype and n.is_contiguous()
-                    and n.device == self.device):
-                return None
-        picked = []
-        for n, k in todo:
-            s = self._acquire_slot(shape, exclude=slot, ahead=True)
-            if s.plan_exec is None:  # its plan graph is captured by the Python path
-                for _, kk, _ in picked:
-                    del self._staged[kk]
-                return None
-            self._staged[k] = s  # marks it busy for the next acquire
-            picked.append((n, k, s))
-        stages = (StageDesc * max(1, len(picked)))()
-        for i, (n, _, s) in enumerate(picked):
-            ps = self._stage_stream(s)
-            ev = self._slot_event(s)
-            st = stages[i]
-            st.src, st.dst, st.bytes = n.data_ptr(), s.ids.data_ptr(), n.numel() * n.element_size()
-            st.stream, st.plan_graph = ps.cuda_stream, s.plan_exec
-            st.done_event = self._event_handle(ev)
-        start = self._start_event()
-        g, self._bufs, exec_handle = hit
-        self._native_launch(main.cuda_stream, self._event_handle(slot.ev), y.data_ptr(),
-                            slot.y.data_ptr(), B * 4, exec_handle,
-                            self._event_handle(start) if picked else None, stages, len(picked))
-        for n, _, s in picked:
-            n.record_stream(s.stage_stream)  # read there until the copy ran
-            s.ev = s.done_ev
-        slot.ev = None
-        self._bufs.plan = slot.plan
-        self._after_step()
-        self.native_steps += 1
-        return self._bufs.loss
-
-    @staticmethod
-    def _event_handle(ev):
-        """The hipEvent_t of a torch event (created by a first record if needed)."""
-        if ev.cuda_event == 0:
-            ev.record()
-        return ev.cuda_event
 
     @staticmethod
     def _xkey(x):
@@ -827,10 +738,10 @@ class FusedCTRTrainer:
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
                     self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
-                self._graphs[key] = (g, self._bufs, g.raw_cuda_graph_exec())
+                self._graphs[key] = (g, self._bufs)
                 self.captures += 1
             return loss
-        g, self._bufs, _ = hit  # the buffer set the graph was captured with
+        g, self._bufs = hit  # the buffer set the graph was captured with
         self._bufs.plan = slot.plan
         g.replay()
         self._after_step()
@@ -900,7 +811,6 @@ class FusedCTRTrainer:
             self._span("catchup", t)
             if not self.plan_first:
                 plan()
-            self._fork_sweep()
         else:
             t_plan = self._mark("plan")
             b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
@@ -976,7 +886,6 @@ class FusedCTRTrainer:
         # the dense Adam where the dense gradient completes: on the weight-gradient stream
         # at one process (beside the embedding apply), after the exchange otherwise
         if tail:
-            self._join_sweep()
             t = self._mark("adam")
             hip_ops.fm_step_tail(b.fm.loss_elem, gz, 1.0 / B, b.loss, gv["bias"].view(1),
                                  self.flat, self.flat_grad, self.m_flat, self.v_flat,
@@ -990,7 +899,6 @@ class FusedCTRTrainer:
         with torch.cuda.stream(wg) if wg is not None else _nullctx():
             self._adam_dense(step_hint)
         self._join_wgrad()
-        self._join_sweep()
         hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss
 
@@ -1010,25 +918,6 @@ class FusedCTRTrainer:
                            step_dev=self.step_cur, table=self.step_table, planes=planes or None)
         for name, pl in resplit:
             hip_ops.split_planes(self.views[name], out=pl)
-
-    def _fork_sweep(self) -> None:
-        """Start this step's background sweep (after the catch-up: the batch's rows are
-        current, so the sweep and the step touch disjoint rows)."""
-        if not (self.deferred and self._vec_ok and self.sweep_slices):
-            return
-        if self._sweep_stream is None:
-            self._sweep_stream = self._new_stream()
-        self._sweep_stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._sweep_stream):
-            t = self._mark("sweep")
-            hip_ops.adam_deferred_sweep(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
-                                        self.v_w, self.last, self.step_ctr, self.sweep_slices,
-                                        self.step_table, self.betas, self.eps, self.weight_decay)
-            self._span("sweep", t)
-
-    def _join_sweep(self) -> None:
-        if self._sweep_stream is not None and self.sweep_slices:
-            torch.cuda.current_stream().wait_stream(self._sweep_stream)
 
     def _deepfm_forward_backward(self, x, y, b: _Bufs, E, w, bias, mean_div):
         """The MLP part of DeepFM / InnerPNN (p_model.py:276-293,322 and 185-200) on

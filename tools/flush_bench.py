@@ -26,14 +26,17 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-lin", action="store_true")
-    ap.add_argument("--variants", default="", help="comma-separated CTR_FLUSH_PIPE values (A/B)")
+    ap.add_argument("--variants", default="",
+                    help="comma-separated kernels (A/B): tile (CTR_FLUSH_DMA=0), dma (default), "
+                         "or a CTR_FLUSH_PIPE value 1 / 2")
     ap.add_argument("--steps-list", default="", help="comma-separated replay lengths")
     args = ap.parse_args()
     import os
     for pv in (args.variants.split(",") if args.variants else [None]):
         for T in (map(int, args.steps_list.split(",")) if args.steps_list else [args.steps]):
             if pv is not None:
-                os.environ["CTR_FLUSH_PIPE"] = pv
+                os.environ["CTR_FLUSH_DMA"] = "0" if pv == "tile" else "1"
+                os.environ["CTR_FLUSH_PIPE"] = pv if pv in ("1", "2") else "0"
             run(args, T, pv)
 
 
