@@ -69,25 +69,17 @@ static inline AdamHP make_hp(double step_size, double bc2_sqrt, double beta1, do
   return h;
 }
 
-// One row of a deferred table (float4 column c of KV, lane c == 0 also owning the linear
-// weight): replay the steps it missed up to step-1, then step `step` with its gradient
-// (the body of deferred_rows_vec<APPLY=true>).
-__device__ __forceinline__ void deferred_apply_row(
+// One row of a deferred table whose state (p, m, v of the float4 column c, and of the
+// linear weight on lane c == 0) and last[] are already in registers: replay the steps it
+// missed up to step-1, then step `step` with its gradient, and store it back.
+__device__ __forceinline__ void deferred_apply_loaded(
     float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
     float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
     int32_t* __restrict__ last, int64_t r, int KV, int c, bool col, float4 g, float glin,
-    int step, const float* __restrict__ tab, AdamHP h) {
-  const int from = last[r];
+    int step, const float* __restrict__ tab, AdamHP h, int from, float4 pp, float4 mm,
+    float4 vv, float pw, float mws, float vws) {
   const int64_t e = r * KV + c;
-  float4 pp, mm, vv;
-  if (col) {
-    pp = E[e]; mm = mE[e]; vv = vE[e];
-  }
   const bool own_lin = w && c == 0;
-  float pw = 0.f, mws = 0.f, vws = 0.f;
-  if (own_lin) {
-    pw = w[r]; mws = mw[r]; vws = vw[r];
-  }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int s = from + 1; s < step; ++s) {
     load_step(h, tab, s);
@@ -104,6 +96,27 @@ __device__ __forceinline__ void deferred_apply_row(
     w[r] = pw; mw[r] = mws; vw[r] = vws;
   }
   if (c == 0) last[r] = step;
+}
+
+// The same with the row's state loaded here (the body of deferred_rows_vec<APPLY=true>).
+__device__ __forceinline__ void deferred_apply_row(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
+    int32_t* __restrict__ last, int64_t r, int KV, int c, bool col, float4 g, float glin,
+    int step, const float* __restrict__ tab, AdamHP h) {
+  const int from = last[r];
+  const int64_t e = r * KV + c;
+  float4 pp, mm, vv;
+  if (col) {
+    pp = E[e]; mm = mE[e]; vv = vE[e];
+  }
+  const bool own_lin = w && c == 0;
+  float pw = 0.f, mws = 0.f, vws = 0.f;
+  if (own_lin) {
+    pw = w[r]; mws = mw[r]; vws = vw[r];
+  }
+  deferred_apply_loaded(E, mE, vE, w, mw, vw, last, r, KV, c, col, g, glin, step, tab, h, from,
+                        pp, mm, vv, pw, mws, vws);
 }
 
 }  // namespace ctr
