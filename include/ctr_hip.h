@@ -41,7 +41,8 @@ enum ctr_idx_type { CTR_IDX_I32 = 0, CTR_IDX_I64 = 1 };
 
 enum ctr_err_flag {
   CTR_EFLAG_INDEX = 1,    /* a feature id outside [0, V) */
-  CTR_EFLAG_CAPACITY = 2  /* a row-sharded exchange run longer than its capacity */
+  CTR_EFLAG_CAPACITY = 2, /* a row-sharded exchange run longer than its capacity */
+  CTR_EFLAG_TIMEOUT = 4   /* a bounded in-launch hand-off gave up (sparse plan; never expected) */
 };
 
 /* GEMM epilogues (ctr_gemm_f32). */

@@ -16,6 +16,7 @@ CTR_OK = 0
 CTR_IDX_I32, CTR_IDX_I64 = 0, 1
 CTR_EFLAG_INDEX = 1
 CTR_EFLAG_CAPACITY = 2
+CTR_EFLAG_TIMEOUT = 4
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RELU_DROP, EPI_GRAD_MASK = range(5)
 
 _vp, _i32, _i64, _f32, _f64, _u64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_double, C.c_uint64

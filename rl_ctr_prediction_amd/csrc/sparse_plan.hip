@@ -310,6 +310,296 @@ __global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
   }
 }
 
+// ------------------------------------------------ plan v2: P + 2 launches ---------------
+// The same stable LSD sort and segments in one launch per pass plus two: a histogram
+// launch (every pass's per-tile digit counts at once, from the ids: a digit's total over
+// the batch does not depend on the order the earlier passes leave), then per pass ONE
+// launch whose blocks take their tile by ticket (arrival order) and get the digit counts
+// of the tiles before theirs from those tiles' own blocks, in the same launch: each block
+// publishes its 256 counts as 8-byte {tag, count} granules (one agent-scope atomic store
+// per digit: the data is the flag, no fence) and reads the granules of every earlier tile,
+// polling the ones not yet tagged. A block only waits for blocks that took earlier
+// tickets, i.e. that are already running, so no residency assumption is made; every spin
+// is bounded (a timeout raises CTR_EFLAG_TIMEOUT and leaves the plan wrong rather than
+// hanging). Segments: one launch, the same hand-off for
+// the head counts. The histogram launch zeroes every granule and ticket the later launches
+// poll (they poll after the kernel boundary), so every build starts from a clean state.
+// Result: bit-identical to the 2-launches-per-pass plan (tests/test_gpu_kernels.py).
+constexpr uint32_t kPlanTimeoutFlag = CTR_EFLAG_TIMEOUT;
+typedef unsigned long long u64g;
+
+struct Plan2Args {
+  const void* idx;
+  int idx_type;
+  int64_t V;
+  int64_t S;
+  int n_tiles, n_seg, passes;
+  int32_t* hist;       // [passes][n_tiles][256]
+  u64g* gran;          // [passes][n_tiles][256] {tag = pass + 1, count}
+  u64g* seg_gran;      // [n_seg] {tag = 1, heads}
+  uint32_t* tickets;   // [passes + 1]
+  const uint32_t* keys_in;
+  const int32_t* vals_in;
+  uint32_t* keys_out;
+  int32_t* vals_out;
+  int shift, pass;
+  // segments
+  const int32_t* rows;
+  int32_t *pos_seg, *unique_rows, *seg_offsets, *num_unique;
+  int32_t* err;
+};
+
+__device__ __forceinline__ void plan2_store_gran(u64g* g, uint32_t tag, uint32_t v) {
+  __hip_atomic_store(g, ((u64g)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64g plan2_load_gran(u64g* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Sum of the counts of granules g[0], g[stride], ... g[(n-1)*stride], each polled until its
+// tag is `tag` (bounded: false on timeout). 8 loads in flight per round.
+__device__ __forceinline__ bool plan2_sum_grans(u64g* g, int n, int64_t stride, uint32_t tag,
+                                                int32_t& sum) {
+  int32_t acc = 0;
+  int spins = 0;
+  for (int t0 = 0; t0 < n; t0 += 8) {
+    u64g v[8];
+    uint32_t ready = 0;
+    for (;;) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (!(ready >> q & 1) && t0 + q < n) v[q] = plan2_load_gran(g + (int64_t)(t0 + q) * stride);
+      bool all = true;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (t0 + q >= n || (ready >> q & 1)) continue;
+        if ((uint32_t)(v[q] >> 32) == tag) ready |= 1u << q;
+        else all = false;
+      }
+      if (all) break;
+      if (++spins > (1 << 22)) {
+        sum = acc;
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (t0 + q < n) acc += (int32_t)(uint32_t)v[q];
+  }
+  sum = acc;
+  return true;
+}
+
+template <int IPT>
+__global__ __launch_bounds__(kSortThreads) void plan2_hist_kernel(Plan2Args a) {
+  __shared__ int32_t h[4][256];
+  const int t = threadIdx.x;
+  const int tile = blockIdx.x;
+  for (int d = t; d < 4 * 256; d += kSortThreads) (&h[0][0])[d] = 0;
+  // the granules and tickets this build's later launches poll: a clean state every build
+  for (int p = 0; p < a.passes; ++p)
+    a.gran[((int64_t)p * a.n_tiles + tile) * 256 + t] = 0;
+  if (tile < a.n_seg && t == 0) a.seg_gran[tile] = 0;
+  for (int s2 = tile + a.n_tiles * t; s2 < a.n_seg; s2 += a.n_tiles * kSortThreads)
+    if (s2 >= a.n_tiles) a.seg_gran[s2] = 0;
+  if (tile == 0 && t <= a.passes) a.tickets[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)tile * (kSortThreads * IPT);
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t e = base + i * kSortThreads + t;
+    if (e < a.S) {
+      const uint32_t key = a.idx_type == CTR_IDX_I64
+          ? (uint32_t)load_row(static_cast<const int64_t*>(a.idx), e, a.V, a.err)
+          : (uint32_t)load_row(static_cast<const int32_t*>(a.idx), e, a.V, a.err);
+      for (int p = 0; p < a.passes; ++p) atomicAdd(&h[p][(key >> (8 * p)) & 255], 1);
+    }
+  }
+  __syncthreads();
+  for (int p = 0; p < a.passes; ++p)
+    a.hist[((int64_t)p * a.n_tiles + tile) * 256 + t] = h[p][t];
+}
+
+template <int IPT, bool FIRST, bool LAST>
+__global__ __launch_bounds__(kSortThreads) void plan2_pass_kernel(Plan2Args a) {
+  constexpr int R = 256, G = IPT < 8 ? IPT : 8;
+  static_assert(IPT % G == 0, "IPT must be a multiple of the ranking group");
+  __shared__ int32_t s_base[R];
+  __shared__ int32_t s_run[R];
+  __shared__ int32_t s_cnt[G][kSortWaves][R];
+  __shared__ int32_t s_pre[G][kSortWaves][R];
+  __shared__ int32_t s_wtot[kSortWaves];
+  __shared__ int32_t s_h[R];
+  __shared__ int s_tile;
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1), w = t / kWave;
+  if (t == 0)
+    s_tile = (int)__hip_atomic_fetch_add(&a.tickets[a.pass], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  s_h[t] = 0;
+  __syncthreads();
+  const int tile = s_tile;
+  const int64_t base = (int64_t)tile * (kSortThreads * IPT);
+  uint32_t key[IPT];
+  int32_t val[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int64_t e = base + i * kSortThreads + t;
+    key[i] = 0;
+    val[i] = 0;
+    if (e < a.S) {
+      if (FIRST) {
+        key[i] = a.idx_type == CTR_IDX_I64
+            ? (uint32_t)load_row(static_cast<const int64_t*>(a.idx), e, a.V, (int32_t*)nullptr)
+            : (uint32_t)load_row(static_cast<const int32_t*>(a.idx), e, a.V, (int32_t*)nullptr);
+        val[i] = (int32_t)e;
+      } else {
+        key[i] = a.keys_in[e];
+        val[i] = a.vals_in[e];
+      }
+      atomicAdd(&s_h[(key[i] >> a.shift) & (R - 1)], 1);
+    }
+  }
+  __syncthreads();
+  // this tile's counts, published for the tiles after it
+  u64g* gp = a.gran + (int64_t)a.pass * a.n_tiles * R;
+  plan2_store_gran(gp + (int64_t)tile * R + t, (uint32_t)a.pass + 1, (uint32_t)s_h[t]);
+  // digit totals over the batch (the histogram launch's per-tile counts), 8 rows at a time
+  int32_t tot = 0;
+  {
+    const int32_t* hcol = a.hist + (int64_t)a.pass * a.n_tiles * R + t;
+    for (int j0 = 0; j0 < a.n_tiles; j0 += 8) {
+      int32_t hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv[u] = j0 + u < a.n_tiles ? hcol[(int64_t)(j0 + u) * R] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tot += hv[u];
+    }
+  }
+  // the earlier tiles' counts of this thread's digit (granules of blocks with earlier tickets)
+  int32_t before = 0;
+  if (!plan2_sum_grans(gp + t, tile, R, (uint32_t)a.pass + 1, before) && a.err)
+    atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
+  const int32_t start = block_exclusive_scan(tot, s_wtot);
+  s_base[t] = start + before;
+  s_run[t] = 0;
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int j = 0; j < kSortWaves; ++j) s_cnt[i][j][t] = 0;
+  __syncthreads();
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
+  int32_t pos[IPT];
+#pragma unroll
+  for (int g0 = 0; g0 < IPT; g0 += G) {
+    int rank[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int64_t e = base + (g0 + i) * kSortThreads + t;
+      const bool ok = e < a.S;
+      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t m = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? m : ~m;
+      }
+      rank[i] = __popcll(peers & lt);
+      if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
+    }
+    __syncthreads();
+    {
+      int32_t run = s_run[t];
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int j = 0; j < kSortWaves; ++j) {
+          const int32_t c = s_cnt[i][j][t];
+          s_pre[i][j][t] = run;
+          s_cnt[i][j][t] = 0;
+          run += c;
+        }
+      s_run[t] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int64_t e = base + (g0 + i) * kSortThreads + t;
+      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
+      pos[g0 + i] = e < a.S ? s_base[d] + s_pre[i][w][d] + rank[i] : -1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    if (pos[i] >= 0) {
+      a.keys_out[pos[i]] = key[i];
+      a.vals_out[pos[i]] = val[i];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSortThreads) void plan2_seg_kernel(Plan2Args a) {
+  __shared__ int32_t s_w[kSortWaves];
+  __shared__ int32_t s_tot;
+  __shared__ int s_tile;
+  __shared__ int32_t s_before;
+  const int t = threadIdx.x;
+  if (t == 0)
+    s_tile = (int)__hip_atomic_fetch_add(&a.tickets[a.passes], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int tile = s_tile;
+  const int64_t s0 = (int64_t)tile * kSegTile + (int64_t)t * kSegIPT;
+  int32_t r[kSegIPT];
+  bool head[kSegIPT];
+  int32_t cnt = 0;
+  int32_t prev = (s0 > 0 && s0 - 1 < a.S) ? a.rows[s0 - 1] : -1;
+#pragma unroll
+  for (int i = 0; i < kSegIPT; ++i) {
+    const int64_t s = s0 + i;
+    r[i] = s < a.S ? a.rows[s] : -1;
+    head[i] = s < a.S && (s == 0 || r[i] != prev);
+    prev = r[i];
+    cnt += head[i] ? 1 : 0;
+  }
+  const int32_t ex = block_exclusive_scan(cnt, s_w);
+  if (t == kSortThreads - 1) {
+    s_tot = ex + cnt;
+    plan2_store_gran(a.seg_gran + tile, 1u, (uint32_t)(ex + cnt));
+  }
+  // heads of the tiles before this one: wave 0 sums their granules, 64 at a time
+  if (t < kWave) {
+    int32_t part = 0;
+    bool ok = true;
+    for (int j0 = 0; j0 < tile; j0 += kWave) {
+      int32_t v = 0;
+      if (j0 + t < tile) ok &= plan2_sum_grans(a.seg_gran + j0 + t, 1, 1, 1u, v);
+      part += v;
+    }
+    part = wave_sum_i32(part);
+    if (!ok && a.err) atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
+    if (t == 0) s_before = part;
+  }
+  __syncthreads();
+  int32_t u = s_before + ex - 1;
+#pragma unroll
+  for (int i = 0; i < kSegIPT; ++i) {
+    const int64_t s = s0 + i;
+    if (s < a.S) {
+      if (head[i]) {
+        ++u;
+        a.unique_rows[u] = r[i];
+        a.seg_offsets[u] = (int32_t)s;
+      }
+      a.pos_seg[s] = u;
+      if (s == a.S - 1) {
+        *a.num_unique = u + 1;
+        a.seg_offsets[u + 1] = (int32_t)a.S;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ row sharding -------------
 // slot -> unique-row ordinal (the inverse of the plan's grouping): the forward of a
 // row-sharded step reads the rows it received, compacted in unique order.
@@ -447,6 +737,9 @@ struct PlanLayout {
   int32_t* vals[2];
   int32_t* hist;
   int32_t* tile_heads;
+  u64g* gran;       // plan v2: [4][n_tiles][256]
+  u64g* seg_gran;   // plan v2: [n_seg]
+  uint32_t* tickets;
   size_t total;
 };
 
@@ -464,11 +757,70 @@ static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
     L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
     L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
   }
-  // histograms sized for the widest digit (the plan's buffers do not know V)
-  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles));
+  // histograms sized for the widest digit (the plan's buffers do not know V); plan v2: one
+  // 256-bin histogram per pass (up to 4 passes of 8 bits)
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * std::max<int64_t>(Radix<11>::kBins, 4 * 256) * n_tiles));
   L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
+  L->gran = reinterpret_cast<u64g*>(take(sizeof(u64g) * 4 * 256 * n_tiles));
+  L->seg_gran = reinterpret_cast<u64g*>(take(sizeof(u64g) * n_seg));
+  L->tickets = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * 8));
   L->total = off;
   return off;
+}
+
+// CTR_PLAN_V2=0: the two-launches-per-pass plan (A/B); default: v2
+static bool plan_v2() {
+  const char* e = getenv("CTR_PLAN_V2");
+  return !(e && e[0] == '0');
+}
+
+template <int IPT>
+static int run_plan_v2(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
+                       PlanLayout& L, int passes, int32_t* err, hipStream_t st) {
+  const int64_t S = plan->S;
+  Plan2Args a;
+  memset(&a, 0, sizeof(a));
+  a.idx = idx;
+  a.idx_type = idx_type;
+  a.V = V;
+  a.S = S;
+  a.n_tiles = (int)ceil_div(S, kSortThreads * IPT);
+  a.n_seg = (int)ceil_div(S, kSegTile);
+  a.passes = passes;
+  a.hist = L.hist;
+  a.gran = L.gran;
+  a.seg_gran = L.seg_gran;
+  a.tickets = L.tickets;
+  a.err = err;
+  const unsigned grid = (unsigned)a.n_tiles;
+  hipLaunchKernelGGL((plan2_hist_kernel<IPT>), grid, kSortThreads, 0, st, a);
+  CTR_LAUNCH_CHECK("plan2_hist_kernel");
+  for (int p = 0; p < passes; ++p) {
+    const bool first = p == 0, last = p == passes - 1;
+    a.pass = p;
+    a.shift = 8 * p;
+    a.keys_in = first ? nullptr : L.keys[(p - 1) & 1];
+    a.vals_in = first ? nullptr : L.vals[(p - 1) & 1];
+    a.keys_out = last ? reinterpret_cast<uint32_t*>(plan->sorted_rows) : L.keys[p & 1];
+    a.vals_out = last ? plan->sorted_slots : L.vals[p & 1];
+    if (first && last)
+      hipLaunchKernelGGL((plan2_pass_kernel<IPT, true, true>), grid, kSortThreads, 0, st, a);
+    else if (first)
+      hipLaunchKernelGGL((plan2_pass_kernel<IPT, true, false>), grid, kSortThreads, 0, st, a);
+    else if (last)
+      hipLaunchKernelGGL((plan2_pass_kernel<IPT, false, true>), grid, kSortThreads, 0, st, a);
+    else
+      hipLaunchKernelGGL((plan2_pass_kernel<IPT, false, false>), grid, kSortThreads, 0, st, a);
+    CTR_LAUNCH_CHECK("plan2_pass_kernel");
+  }
+  a.rows = plan->sorted_rows;
+  a.pos_seg = plan->pos_seg;
+  a.unique_rows = plan->unique_rows;
+  a.seg_offsets = plan->seg_offsets;
+  a.num_unique = plan->num_unique;
+  hipLaunchKernelGGL(plan2_seg_kernel, (unsigned)a.n_seg, kSortThreads, 0, st, a);
+  CTR_LAUNCH_CHECK("plan2_seg_kernel");
+  return CTR_OK;
 }
 
 template <int IPT, int BITS>
@@ -543,6 +895,15 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
     return CTR_ERR_WORKSPACE;
   }
   const int ipt = plan_ipt(S);
+  if (plan_v2()) {  // 8-bit digits: one histogram launch + one per pass + one for segments
+    const int passes = (int)ceil_div(key_bits(V), 8);
+    switch (ipt) {
+      case 4: return run_plan_v2<4>(idx, idx_type, V, plan, L, passes, err_flag, st);
+      case 8: return run_plan_v2<8>(idx, idx_type, V, plan, L, passes, err_flag, st);
+      case 16: return run_plan_v2<16>(idx, idx_type, V, plan, L, passes, err_flag, st);
+      default: return run_plan_v2<32>(idx, idx_type, V, plan, L, passes, err_flag, st);
+    }
+  }
   RadixPass a;
   memset(&a, 0, sizeof(a));
   a.idx = idx;

@@ -13,7 +13,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ._lib import (CTR_EFLAG_CAPACITY, CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
+from ._lib import (CTR_EFLAG_CAPACITY, CTR_EFLAG_INDEX, CTR_EFLAG_TIMEOUT, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
                    EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, PlaneViewDesc, SparsePlan,
                    lib)
 
@@ -133,6 +133,9 @@ def check_index_error(err_flag: torch.Tensor) -> None:
     if v & CTR_EFLAG_CAPACITY:  # a library invariant broke (the host sizes the capacity)
         err_flag.zero_()
         raise RuntimeError("row-sharded exchange: a run exceeded its capacity")
+    if v & CTR_EFLAG_TIMEOUT:  # a bounded in-launch hand-off gave up: results are invalid
+        err_flag.zero_()
+        raise RuntimeError("sparse plan: an in-launch hand-off timed out")
     if v & CTR_EFLAG_INDEX:
         err_flag.zero_()
         raise IndexError("index out of range in self")

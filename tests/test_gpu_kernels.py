@@ -34,7 +34,11 @@ def _ids(rng, B, F, V, hot=True):
                                    (8192, 26, 10_000_000), (20165, 26, 2),
                                    (65536, 26, 40_000_000), (777, 22, 2**31 - 1)])
 @pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
-def test_sparse_plan_bit_exact(cuda, B, F, V, dtype):
+@pytest.mark.parametrize("v2", ["1", "0"])
+def test_sparse_plan_bit_exact(cuda, B, F, V, dtype, v2, monkeypatch):
+    """v2 = 1 (default): histogram + one launch per pass (tiles by ticket, the earlier tiles'
+    counts by in-launch granule hand-off) + one segment launch; 0: two launches per pass."""
+    monkeypatch.setenv("CTR_PLAN_V2", v2)
     H = _hip()
     rng = np.random.default_rng(B * 31 + F)
     x = _ids(rng, B, F, V)
@@ -47,6 +51,41 @@ def test_sparse_plan_bit_exact(cuda, B, F, V, dtype):
     np.testing.assert_array_equal(plan.pos_seg.cpu().numpy()[: B * F], pos_seg)
     np.testing.assert_array_equal(plan.unique_rows.cpu().numpy()[:U], uniq)
     np.testing.assert_array_equal(plan.seg_offsets.cpu().numpy()[: U + 1], off)
+
+
+def test_sparse_plan_rebuilds_and_graph_replay(cuda):
+    """The same plan buffers rebuilt for different batches (every build resets the hand-off
+    state it polls), eagerly and as a replayed HIP graph, stay bit-exact; no timeout flag."""
+    H = _hip()
+    rng = np.random.default_rng(5)
+    B, F, V = 4096, 26, 1_000_000
+    xs = [torch.tensor(_ids(rng, B, F, V), device=cuda) for _ in range(4)]
+    ids = torch.empty_like(xs[0])
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    plan = H.SparsePlanBuffers(B * F, cuda)
+    plan.build(xs[0], V, err_flag=err)  # sizes the scratch
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ids.copy_(xs[0])
+        with torch.cuda.graph(g, stream=s):
+            plan.build(ids, V, err_flag=err)
+    torch.cuda.current_stream().wait_stream(s)
+    for i, x in enumerate(xs * 2):
+        if i % 2:
+            plan.build(x, V, err_flag=err)
+        else:
+            ids.copy_(x)
+            g.replay()
+        torch.cuda.synchronize()
+        order, rows, pos_seg, uniq, off = O.sparse_plan(x.cpu().numpy())
+        U = plan.num_unique_host()
+        assert U == uniq.size, i
+        np.testing.assert_array_equal(plan.sorted_slots.cpu().numpy()[: B * F], order)
+        np.testing.assert_array_equal(plan.pos_seg.cpu().numpy()[: B * F], pos_seg)
+        np.testing.assert_array_equal(plan.seg_offsets.cpu().numpy()[: U + 1], off)
+    assert int(err.item()) == 0
 
 
 def test_sparse_plan_empty(cuda):
