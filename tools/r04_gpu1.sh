@@ -3,7 +3,7 @@
 # dX tiling in-step A/B, scatter counters. Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-bash tools/gpu_tests.sh tests/test_gpu_deferred.py tests/test_gpu_driver_loop.py tests/test_gpu_kernels.py tests/test_gpu_sharded.py tests/test_ops_abi.py "tests/test_gpu_gemm_planes.py::test_gemm_planes_every_tiling" || exit 1
+bash tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_deferred.py tests/test_gpu_driver_loop.py tests/test_gpu_sharded.py tests/test_ops_abi.py "tests/test_gpu_gemm_planes.py::test_gemm_planes_every_tiling" || exit 1
 echo "tests ok"
 bash tools/r04_flush_ab.sh > gpurun_out/flush_ab.log 2>&1 || { tail -5 gpurun_out/flush_ab.log; exit 1; }
 echo "flush ab ok"; cat gpurun_out/r04_flush_ab.txt | head -20
@@ -11,10 +11,5 @@ for C in c3 c2; do
   timeout -k 10 300 python bench.py --config $C --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r04_bench_$C.log 2>&1 || { tail -5 gpurun_out/r04_bench_$C.log; exit 1; }
   echo "bench $C $(tail -1 gpurun_out/r04_bench_$C.log | grep -o '"value": [0-9.]*')"
 done
-ENV_A="CTR_SEG_DIRECT=1" ENV_B="CTR_SEG_DIRECT=0" CFGS="c3 c2" RUNS=2 bash tools/env_ab.sh || exit 1
-VARIANTS="base|
-t29|8192,1664,320,0,1=29,1,1
-t30|8192,1664,320,0,1=30,1,1
-t31|8192,1664,320,0,1=31,1,1" bash tools/gemm_instep.sh || exit 1
-python3 tools/gemm_instep.py gpurun_out/instep_base gpurun_out/instep_t29 gpurun_out/instep_t30 gpurun_out/instep_t31 > gpurun_out/r04_dx_instep.txt 2>&1; cat gpurun_out/r04_dx_instep.txt | head -30
-bash tools/scatter_pmc.sh || exit 1
+ENV_A="CTR_SEG_DIRECT=1" ENV_B="CTR_SEG_DIRECT=0" CFGS="c3 c2" RUNS=1 bash tools/env_ab.sh || exit 1
+ENV_A="CTR_PLAN_V2=1" ENV_B="CTR_PLAN_V2=0" CFGS="c2 c3" RUNS=1 bash tools/env_ab.sh || exit 1
