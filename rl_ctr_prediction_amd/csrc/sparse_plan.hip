@@ -464,22 +464,40 @@ __global__ __launch_bounds__(kSortThreads) void plan2_pass_kernel(Plan2Args a) {
   // this tile's counts, published for the tiles after it
   u64g* gp = a.gran + (int64_t)a.pass * a.n_tiles * R;
   plan2_store_gran(gp + (int64_t)tile * R + t, (uint32_t)a.pass + 1, (uint32_t)s_h[t]);
-  // digit totals over the batch (the histogram launch's per-tile counts), 8 rows at a time
-  int32_t tot = 0;
+  // digit totals over the batch (the histogram launch's per-tile counts) and the earlier
+  // tiles' counts (granules of the blocks with earlier tickets), 16 tiles' loads of each in
+  // flight per round
+  int32_t tot = 0, before = 0;
   {
     const int32_t* hcol = a.hist + (int64_t)a.pass * a.n_tiles * R + t;
-    for (int j0 = 0; j0 < a.n_tiles; j0 += 8) {
-      int32_t hv[8];
+    u64g* gcol = gp + t;
+    const uint32_t tag = (uint32_t)a.pass + 1;
+    int spins = 0;
+    for (int j0 = 0; j0 < a.n_tiles; j0 += 16) {
+      int32_t hv[16];
+      u64g gv[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) hv[u] = j0 + u < a.n_tiles ? hcol[(int64_t)(j0 + u) * R] : 0;
+      for (int u = 0; u < 16; ++u) {
+        hv[u] = j0 + u < a.n_tiles ? hcol[(int64_t)(j0 + u) * R] : 0;
+        gv[u] = j0 + u < tile ? plan2_load_gran(gcol + (int64_t)(j0 + u) * R) : 0;
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) tot += hv[u];
+      for (int u = 0; u < 16; ++u) {
+        tot += hv[u];
+        if (j0 + u < tile) {
+          while ((uint32_t)(gv[u] >> 32) != tag) {  // not published yet: poll (bounded)
+            if (++spins > (1 << 22)) {
+              if (a.err) atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            gv[u] = plan2_load_gran(gcol + (int64_t)(j0 + u) * R);
+          }
+          before += (int32_t)(uint32_t)gv[u];
+        }
+      }
     }
   }
-  // the earlier tiles' counts of this thread's digit (granules of blocks with earlier tickets)
-  int32_t before = 0;
-  if (!plan2_sum_grans(gp + t, tile, R, (uint32_t)a.pass + 1, before) && a.err)
-    atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
   const int32_t start = block_exclusive_scan(tot, s_wtot);
   s_base[t] = start + before;
   s_run[t] = 0;
@@ -540,7 +558,6 @@ __global__ __launch_bounds__(kSortThreads) void plan2_pass_kernel(Plan2Args a) {
 
 __global__ __launch_bounds__(kSortThreads) void plan2_seg_kernel(Plan2Args a) {
   __shared__ int32_t s_w[kSortWaves];
-  __shared__ int32_t s_tot;
   __shared__ int s_tile;
   __shared__ int32_t s_before;
   const int t = threadIdx.x;
@@ -564,21 +581,21 @@ __global__ __launch_bounds__(kSortThreads) void plan2_seg_kernel(Plan2Args a) {
   }
   const int32_t ex = block_exclusive_scan(cnt, s_w);
   if (t == kSortThreads - 1) {
-    s_tot = ex + cnt;
     plan2_store_gran(a.seg_gran + tile, 1u, (uint32_t)(ex + cnt));
   }
-  // heads of the tiles before this one: wave 0 sums their granules, 64 at a time
-  if (t < kWave) {
+  // heads of the tiles before this one: every thread sums a strided share of their
+  // granules (up to 256 in flight at once), then a block reduction
+  {
     int32_t part = 0;
     bool ok = true;
-    for (int j0 = 0; j0 < tile; j0 += kWave) {
+    for (int j = t; j < tile; j += kSortThreads) {
       int32_t v = 0;
-      if (j0 + t < tile) ok &= plan2_sum_grans(a.seg_gran + j0 + t, 1, 1, 1u, v);
+      ok &= plan2_sum_grans(a.seg_gran + j, 1, 1, 1u, v);
       part += v;
     }
-    part = wave_sum_i32(part);
     if (!ok && a.err) atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
-    if (t == 0) s_before = part;
+    const int32_t pex = block_exclusive_scan(part, s_w);
+    if (t == kSortThreads - 1) s_before = pex + part;
   }
   __syncthreads();
   int32_t u = s_before + ex - 1;

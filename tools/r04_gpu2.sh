@@ -10,3 +10,4 @@ t30|8192,1664,320,0,1=30,1,1
 t31|8192,1664,320,0,1=31,1,1" bash tools/gemm_instep.sh || exit 1
 python3 tools/gemm_instep.py gpurun_out/instep_base gpurun_out/instep_t29 gpurun_out/instep_t30 gpurun_out/instep_t31 > gpurun_out/r04_dx_instep.txt 2>&1; cat gpurun_out/r04_dx_instep.txt | head -30
 bash tools/scatter_pmc.sh || exit 1
+timeout -k 10 300 python tools/sharded_host_cost.py --config c3 > gpurun_out/r04_sharded_host.txt 2>&1 || exit 1; cat gpurun_out/r04_sharded_host.txt | tail -2
