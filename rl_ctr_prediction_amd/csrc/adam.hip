@@ -212,15 +212,18 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
   const int target = APPLY ? step - 1 : step;
   for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; u < U; u += groups) {
     const int64_t r = rows[u];
-    const int from = last[r];
-    if (!APPLY && from >= target) continue;
+    // the row's state is loaded beside last[r], not behind the staleness test: one dependent
+    // round trip less per row (a current row's loads are wasted, and with the periodic
+    // flush few rows of a batch are current)
     const int64_t e = r * K4 + c;
+    const int from = last[r];
     float4 pp = E[e], mm = mE[e], vv = vE[e];
     float pw = 0.f, mws = 0.f, vws = 0.f;
     const bool own_lin = w && c == 0;
     if (own_lin) {
       pw = w[r]; mws = mw[r]; vws = vw[r];
     }
+    if (!APPLY && from >= target) continue;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int s = from + 1; s <= target; ++s) {
       load_step(h, tab, s);
