@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 ARGS=${@:-tests}
-timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $ARGS \
+timeout -k 10 1000 python -u -m pytest ${PYTEST_STOP:--x} -v --timeout 300 --timeout-method thread -m gpu $ARGS \
   > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 tail -15 gpurun_out/gpu_tests.log
