@@ -4,7 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 PYTEST_STOP="--maxfail=15" bash tools/gpu_tests.sh tests/test_gpu_kernels.py tests/test_gpu_deferred.py tests/test_gpu_driver_loop.py tests/test_gpu_sharded.py tests/test_ops_abi.py "tests/test_gpu_gemm_planes.py::test_gemm_planes_every_tiling"
-echo "tests rc=$?"; grep -E "^FAILED|^ERROR" gpurun_out/gpu_tests.log | head -20
+rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|^ERROR" gpurun_out/gpu_tests.log | head -20
+[ $rc -le 1 ] || exit $rc  # a crash, abort or time limit: nothing more on the GPU in this call
 bash tools/r04_flush_ab.sh > gpurun_out/flush_ab.log 2>&1 || { tail -5 gpurun_out/flush_ab.log; exit 1; }
 echo "flush ab ok"; cat gpurun_out/r04_flush_ab.txt | head -20
 for C in c3 c2; do
