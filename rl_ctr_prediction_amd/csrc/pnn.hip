@@ -41,7 +41,11 @@ __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restric
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
   if (b >= B) return;  // wave-uniform; the tile is wave-private (no block barrier)
-  const int ld = K + 1;
+  // row stride: K + 4 when K % 4 == 0 (16-B aligned rows: the dots read float4s; the 16
+  // lanes of a ds_read_b128 quarter-wave read rows j..j+15 of one field pair walk, banks
+  // 4j + k, all distinct), else K + 1
+  const bool vec = (K & 3) == 0;
+  const int ld = vec ? K + 4 : K + 1;
   float* tile = lds + (int64_t)wave * F * ld;
   float* ob = cat ? cat + b * ldc : nullptr;
   stage_rows_wave(idx, b, F, K, V, emb, tile, ld, ob, err, lane);
@@ -62,7 +66,18 @@ __global__ __launch_bounds__(256) void ipnn_forward_kernel(const IdxT* __restric
     float acc = 0.f;
     {
 #pragma clang fp contract(off)
-      for (int k = 0; k < K; ++k) acc += ei[k] * ej[k];  // torch.mul, then torch.sum
+      if (vec) {  // the same products and sums in the same k order, four k per LDS read
+        for (int k = 0; k < K; k += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(ei + k);
+          const float4 y = *reinterpret_cast<const float4*>(ej + k);
+          acc += x.x * y.x;
+          acc += x.y * y.y;
+          acc += x.z * y.z;
+          acc += x.w * y.w;
+        }
+      } else {
+        for (int k = 0; k < K; ++k) acc += ei[k] * ej[k];  // torch.mul, then torch.sum
+      }
     }
     if (ob) ob[(int64_t)F * K + p] = acc;
     if (xb) {
@@ -232,7 +247,7 @@ extern "C" int ctr_ipnn_forward_planes(const void* idx, int idx_type, int64_t B,
                                        int64_t V, const float* emb, float* cat, int64_t ldc,
                                        const ctr_planes* cat_planes, int32_t* err_flag,
                                        ctr_stream_t stream) {
-  const size_t per_wave = (size_t)F * (K + 1);
+  const size_t per_wave = (size_t)F * (K % 4 == 0 ? K + 4 : K + 1);
   int rc = ipnn_check(idx, idx_type, B, F, K, V, per_wave);
   if (rc != CTR_OK) return rc;
   const int64_t W = (int64_t)F * K + F * (F - 1) / 2;
