@@ -507,263 +507,6 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
   }
 }
 
-// The tiled flush with its loads on LDS-DMA, one batch ahead (CTR_FLUSH_DMA, default):
-// a wave walks its items — (64-row tile, batch of UNR wave-instructions of float4 columns)
-// — and for each: waits for that item's DMA, moves it LDS -> registers, issues the NEXT
-// item's DMA (global_load_lds: no registers held while in flight), then replays the item
-// and stores it. So every wave keeps its next batch's 3 * UNR KiB in flight under its own
-// replay: HBM and VALU work overlap inside each wave, where the register-staged kernels
-// ran their waves in phase (all load, then all replay: the flush cost the SUM of its HBM
-// pass and its replay). The LDS reads are asm (hipcc would drain every load in flight
-// before a C++ LDS read after an LDS-DMA) behind an explicit wait; rows past V load a
-// clamped row and store through a buffer descriptor bounded at V, which drops them.
-// Same rows, same steps, same adam_elem: bitwise deferred_flush_tile.
-__device__ __forceinline__ float4 lds_read4(const char* p) {
-  float4 v;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-__device__ __forceinline__ float lds_read1(const char* p) {
-  float v;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-#define CTR_VMWAIT(N_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory")
-
-template <int K4, int UNR>
-__global__ __launch_bounds__(256) void deferred_flush_dma(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
-    int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  constexpr int RPI = kWave / K4;          // rows per wave-instruction
-  constexpr int NB = K4 / UNR;             // batches per 64-row tile
-  constexpr int PIECES = 3 * UNR;          // 1 KiB E / m / v pieces per batch
-  constexpr int SLOT = PIECES * 1024 + 4 * 256;  // + the tile's last / w / m_w / v_w
-  static_assert(K4 % UNR == 0, "whole batches per tile");
-  __shared__ __attribute__((aligned(1024))) char smem[4 * SLOT];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* slot = smem + wave * SLOT;
-  const int c = lane % K4, r_in = lane / K4;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-  const int64_t n_tiles = (V + kWave - 1) / kWave;
-  const int64_t tile0 = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
-  if (tile0 >= n_tiles) return;  // wave-uniform (no block barrier in this kernel)
-  const int64_t n_items = ((n_tiles - 1 - tile0) / waves + 1) * NB;
-  const bool lin = w != nullptr;
-  // the per-step scalars by scalar loads (a uniform index: SMEM, counted in lgkmcnt): no
-  // vector load may sit in the replay loop, or hipcc's wait pass drains the next item's DMA
-  // (vmcnt(0)) at every replayed step
-  auto set_step = [&](int t) { load_step(h, tab, __builtin_amdgcn_readfirstlane(t)); };
-  // item j: tile tile0 + (j / NB) * waves, batch j % NB
-  auto issue = [&](int64_t j) {
-    const int64_t base = (tile0 + (j / NB) * waves) * kWave;
-    const int bi = (int)(j % NB);
-    if (bi == 0) {  // the tile's per-row state, 4 B per lane (rows past V: the last row)
-      const int64_t r = min<int64_t>(base + lane, V - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(last + r),
-                                       (__attribute__((address_space(3))) void*)(slot + PIECES * 1024), 4, 0, 0);
-      if (lin) {
-        __builtin_amdgcn_global_load_lds((const void*)(w + r),
-                                         (__attribute__((address_space(3))) void*)(slot + PIECES * 1024 + 256), 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(mw + r),
-                                         (__attribute__((address_space(3))) void*)(slot + PIECES * 1024 + 512), 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(vw + r),
-                                         (__attribute__((address_space(3))) void*)(slot + PIECES * 1024 + 768), 4, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int64_t row = min<int64_t>(base + (bi * UNR + u) * RPI + r_in, V - 1);
-      const int64_t e = row * K4 + c;
-      __builtin_amdgcn_global_load_lds((const void*)(E + e), (__attribute__((address_space(3))) void*)(slot + u * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(mE + e), (__attribute__((address_space(3))) void*)(slot + (UNR + u) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vE + e), (__attribute__((address_space(3))) void*)(slot + (2 * UNR + u) * 1024), 16, 0, 0);
-    }
-  };
-  int from_l = step;  // the lane's row of the current tile: its last[] (rows past V: step)
-  issue(0);
-#pragma unroll 1
-  for (int64_t j = 0; j < n_items; ++j) {
-    asm volatile("" ::: "memory");
-    // item j's DMA has landed (and the previous item's stores: loads and stores retire out
-    // of order on vmcnt, so no counted wait can tell them apart; the store latency of one
-    // wave hides under the other waves' replays)
-    CTR_VMWAIT(0);
-    const int64_t tile = tile0 + (j / NB) * waves;
-    const int64_t base = tile * kWave;
-    const int bi = (int)(j % NB);
-    float4 pp[UNR], mm[UNR], vv[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      pp[u] = lds_read4(slot + u * 1024 + lane * 16);
-      mm[u] = lds_read4(slot + (UNR + u) * 1024 + lane * 16);
-      vv[u] = lds_read4(slot + (2 * UNR + u) * 1024 + lane * 16);
-    }
-    float pw = 0.f, mws = 0.f, vws = 0.f;
-    int last_l = 0;
-    if (bi == 0) {
-      last_l = __builtin_bit_cast(int, lds_read1(slot + PIECES * 1024 + lane * 4));
-      if (lin) {
-        pw = lds_read1(slot + PIECES * 1024 + 256 + lane * 4);
-        mws = lds_read1(slot + PIECES * 1024 + 512 + lane * 4);
-        vws = lds_read1(slot + PIECES * 1024 + 768 + lane * 4);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // the slot is free again: the next item's loads go in flight under this item's replay
-    if (j + 1 < n_items) issue(j + 1);
-    asm volatile("" ::: "memory");  // (the counted waits assume this issue order)
-    if (bi == 0) from_l = base + lane < V ? last_l : step;
-    int from[UNR];
-    int f0 = step;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      from[u] = __shfl(from_l, (bi * UNR + u) * RPI + r_in, kWave);
-      f0 = min(f0, from[u]);
-    }
-    for (int s = f0 + 1; s <= step; ++s) {
-      set_step(s);
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        if (s > from[u]) adam_replay_vec(pp[u], mm[u], vv[u], h);
-    }
-    asm volatile("" ::: "memory");
-    // stores through descriptors bounded at the table's end (rows past V are dropped)
-    const int64_t valid_rows = min<int64_t>(kWave, V - base);
-    const int nbytes = (int)(valid_rows * K4 * 16);
-    __amdgpu_buffer_rsrc_t rE = __builtin_amdgcn_make_buffer_rsrc(E + base * K4, (short)0, nbytes, 0x00020000);
-    __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc(mE + base * K4, (short)0, nbytes, 0x00020000);
-    __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(vE + base * K4, (short)0, nbytes, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int off = (((bi * UNR + u) * RPI + r_in) * K4 + c) * 16;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pp[u]), rE, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, mm[u]), rM, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, vv[u]), rV, off, 0, 0);
-    }
-    if (bi == 0) {  // the tile's linear weights (lane = row) and last[]
-      if (lin && from_l < step) {
-        for (int s = from_l + 1; s <= step; ++s) {
-          set_step(s);
-          adam_elem(pw, 0.f, mws, vws, h);
-        }
-      }
-      const int nb4 = (int)(valid_rows * 4);
-      __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc(last + base, (short)0, nb4, 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32((unsigned)step, rL, lane * 4, 0, 0);
-      if (lin) {
-        __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(w + base, (short)0, nb4, 0x00020000);
-        __amdgpu_buffer_rsrc_t rmw = __builtin_amdgcn_make_buffer_rsrc(mw + base, (short)0, nb4, 0x00020000);
-        __amdgpu_buffer_rsrc_t rvw = __builtin_amdgcn_make_buffer_rsrc(vw + base, (short)0, nb4, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, pw), rw, lane * 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mws), rmw, lane * 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, vws), rvw, lane * 4, 0, 0);
-      }
-    }
-  }
-  CTR_VMWAIT(0);
-}
-#undef CTR_VMWAIT
-
-// The tiled flush, software-pipelined: the loads of batch b+1 are issued before batch b's
-// replay, into a second register buffer (UNR rows per buffer; UNR = 2 keeps the register
-// footprint of the single-buffered UNR = 4 kernel), so each wave keeps HBM busy while its
-// VALU replays. Without it the waves of a CU run in phase — all load, all replay — and the
-// flush costs the SUM of its HBM pass and its replay arithmetic (C3 table: 2.1 ms + 0.115 ms
-// per replayed step), not their maximum. Same rows, same steps, same adam_elem: bitwise
-// deferred_flush_tile.
-template <int K4, int UNR, bool LDS_TAB>
-__global__ __launch_bounds__(256) void deferred_flush_pipe(
-    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
-    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
-    int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
-  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
-  if (LDS_TAB) {
-    for (int i = threadIdx.x; i <= step; i += blockDim.x)
-      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
-    __syncthreads();
-  }
-  constexpr int RPI = kWave / K4;
-  constexpr int NB = K4 / UNR;  // batches per 64-row tile
-  static_assert(K4 % UNR == 0 && NB % 2 == 0, "an even number of UNR-row batches per tile");
-  const int lane = threadIdx.x & (kWave - 1);
-  const int c = lane % K4, r_in = lane / K4;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-  const int64_t n_tiles = (V + kWave - 1) / kWave;
-  auto set_step = [&](int t) {
-    if (LDS_TAB) {
-      const float2 v = s_tab[t];
-      h.neg_step_size = v.x;
-      h.inv_bc2_sqrt = v.y;
-    } else {
-      load_step(h, tab, t);
-    }
-  };
-  struct Buf {
-    float4 p[UNR], m[UNR], v[UNR];
-    int from[UNR];
-    int f0;
-  };
-  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-       tile < n_tiles; tile += waves) {
-    const int64_t base = tile * kWave;
-    const int64_t my = base + lane;
-    const bool ok = my < V;
-    const int from_l = ok ? last[my] : step;
-    if (__all(from_l >= step)) continue;
-    auto load = [&](Buf& b, int bi) {
-      b.f0 = step;
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int r = (bi * UNR + u) * RPI + r_in;
-        b.from[u] = __shfl(from_l, r, kWave);
-        b.f0 = min(b.f0, b.from[u]);
-        if (b.from[u] < step) {
-          const int64_t e = (base + r) * K4 + c;
-          b.p[u] = E[e]; b.m[u] = mE[e]; b.v[u] = vE[e];
-        }
-      }
-    };
-    auto run = [&](Buf& b, int bi) {
-      for (int s = b.f0 + 1; s <= step; ++s) {
-        set_step(s);
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-          if (s > b.from[u]) adam_replay_vec(b.p[u], b.m[u], b.v[u], h);
-      }
-#pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        if (b.from[u] < step) {
-          const int64_t e = (base + (bi * UNR + u) * RPI + r_in) * K4 + c;
-          E[e] = b.p[u]; mE[e] = b.m[u]; vE[e] = b.v[u];
-        }
-    };
-    Buf b0, b1;
-    load(b0, 0);
-    // the tile's linear weights replay while batch 0's loads are in flight
-    if (w && from_l < step) {
-      float pp = w[my], mm = mw[my], vv = vw[my];
-      for (int s = from_l + 1; s <= step; ++s) {
-        set_step(s);
-        adam_elem(pp, 0.f, mm, vv, h);
-      }
-      w[my] = pp; mw[my] = mm; vw[my] = vv;
-    }
-#pragma unroll 1
-    for (int bi = 0; bi < NB; bi += 2) {
-      load(b1, bi + 1);
-      run(b0, bi);
-      if (bi + 2 < NB) load(b0, bi + 2);
-      run(b1, bi + 1);
-    }
-    if (from_l < step) last[my] = step;
-  }
-}
-
 // Any K: a thread per row (rows list, or all rows when rows == NULL).
 template <bool APPLY>
 __global__ __launch_bounds__(256) void deferred_scalar(
@@ -1030,69 +773,16 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
                        reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
                        step_table, h)
-#define CTR_DEF_PIPE(K4_, UNR_)                                                                  \
-  if (lds)                                                                                      \
-    hipLaunchKernelGGL((deferred_flush_pipe<K4_, UNR_, true>), grid, 256, lds_bytes, st,        \
-                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
-                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
-                       step_table, h);                                                          \
-  else                                                                                          \
-    hipLaunchKernelGGL((deferred_flush_pipe<K4_, UNR_, false>), grid, 256, 0, st,               \
-                       reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \
-                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step, \
-                       step_table, h)
-    // CTR_FLUSH_PIPE: 0 the single-buffered tile kernel, 1 / 2 the pipelined one with 1 / 2
-    // rows per buffer (A/B); CTR_FLUSH_DMA=0: not the LDS-DMA kernel (the default for K4 >= 4)
-    const char* pe = getenv("CTR_FLUSH_PIPE");
-    const int pipe = pe ? atoi(pe) : 0;
-    const char* de = getenv("CTR_FLUSH_DMA");
-    const bool dma = !(de && de[0] == '0') && pipe == 0 && K4 >= 4 && K4 <= 64;
-    if (dma) {
-      // one resident round: 256 CUs x 5 blocks (28 KiB of LDS, <= 96 VGPRs each)
-      const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_tiles, 4), 1280));
-#define CTR_DEF_DMA(K4_)                                                                          \
-  hipLaunchKernelGGL((deferred_flush_dma<K4_, 2>), gd, 256, 0, st,                               \
-                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),           \
-                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last, (int)step,    \
-                     step_table, h)
-      switch (K4) {
-        case 4: CTR_DEF_DMA(4); break;
-        case 8: CTR_DEF_DMA(8); break;
-        case 16: CTR_DEF_DMA(16); break;
-        case 32: CTR_DEF_DMA(32); break;
-        case 64: CTR_DEF_DMA(64); break;
-      }
-#undef CTR_DEF_DMA
-    } else if (pipe == 1 && K4 >= 2) {
-      switch (K4) {
-        case 2: CTR_DEF_PIPE(2, 1); break;
-        case 4: CTR_DEF_PIPE(4, 1); break;
-        case 8: CTR_DEF_PIPE(8, 1); break;
-        case 16: CTR_DEF_PIPE(16, 1); break;
-        case 32: CTR_DEF_PIPE(32, 1); break;
-        case 64: CTR_DEF_PIPE(64, 1); break;
-      }
-    } else if (pipe == 2 && K4 >= 4) {
-      switch (K4) {
-        case 4: CTR_DEF_PIPE(4, 2); break;
-        case 8: CTR_DEF_PIPE(8, 2); break;
-        case 16: CTR_DEF_PIPE(16, 2); break;
-        case 32: CTR_DEF_PIPE(32, 2); break;
-        case 64: CTR_DEF_PIPE(64, 2); break;
-      }
-    } else {
-      switch (K4) {
-        case 1: CTR_DEF_FLUSH(1, 1); break;
-        case 2: CTR_DEF_FLUSH(2, 2); break;
-        case 4: CTR_DEF_FLUSH(4, 4); break;
-        case 8: CTR_DEF_FLUSH(8, CTR_FLUSH_UNR); break;
-        case 16: CTR_DEF_FLUSH(16, CTR_FLUSH_UNR); break;
-        case 32: CTR_DEF_FLUSH(32, CTR_FLUSH_UNR); break;
-        case 64: CTR_DEF_FLUSH(64, CTR_FLUSH_UNR); break;
-      }
+    switch (K4) {
+      case 1: CTR_DEF_FLUSH(1, 1); break;
+      case 2: CTR_DEF_FLUSH(2, 2); break;
+      case 4: CTR_DEF_FLUSH(4, 4); break;
+      case 8: CTR_DEF_FLUSH(8, CTR_FLUSH_UNR); break;
+      case 16: CTR_DEF_FLUSH(16, CTR_FLUSH_UNR); break;
+      case 32: CTR_DEF_FLUSH(32, CTR_FLUSH_UNR); break;
+      case 64: CTR_DEF_FLUSH(64, CTR_FLUSH_UNR); break;
     }
 #undef CTR_DEF_FLUSH
-#undef CTR_DEF_PIPE
     CTR_LAUNCH_CHECK("deferred_flush_tile");
     return CTR_OK;
   }

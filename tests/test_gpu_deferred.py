@@ -112,8 +112,8 @@ def test_fused_scatter_apply_equals_unfused(cuda, kind, K, direct, monkeypatch):
     tables, the moments and (keep_grads) the per-row sums — on Zipf batches whose hot rows
     span many chunks. K 16 / 32 / 64: 16 / 8 / 4 rows per wave in the fused pass, so both
     of its spanning-row paths (a row's own lane group, the whole wave for hot rows) run.
-    direct = 1 (default): the rows inside one chunk summed by the apply pass itself
-    (seg_span_chunk + seg_apply_direct); 0: the chunk pass + combine-apply pair."""
+    direct = 1 (opt-in): the rows inside one chunk summed by the apply pass itself
+    (seg_span_chunk + seg_apply_direct); 0 (default): the chunk pass + combine-apply pair."""
     monkeypatch.setenv("CTR_SEG_DIRECT", direct)
     import rl_ctr_prediction_amd as P
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
@@ -254,12 +254,12 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
                                        (8, 100_003, 23, True), (128, 100_003, 23, True),
                                        (10, 100_003, 23, True), (64, 37, 5, True),
                                        (32, 70_001, 300, False), (256, 4_099, 9, True)])
-def test_flush_variants_bitwise(cuda, K, V, T, lin, monkeypatch):
-    """The LDS-DMA flush (the default for K % 4 == 0, 16 <= K <= 256) and the
-    software-pipelined register flush (CTR_FLUSH_PIPE=1 / 2) == the single-buffered tile
-    kernel (CTR_FLUSH_DMA=0), bitwise, on rows of mixed staleness (current, 1 step, up to
-    the full region), a row count that is not a multiple of 64 (and one below 64), steps
-    older than any LDS window (T = 300) and a table without linear weights."""
+def test_flush_tile_equals_scalar_bitwise(cuda, K, V, T, lin):
+    """The tiled flush (deferred_flush_tile: 64-row tiles, float4 columns, K % 4 == 0) ==
+    the thread-per-row kernel (deferred_scalar, taken for tables that are not 16-B aligned),
+    bitwise, on rows of mixed staleness (current, 1 step, up to the full region), a row
+    count that is not a multiple of 64 (and one below 64), steps older than any LDS window
+    (T = 300) and a table without linear weights."""
     from rl_ctr_prediction_amd import hip_ops as H
     g = torch.Generator(device=cuda).manual_seed(K + V)
     E0 = torch.randn(V, K, device=cuda, generator=g) * 0.05
@@ -268,19 +268,25 @@ def test_flush_variants_bitwise(cuda, K, V, T, lin, monkeypatch):
     w0 = torch.randn(V, device=cuda, generator=g) * 0.05
     last0 = torch.randint(0, T + 1, (V,), device=cuda, generator=g, dtype=torch.int32)
     last0[:min(640, V // 2)] = T  # whole tiles already current
+
+    def shifted(t):  # the same values at a 4-B (not 16-B) aligned address
+        buf = torch.empty(t.numel() + 1, device=cuda)
+        out = buf[1:].view(t.shape)
+        out.copy_(t)
+        return out
+
     tab = H.AdamStepTable(1e-3, (0.9, 0.999), cuda)
     out = []
-    for dma, pipe in (("0", "0"), ("1", "0"), ("1", "1"), ("1", "2")):
-        monkeypatch.setenv("CTR_FLUSH_DMA", dma)
-        monkeypatch.setenv("CTR_FLUSH_PIPE", pipe)
-        E, m, v, w = E0.clone(), m0.clone(), v0.clone(), w0.clone()
+    for aligned in (True, False):
+        mk = (lambda t: t.clone()) if aligned else shifted
+        E, m, v = mk(E0), mk(m0), mk(v0)
+        w = w0.clone()
         mw, vw, last = torch.zeros_like(w), torch.zeros_like(w), last0.clone()
         if lin:
             H.adam_deferred_flush(E, m, v, w, mw, vw, last, T, tab, weight_decay=1e-5)
         else:
             H.adam_deferred_flush(E, m, v, None, None, None, last, T, tab, weight_decay=1e-5)
         out.append((E, m, v, w, mw, vw, last))
-    for o in out[1:]:
-        for a, b in zip(out[0], o):
-            assert torch.equal(a, b)
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
     assert int(out[0][6].min()) == T

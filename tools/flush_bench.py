@@ -26,21 +26,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-lin", action="store_true")
-    ap.add_argument("--variants", default="",
-                    help="comma-separated kernels (A/B): tile (CTR_FLUSH_DMA=0), dma (default), "
-                         "or a CTR_FLUSH_PIPE value 1 / 2")
     ap.add_argument("--steps-list", default="", help="comma-separated replay lengths")
     args = ap.parse_args()
-    import os
-    for pv in (args.variants.split(",") if args.variants else [None]):
-        for T in (map(int, args.steps_list.split(",")) if args.steps_list else [args.steps]):
-            if pv is not None:
-                os.environ["CTR_FLUSH_DMA"] = "0" if pv == "tile" else "1"
-                os.environ["CTR_FLUSH_PIPE"] = pv if pv in ("1", "2") else "0"
-            run(args, T, pv)
+    for T in (map(int, args.steps_list.split(",")) if args.steps_list else [args.steps]):
+        run(args, T)
 
 
-def run(args, T, variant):
+def run(args, T):
     V, K = args.V, args.K
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -64,7 +56,7 @@ def run(args, T, variant):
             times.append(e0.elapsed_time(e1))
     ms = sorted(times)[len(times) // 2]
     nbytes = 24 * V * K + (0 if lin is None else 24 * V) + 8 * V
-    print(json.dumps({"kernel": "deferred_flush", "variant": variant, "V": V, "K": K,
+    print(json.dumps({"kernel": "deferred_flush", "V": V, "K": K,
                       "steps_replayed": T, "ms": ms, "ms_all": times,
                       "GBps": nbytes / (ms * 1e-3) / 1e9,
                       "elem_steps_per_s": V * (K + (0 if lin is None else 1)) * T / (ms * 1e-3)}))
