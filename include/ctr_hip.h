@@ -41,8 +41,7 @@ enum ctr_idx_type { CTR_IDX_I32 = 0, CTR_IDX_I64 = 1 };
 
 enum ctr_err_flag {
   CTR_EFLAG_INDEX = 1,    /* a feature id outside [0, V) */
-  CTR_EFLAG_CAPACITY = 2, /* a row-sharded exchange run longer than its capacity */
-  CTR_EFLAG_TIMEOUT = 4   /* a bounded in-launch hand-off gave up (sparse plan; never expected) */
+  CTR_EFLAG_CAPACITY = 2  /* a row-sharded exchange run longer than its capacity */
 };
 
 /* GEMM epilogues (ctr_gemm_f32). */
@@ -288,6 +287,13 @@ int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, int64_t cap
                         ctr_stream_t stream);
 int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
                           void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
+/* The same plan (bit-identical) for ids laid out as a [S/F][F] matrix (slot s = b*F + f: the
+ * batch's feature fields as columns): each column sorted inside one workgroup, then merged —
+ * 2 launches of work where a column's ids occupy a range of their own (the CTR layouts), and
+ * exact for any ids. Falls back to ctr_sparse_plan_build for S/F > 8192 or F > 256. */
+int ctr_sparse_plan_build_cols(const void* idx, int idx_type, int64_t V, int64_t F,
+                               const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,
+                               int32_t* err_flag, ctr_stream_t stream);
 
 /* Segmented row sums over a plan, deterministic: each row's slots are summed in slot
  * order in chunks of 16 positions, chunk partials are then added in chunk order (hot

@@ -16,7 +16,6 @@ CTR_OK = 0
 CTR_IDX_I32, CTR_IDX_I64 = 0, 1
 CTR_EFLAG_INDEX = 1
 CTR_EFLAG_CAPACITY = 2
-CTR_EFLAG_TIMEOUT = 4
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RELU_DROP, EPI_GRAD_MASK = range(5)
 
 _vp, _i32, _i64, _f32, _f64, _u64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_double, C.c_uint64
@@ -161,6 +160,7 @@ SIGNATURES = {
     "ctr_transpose_f32": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "ctr_sparse_plan_workspace_bytes": (_i64, [_i64, _i64]),
     "ctr_sparse_plan_build": (_i32, [_vp, _i32, _i64, _plan_p, _vp, _i64, _vp, _vp]),
+    "ctr_sparse_plan_build_cols": (_i32, [_vp, _i32, _i64, _i64, _plan_p, _vp, _i64, _vp, _vp]),
     "ctr_plan_slot_to_unique": (_i32, [_plan_p, _vp, _vp]),
     "ctr_plan_shard_counts": (_i32, [_plan_p, _i64, _i32, _vp, _vp]),
     "ctr_ids_add": (_i32, [_vp, _i64, _i32, _vp]),

@@ -326,267 +326,11 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
   }
 }
 
-// ---- the direct apply (CTR_SEG_DIRECT, fused scatter + Adam): rows inside one chunk are
-// summed by the apply pass itself -------------------------------------------------------
-// 93 % of a C3 batch's unique rows (39 % of its slots) lie inside one 16-position chunk.
-// seg_span_chunk_kernel sums only the runs that SPAN chunks (the chunk's first and last
-// run, when they do) into the chunk partials; positions of rows inside the chunk are
-// skipped after their 8 bytes of plan. seg_apply_direct_kernel then sums each inside-one-
-// chunk row straight from its slots — in position order from zero, exactly seg_chunk's
-// run walk — with the FM term's e = the row's table value it loads for the Adam step
-// anyway, and combines the spanning rows' partials as seg_combine_apply_kernel does. Every
-// sum is the same operations in the same order as ctr_fm_embedding_grad's (bitwise, tested),
-// without the `out` round trip of the inside rows' sums or a per-slot table-row read.
-template <int LPR, int MODE>
-__global__ __launch_bounds__(256) void seg_span_chunk_kernel(SegArgs a) {
-  using VT = float4;
-  constexpr int kChunk = seg_chunk<LPR>();
-  const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR;
-  const int c = threadIdx.x % LPR;
-  const int64_t start = gid * kChunk;
-  if (start >= a.S) return;
-  const bool col = c < a.KV;
-  const int n = (int)min<int64_t>(kChunk, a.S - start);
-  int seg[kChunk], slot[kChunk];
-#pragma unroll
-  for (int i = 0; i < kChunk; ++i) {
-    seg[i] = -1;
-    slot[i] = 0;
-    if (i < n) {
-      slot[i] = a.sorted_slots[start + i];
-      seg[i] = a.pos_seg[start + i];
-    }
-  }
-  const int uf = seg[0], ul = seg[n - 1];
-  const int32_t f0 = a.seg_offsets[uf], f1 = a.seg_offsets[uf + 1];
-  const int32_t l0 = a.seg_offsets[ul], l1 = a.seg_offsets[ul + 1];
-  const bool span_f = f0 / kChunk != (f1 - 1) / kChunk;
-  const bool span_l = ul != uf && l0 / kChunk != (l1 - 1) / kChunk;
-  if (!span_f && !span_l) return;  // lane-group uniform: no spanning row in this chunk
-  VT val[kChunk];
-  float gl[kChunk];
-#pragma unroll
-  for (int i = 0; i < kChunk; ++i) {
-    val[i] = VOps<VT>::zero();
-    gl[i] = 0.f;
-    const bool act = i < n && ((seg[i] == uf && span_f) || (seg[i] == ul && span_l));
-    if (act) {
-      if (MODE == MODE_FM) {
-        const int64_t b = slot[i] / a.F;
-        const float g = a.gz[b];
-        gl[i] = g;
-        if (col) {
-          const int32_t row = a.sorted_rows[start + i];
-          const VT sv = static_cast<const VT*>(a.sum_e)[b * a.KV + c];
-          const VT e = static_cast<const VT*>(a.emb)[(int64_t)row * a.KV + c];
-          const VT d = a.dx ? static_cast<const VT*>(a.dx)[(int64_t)slot[i] * a.KV + c]
-                            : VOps<VT>::zero();
-          val[i] = VOps<VT>::fm(g, sv, e, d);
-        }
-      } else {
-        if (a.vals_lin) gl[i] = a.vals_lin[slot[i]];
-        if (col) val[i] = static_cast<const VT*>(a.vals)[(int64_t)slot[i] * a.KV + c];
-      }
-    }
-  }
-  VT accf = VOps<VT>::zero(), accl4 = VOps<VT>::zero();
-  float af = 0.f, al = 0.f;
-#pragma unroll
-  for (int i = 0; i < kChunk; ++i) {
-    if (i < n) {
-      if (seg[i] == uf) {
-        VOps<VT>::add(accf, val[i]);
-        af += gl[i];
-      } else if (seg[i] == ul) {
-        VOps<VT>::add(accl4, val[i]);
-        al += gl[i];
-      }
-    }
-  }
-  if (span_f) {
-    if (col) static_cast<VT*>(a.part)[(gid * 2) * a.KV + c] = accf;
-    if (c == 0) a.part_lin[gid * 2] = af;
-  }
-  if (span_l) {
-    if (col) static_cast<VT*>(a.part)[(gid * 2 + 1) * a.KV + c] = accl4;
-    if (c == 0) a.part_lin[gid * 2 + 1] = al;
-  }
-}
-
-template <int LPR, int MODE>
-__global__ __launch_bounds__(256) void seg_apply_direct_kernel(SegArgs a) {
-  using VT = float4;
-  constexpr int kChunk = seg_chunk<LPR>();
-  constexpr int G = kWave / LPR;
-  constexpr int T = G < 8 ? 8 : (G > 16 ? 16 : G);
-  __shared__ VT s_sum[4][kWave];
-  __shared__ float s_lin[4][G];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wib = threadIdx.x / kWave;
-  const int g = lane / LPR, c = lane % LPR;
-  const bool col = c < a.KV;
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
-  const int U = *a.num_unique;
-  const int step = *a.step_ptr;
-  const VT* __restrict__ part = static_cast<const VT*>(a.part);
-  const bool lin = a.w != nullptr;
-  for (int64_t u0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave) * G; u0 < U;
-       u0 += waves * G) {
-    const int64_t u = u0 + g;
-    const bool valid = u < U;
-    int32_t off0 = 0, off1 = 1;
-    int64_t r = 0;
-    if (valid) {
-      off0 = a.seg_offsets[u];
-      off1 = a.seg_offsets[u + 1];
-      r = a.unique_rows[u];
-    }
-    // the row's state, in flight with its sums' loads (the FM term's e is its p)
-    int from = 0;
-    VT pp = VOps<VT>::zero(), mm = pp, vv = pp;
-    float pw = 0.f, mws = 0.f, vws = 0.f;
-    if (valid) {
-      from = a.last[r];
-      if (col) {
-        const int64_t e = r * a.KV + c;
-        pp = a.E[e]; mm = a.mE[e]; vv = a.vE[e];
-      }
-      if (lin && c == 0) {
-        pw = a.w[r]; mws = a.mw[r]; vws = a.vw[r];
-      }
-    }
-    const int64_t fs = off0 / kChunk, ls = (off1 - 1) / kChunk;
-    const int P = (int)(ls - fs + 1);
-    const int64_t k0 = fs * 2 + ((off0 % kChunk) == 0 ? 0 : 1);
-    uint64_t big = __ballot(valid && P > T && c == 0);
-    while (big) {
-      const int src = __builtin_ctzll(big);
-      big &= big - 1;
-      const int j = src / LPR;
-      const int Pj = __shfl(P, src, kWave);
-      const int64_t fsj = __shfl((int)fs, src, kWave);
-      const int64_t k0j = __shfl((int)k0, src, kWave);
-      VT acc = VOps<VT>::zero();
-      float accl = 0.f;
-      for (int i = g; i < Pj; i += G) {
-        const int64_t k = i == 0 ? k0j : (fsj + i) * 2;
-        if (col) VOps<VT>::add(acc, part[k * a.KV + c]);
-        accl += a.part_lin[k];
-      }
-#pragma unroll
-      for (int o = LPR; o < kWave; o <<= 1) {
-        VOps<VT>::add(acc, VOps<VT>::shfl_xor(acc, o));
-        accl += __shfl_xor(accl, o, kWave);
-      }
-      if (g == 0) {
-        s_sum[wib][j * LPR + c] = acc;
-        if (c == 0) s_lin[wib][j] = accl;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave-private slots are written
-    __builtin_amdgcn_wave_barrier();
-    if (valid) {
-      VT gr = VOps<VT>::zero();
-      float gl = 0.f;
-      if (P == 1) {  // inside one chunk: its slots in position order (seg_chunk's walk)
-        const int n = off1 - off0;
-        for (int i0 = 0; i0 < n; i0 += 4) {
-          VT v4[4];
-          float g4[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v4[q] = VOps<VT>::zero();
-            g4[q] = 0.f;
-            if (i0 + q < n) {
-              const int32_t sl = a.sorted_slots[off0 + i0 + q];
-              if (MODE == MODE_FM) {
-                const int64_t b = sl / a.F;
-                const float gz = a.gz[b];
-                g4[q] = gz;
-                if (col) {
-                  const VT sv = static_cast<const VT*>(a.sum_e)[b * a.KV + c];
-                  const VT d = a.dx ? static_cast<const VT*>(a.dx)[(int64_t)sl * a.KV + c]
-                                    : VOps<VT>::zero();
-                  v4[q] = VOps<VT>::fm(gz, sv, pp, d);
-                }
-              } else {
-                if (a.vals_lin) g4[q] = a.vals_lin[sl];
-                if (col) v4[q] = static_cast<const VT*>(a.vals)[(int64_t)sl * a.KV + c];
-              }
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (i0 + q < n) {
-              VOps<VT>::add(gr, v4[q]);
-              gl += g4[q];
-            }
-        }
-      } else if (P <= T) {
-        VT acc[G];
-        float accl[G];
-#pragma unroll
-        for (int s2 = 0; s2 < G; ++s2) {
-          acc[s2] = VOps<VT>::zero();
-          accl[s2] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < T; ++i) {
-          if (i < P) {
-            const int64_t k = i == 0 ? k0 : (fs + i) * 2;
-            if (col) VOps<VT>::add(acc[i % G], part[k * a.KV + c]);
-            accl[i % G] += a.part_lin[k];
-          }
-        }
-#pragma unroll
-        for (int w2 = 1; w2 < G; w2 <<= 1)
-#pragma unroll
-          for (int s2 = 0; s2 + w2 < G; s2 += 2 * w2) {
-            VOps<VT>::add(acc[s2], acc[s2 + w2]);
-            accl[s2] += accl[s2 + w2];
-          }
-        gr = acc[0];
-        gl = accl[0];
-      } else {
-        gr = s_sum[wib][g * LPR + c];
-        gl = s_lin[wib][g];
-      }
-      if (a.out_keep) seg_emit<VT>(a, u, c, col, gr, gl);
-      deferred_apply_loaded(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, r, a.KV, c, col, gr, gl,
-                            step, a.tab, a.hp, from, pp, mm, vv, pw, mws, vws);
-    }
-    __builtin_amdgcn_wave_barrier();  // the slots are re-filled by the next iteration
-  }
-}
-
-// CTR_SEG_DIRECT=1: the direct apply (A/B; measured slower end-to-end: C2 45.6 vs 55.8,
-// C3 12.0 vs 12.4 M ex/s); default the chunk pass + combine-apply pair
-static bool seg_direct() {
-  const char* e = getenv("CTR_SEG_DIRECT");
-  return e && e[0] == '1';
-}
-
 template <typename VT, int LPR>
 static int launch_seg_lpr(SegArgs& a, int mode, hipStream_t st) {
   const int64_t n_chunks = ceil_div(a.S, seg_chunk<LPR>());
   const int groups_per_block = 256 / LPR;
   const unsigned g1 = (unsigned)ceil_div(n_chunks, groups_per_block);
-  if constexpr (std::is_same<VT, float4>::value) {
-    if (a.apply && seg_direct()) {  // spanning rows' partials, then sums + apply per row
-      const unsigned gd = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(a.S, 4), 2048));
-      if (mode == MODE_FM) {
-        hipLaunchKernelGGL((seg_span_chunk_kernel<LPR, MODE_FM>), g1, 256, 0, st, a);
-        CTR_LAUNCH_CHECK("seg_span_chunk_kernel");
-        hipLaunchKernelGGL((seg_apply_direct_kernel<LPR, MODE_FM>), gd, 256, 0, st, a);
-      } else {
-        hipLaunchKernelGGL((seg_span_chunk_kernel<LPR, MODE_VALS>), g1, 256, 0, st, a);
-        CTR_LAUNCH_CHECK("seg_span_chunk_kernel");
-        hipLaunchKernelGGL((seg_apply_direct_kernel<LPR, MODE_VALS>), gd, 256, 0, st, a);
-      }
-      CTR_LAUNCH_CHECK("seg_apply_direct_kernel");
-      return CTR_OK;
-    }
-  }
   if (mode == MODE_FM)
     hipLaunchKernelGGL((seg_chunk_kernel<VT, LPR, MODE_FM>), g1, 256, 0, st, a);
   else

@@ -4,6 +4,9 @@
 // rows in ascending order and their segment offsets — bit-identical to numpy's stable
 // argsort + unique (tests/test_gpu_kernels.py).
 //
+// Two builds, the same plan bit for bit: the column plan (ctr_sparse_plan_build_cols, below:
+// a batch's [B][F] ids sorted per column in LDS, then merged — what the trainers use) and the
+// flat LSD plan (ctr_sparse_plan_build: any id vector). The flat plan is an
 // LSD radix sort, 8- or 10-bit digits (plan_bits; 11 for A/B runs), two launches per pass and no
 // inter-workgroup hand-off inside a launch (a cross-XCD look-back chain costs ~1 us per hop
 // on gfx950; a kernel boundary ~1.5 us):
@@ -243,8 +246,10 @@ constexpr int kSegTile = kSortThreads * kSegIPT;
 
 __global__ __launch_bounds__(kSortThreads) void seg_count_kernel(const int32_t* __restrict__ rows,
                                                                  int64_t S,
-                                                                 int32_t* __restrict__ tile_heads) {
+                                                                 int32_t* __restrict__ tile_heads,
+                                                                 const int32_t* __restrict__ skip) {
   __shared__ int32_t s_w[kSortWaves];
+  if (skip && *skip == 0) return;  // the column plan's merge wrote the segments
   const int64_t base = (int64_t)blockIdx.x * kSegTile;
   int32_t c = 0;
 #pragma unroll
@@ -265,8 +270,10 @@ __global__ __launch_bounds__(kSortThreads) void seg_count_kernel(const int32_t* 
 __global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
     const int32_t* __restrict__ rows, int64_t S, const int32_t* __restrict__ tile_heads,
     int n_tiles, int32_t* __restrict__ pos_seg, int32_t* __restrict__ unique_rows,
-    int32_t* __restrict__ seg_offsets, int32_t* __restrict__ num_unique) {
+    int32_t* __restrict__ seg_offsets, int32_t* __restrict__ num_unique,
+    const int32_t* __restrict__ skip) {
   __shared__ int32_t s_w[kSortWaves];
+  if (skip && *skip == 0) return;
   const int t = threadIdx.x;
   // heads in the tiles before this one
   int32_t before = 0;
@@ -310,310 +317,328 @@ __global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
   }
 }
 
-// ------------------------------------------------ plan v2: P + 2 launches ---------------
-// The same stable LSD sort and segments in one launch per pass plus two: a histogram
-// launch (every pass's per-tile digit counts at once, from the ids: a digit's total over
-// the batch does not depend on the order the earlier passes leave), then per pass ONE
-// launch whose blocks take their tile by ticket (arrival order) and get the digit counts
-// of the tiles before theirs from those tiles' own blocks, in the same launch: each block
-// publishes its 256 counts as 8-byte {tag, count} granules (one agent-scope atomic store
-// per digit: the data is the flag, no fence) and reads the granules of every earlier tile,
-// polling the ones not yet tagged. A block only waits for blocks that took earlier
-// tickets, i.e. that are already running, so no residency assumption is made; every spin
-// is bounded (a timeout raises CTR_EFLAG_TIMEOUT and leaves the plan wrong rather than
-// hanging). Segments: one launch, the same hand-off for
-// the head counts. The histogram launch zeroes every granule and ticket the later launches
-// poll (they poll after the kernel boundary), so every build starts from a clean state.
-// Result: bit-identical to the 2-launches-per-pass plan (tests/test_gpu_kernels.py).
-constexpr uint32_t kPlanTimeoutFlag = CTR_EFLAG_TIMEOUT;
-typedef unsigned long long u64g;
+// ------------------------------------------- column plan: 2 launches (+1 that idles) -------
+// The ids of a batch are a [B][F] matrix (slot s = b*F + f) whose columns are the feature
+// fields, and in every CTR layout (the reference's creat_data.py feature offsets, Criteo /
+// Avazu field ranges) each column's ids lie in a range of their own. The stable (row, slot)
+// order of the whole batch is then the concatenation of each column's own stable order, and
+// a column of B <= 8192 ids sorts inside one workgroup's LDS. So:
+//   colplan_sort  one block per run (a column of B <= 8192 ids; 256 / 512 / 1024 threads x 8):
+//                 the run's ids are loaded striped, sorted by a stable LSD radix on
+//                 (row - run min) in LDS — 8-bit digits, only as many passes as the run's
+//                 row range needs, each ranked with wave ballots in (item, wave, lane) order
+//                 as radix_scatter ranks — and written out with each position's ordinal among
+//                 the run's distinct rows; run_info = {min, max, length, distinct rows}.
+//   colplan_merge one thread per slot: its sorted position is its position in its run plus,
+//                 for every other run, how many of that run's (row, slot) keys are smaller —
+//                 the whole run when its max row is below the slot's row, none when its min
+//                 is above, a binary search otherwise (runs whose ranges overlap: any layout
+//                 stays exact). When no two runs' ranges overlap (checked by every block
+//                 from run_info) the segment of a slot is the distinct rows of the runs below
+//                 plus its ordinal in its run, and this launch writes the whole plan;
+//                 otherwise it counts every row's first position into its sorted tile's
+//                 head count (the binary searches tell whether another run holds the row
+//                 at a smaller slot) and leaves flags[0] = 1 for seg_write (which returns at
+//                 once on flags[0] == 0) to turn those counts into the segments.
+// Bit-identical to the LSD plan (tests/test_gpu_kernels.py), no inter-workgroup hand-off.
+constexpr int kColMaxRuns = 256;
+constexpr int kColIPT = 8;  // ids per thread of a column sort (blocks of 256 / 512 / 1024)
 
-struct Plan2Args {
+struct ColArgs {
   const void* idx;
   int idx_type;
-  int64_t V;
-  int64_t S;
-  int n_tiles, n_seg, passes;
-  int32_t* hist;       // [passes][n_tiles][256]
-  u64g* gran;          // [passes][n_tiles][256] {tag = pass + 1, count}
-  u64g* seg_gran;      // [n_seg] {tag = 1, heads}
-  uint32_t* tickets;   // [passes + 1]
-  const uint32_t* keys_in;
-  const int32_t* vals_in;
-  uint32_t* keys_out;
-  int32_t* vals_out;
-  int shift, pass;
-  // segments
-  const int32_t* rows;
-  int32_t *pos_seg, *unique_rows, *seg_offsets, *num_unique;
+  int64_t V, S, B;
+  int F, RM, nc, n_runs;  // run r = (column r / nc, chunk r % nc) of RM rows
+  int32_t* run_rows;      // [S] runs back to back, run r at f*B + c*RM
+  int32_t* run_slots;
+  int32_t* run_seg;
+  int32_t* run_info;      // [n_runs][4]
+  int32_t* tile_heads;    // [ceil(S / kSegTile)]: zeroed by the sort, counted by the merge
+  int32_t* flags;
   int32_t* err;
+  ctr_sparse_plan plan;
 };
 
-__device__ __forceinline__ void plan2_store_gran(u64g* g, uint32_t tag, uint32_t v) {
-  __hip_atomic_store(g, ((u64g)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u64g plan2_load_gran(u64g* g) {
-  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Sum of the counts of granules g[0], g[stride], ... g[(n-1)*stride], each polled until its
-// tag is `tag` (bounded: false on timeout). 8 loads in flight per round.
-__device__ __forceinline__ bool plan2_sum_grans(u64g* g, int n, int64_t stride, uint32_t tag,
-                                                int32_t& sum) {
-  int32_t acc = 0;
-  int spins = 0;
-  for (int t0 = 0; t0 < n; t0 += 8) {
-    u64g v[8];
-    uint32_t ready = 0;
-    for (;;) {
+// block-wide helpers for NW waves (s_w: NW ints)
+template <int NW>
+__device__ __forceinline__ int32_t col_block_reduce(int32_t v, bool is_max, int32_t* s_w) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (!(ready >> q & 1) && t0 + q < n) v[q] = plan2_load_gran(g + (int64_t)(t0 + q) * stride);
-      bool all = true;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (t0 + q >= n || (ready >> q & 1)) continue;
-        if ((uint32_t)(v[q] >> 32) == tag) ready |= 1u << q;
-        else all = false;
-      }
-      if (all) break;
-      if (++spins > (1 << 22)) {
-        sum = acc;
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (t0 + q < n) acc += (int32_t)(uint32_t)v[q];
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const int32_t y = __shfl_xor(v, o, kWave);
+    v = is_max ? max(v, y) : min(v, y);
   }
-  sum = acc;
-  return true;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (lane == 0) s_w[w] = v;
+  __syncthreads();
+  int32_t r = s_w[0];
+#pragma unroll
+  for (int j = 1; j < NW; ++j) r = is_max ? max(r, s_w[j]) : min(r, s_w[j]);
+  __syncthreads();
+  return r;
 }
 
-template <int IPT>
-__global__ __launch_bounds__(kSortThreads) void plan2_hist_kernel(Plan2Args a) {
-  __shared__ int32_t h[4][256];
-  const int t = threadIdx.x;
-  const int tile = blockIdx.x;
-  for (int d = t; d < 4 * 256; d += kSortThreads) (&h[0][0])[d] = 0;
-  // the granules and tickets this build's later launches poll: a clean state every build
-  for (int p = 0; p < a.passes; ++p)
-    a.gran[((int64_t)p * a.n_tiles + tile) * 256 + t] = 0;
-  if (tile < a.n_seg && t == 0) a.seg_gran[tile] = 0;
-  for (int s2 = tile + a.n_tiles * t; s2 < a.n_seg; s2 += a.n_tiles * kSortThreads)
-    if (s2 >= a.n_tiles) a.seg_gran[s2] = 0;
-  if (tile == 0 && t <= a.passes) a.tickets[t] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)tile * (kSortThreads * IPT);
+template <int NW>
+__device__ __forceinline__ int32_t col_block_exscan(int32_t v, int32_t* s_w) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int32_t x = v;
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const int64_t e = base + i * kSortThreads + t;
-    if (e < a.S) {
-      const uint32_t key = a.idx_type == CTR_IDX_I64
-          ? (uint32_t)load_row(static_cast<const int64_t*>(a.idx), e, a.V, a.err)
-          : (uint32_t)load_row(static_cast<const int32_t*>(a.idx), e, a.V, a.err);
-      for (int p = 0; p < a.passes; ++p) atomicAdd(&h[p][(key >> (8 * p)) & 255], 1);
-    }
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
   }
+  if (lane == kWave - 1) s_w[w] = x;
   __syncthreads();
-  for (int p = 0; p < a.passes; ++p)
-    a.hist[((int64_t)p * a.n_tiles + tile) * 256 + t] = h[p][t];
+  int32_t off = 0;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) off += j < w ? s_w[j] : 0;
+  __syncthreads();
+  return off + x - v;
 }
 
-template <int IPT, bool FIRST, bool LAST>
-__global__ __launch_bounds__(kSortThreads) void plan2_pass_kernel(Plan2Args a) {
-  constexpr int R = 256, G = IPT < 8 ? IPT : 8;
-  static_assert(IPT % G == 0, "IPT must be a multiple of the ranking group");
+// One run per block of NT threads x IPT ids (striped: item i of thread t = i*NT + t, so
+// (item, wave, lane) order is slot order). Per 8-bit pass: every item's rank among the
+// equal digits of its wave-instruction by 8 ballots; the (item row, wave) counts of a group
+// of G item rows -> per digit exclusive prefixes carried across groups (no histogram
+// atomics: the counts after the last group ARE the histogram — a Zipf-hot row would
+// serialise LDS atomics on one bin); then the digit bases (a scan of those totals) and the
+// scatter into LDS.
+template <int NT, int IPT>
+__global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
+  constexpr int NW = NT / kWave;
+  constexpr int RM = NT * IPT;
+  constexpr int R = 256;
+  constexpr int G = 2;  // item rows ranked per barrier pair (2 x 2 x NW KB of counts)
+  static_assert(IPT % G == 0, "whole groups");
+  __shared__ uint32_t sk[RM];
+  __shared__ int32_t sv[RM];
   __shared__ int32_t s_base[R];
   __shared__ int32_t s_run[R];
-  __shared__ int32_t s_cnt[G][kSortWaves][R];
-  __shared__ int32_t s_pre[G][kSortWaves][R];
-  __shared__ int32_t s_wtot[kSortWaves];
-  __shared__ int32_t s_h[R];
-  __shared__ int s_tile;
+  __shared__ int32_t s_cnt[G][NW][R];
+  __shared__ int32_t s_pre[G][NW][R];
+  __shared__ int32_t s_w[NW];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
-  if (t == 0)
-    s_tile = (int)__hip_atomic_fetch_add(&a.tickets[a.pass], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-  s_h[t] = 0;
-  __syncthreads();
-  const int tile = s_tile;
-  const int64_t base = (int64_t)tile * (kSortThreads * IPT);
+  const int r = blockIdx.x;
+  const int f = r / a.nc, c = r - f * a.nc;
+  const int64_t b0 = (int64_t)c * RM;
+  for (int64_t j = (int64_t)r * NT + t; j < ceil_div(a.S, (int64_t)kSegTile); j += (int64_t)a.n_runs * NT)
+    a.tile_heads[j] = 0;
+  const int n = (int)min<int64_t>(RM, a.B - b0);
   uint32_t key[IPT];
   int32_t val[IPT];
+  int32_t lo = INT32_MAX, hi = 0;
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
-    const int64_t e = base + i * kSortThreads + t;
+    const int q = i * NT + t;
     key[i] = 0;
     val[i] = 0;
-    if (e < a.S) {
-      if (FIRST) {
-        key[i] = a.idx_type == CTR_IDX_I64
-            ? (uint32_t)load_row(static_cast<const int64_t*>(a.idx), e, a.V, (int32_t*)nullptr)
-            : (uint32_t)load_row(static_cast<const int32_t*>(a.idx), e, a.V, (int32_t*)nullptr);
-        val[i] = (int32_t)e;
-      } else {
-        key[i] = a.keys_in[e];
-        val[i] = a.vals_in[e];
-      }
-      atomicAdd(&s_h[(key[i] >> a.shift) & (R - 1)], 1);
+    if (q < n) {
+      const int64_t slot = (b0 + q) * a.F + f;
+      const int64_t row = a.idx_type == CTR_IDX_I64
+                              ? load_row(static_cast<const int64_t*>(a.idx), slot, a.V, a.err)
+                              : load_row(static_cast<const int32_t*>(a.idx), slot, a.V, a.err);
+      key[i] = (uint32_t)row;
+      val[i] = (int32_t)slot;
+      lo = min(lo, (int32_t)row);
+      hi = max(hi, (int32_t)row);
     }
   }
-  __syncthreads();
-  // this tile's counts, published for the tiles after it
-  u64g* gp = a.gran + (int64_t)a.pass * a.n_tiles * R;
-  plan2_store_gran(gp + (int64_t)tile * R + t, (uint32_t)a.pass + 1, (uint32_t)s_h[t]);
-  // digit totals over the batch (the histogram launch's per-tile counts) and the earlier
-  // tiles' counts (granules of the blocks with earlier tickets), 16 tiles' loads of each in
-  // flight per round
-  int32_t tot = 0, before = 0;
-  {
-    const int32_t* hcol = a.hist + (int64_t)a.pass * a.n_tiles * R + t;
-    u64g* gcol = gp + t;
-    const uint32_t tag = (uint32_t)a.pass + 1;
-    int spins = 0;
-    for (int j0 = 0; j0 < a.n_tiles; j0 += 16) {
-      int32_t hv[16];
-      u64g gv[16];
+  for (int d = t; d < R; d += NT)
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        hv[u] = j0 + u < a.n_tiles ? hcol[(int64_t)(j0 + u) * R] : 0;
-        gv[u] = j0 + u < tile ? plan2_load_gran(gcol + (int64_t)(j0 + u) * R) : 0;
-      }
+    for (int i = 0; i < G; ++i)
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        tot += hv[u];
-        if (j0 + u < tile) {
-          while ((uint32_t)(gv[u] >> 32) != tag) {  // not published yet: poll (bounded)
-            if (++spins > (1 << 22)) {
-              if (a.err) atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            gv[u] = plan2_load_gran(gcol + (int64_t)(j0 + u) * R);
-          }
-          before += (int32_t)(uint32_t)gv[u];
-        }
-      }
-    }
-  }
-  const int32_t start = block_exclusive_scan(tot, s_wtot);
-  s_base[t] = start + before;
-  s_run[t] = 0;
-#pragma unroll
-  for (int i = 0; i < G; ++i)
-#pragma unroll
-    for (int j = 0; j < kSortWaves; ++j) s_cnt[i][j][t] = 0;
-  __syncthreads();
+      for (int j = 0; j < NW; ++j) s_cnt[i][j][d] = 0;
+  lo = col_block_reduce<NW>(lo, false, s_w);
+  hi = col_block_reduce<NW>(hi, true, s_w);
+  const uint32_t span = (uint32_t)(hi - lo);
+  const int bits = span == 0 ? 0 : 32 - __builtin_clz(span);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
-  int32_t pos[IPT];
-#pragma unroll
-  for (int g0 = 0; g0 < IPT; g0 += G) {
-    int rank[G];
-#pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int64_t e = base + (g0 + i) * kSortThreads + t;
-      const bool ok = e < a.S;
-      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
-      uint64_t peers = __ballot(ok);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint64_t m = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? m : ~m;
-      }
-      rank[i] = __popcll(peers & lt);
-      if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
-    }
+  for (int shift = 0; shift < bits; shift += 8) {
+    if (t < R) s_run[t] = 0;
     __syncthreads();
-    {
-      int32_t run = s_run[t];
+    int32_t loc[IPT];
 #pragma unroll
-      for (int i = 0; i < G; ++i)
+    for (int g0 = 0; g0 < IPT; g0 += G) {
+      int rank[G];
 #pragma unroll
-        for (int j = 0; j < kSortWaves; ++j) {
-          const int32_t c = s_cnt[i][j][t];
-          s_pre[i][j][t] = run;
-          s_cnt[i][j][t] = 0;
-          run += c;
+      for (int i = 0; i < G; ++i) {
+        const bool ok = (g0 + i) * NT + t < n;
+        const uint32_t d = ((key[g0 + i] - (uint32_t)lo) >> shift) & (R - 1);
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+          const uint64_t m = __ballot((d >> bb) & 1u);
+          peers &= ((d >> bb) & 1u) ? m : ~m;
         }
-      s_run[t] = run;
+        rank[i] = __popcll(peers & lt);
+        if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
+      }
+      __syncthreads();
+      for (int d = t; d < R; d += NT) {  // digit d: prefix over (item row, wave), after s_run
+        int32_t run = s_run[d];
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+#pragma unroll
+          for (int j = 0; j < NW; ++j) {
+            const int32_t cn = s_cnt[i][j][d];
+            s_pre[i][j][d] = run;
+            s_cnt[i][j][d] = 0;
+            run += cn;
+          }
+        s_run[d] = run;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const uint32_t d = ((key[g0 + i] - (uint32_t)lo) >> shift) & (R - 1);
+        loc[g0 + i] = s_pre[i][w][d] + rank[i];
+      }
+    }
+    // s_run = the pass's digit histogram: bases by one scan of it
+    {
+      const int32_t h = t < R ? s_run[t] : 0;
+      const int32_t ex = col_block_exscan<NW>(h, s_w);
+      if (t < R) s_base[t] = ex;
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
-      const int64_t e = base + (g0 + i) * kSortThreads + t;
-      const uint32_t d = (key[g0 + i] >> a.shift) & (R - 1);
-      pos[g0 + i] = e < a.S ? s_base[d] + s_pre[i][w][d] + rank[i] : -1;
+    for (int i = 0; i < IPT; ++i)
+      if (i * NT + t < n) {
+        const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
+        const int p = s_base[d] + loc[i];
+        sk[p] = key[i];
+        sv[p] = val[i];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int q = i * NT + t;
+      if (q < n) {
+        key[i] = sk[q];
+        val[i] = sv[q];
+      }
     }
+    __syncthreads();
   }
+  if (bits == 0) {  // one row value: already in slot order
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int q = i * NT + t;
+      if (q < n) {
+        sk[q] = key[i];
+        sv[q] = val[i];
+      }
+    }
+    __syncthreads();
+  }
+  // blocked: thread t writes positions [t*IPT, (t+1)*IPT) with their distinct-row ordinals
+  const int q0 = t * IPT;
+  int32_t cnt = 0;
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
-    if (pos[i] >= 0) {
-      a.keys_out[pos[i]] = key[i];
-      a.vals_out[pos[i]] = val[i];
+    const int q = q0 + i;
+    cnt += (q < n && (q == 0 || sk[q] != sk[q - 1])) ? 1 : 0;
+  }
+  const int32_t ex = col_block_exscan<NW>(cnt, s_w);
+  int32_t u = ex - 1;
+  const int64_t off = (int64_t)f * a.B + b0;
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int q = q0 + i;
+    if (q < n) {
+      const uint32_t k = sk[q];
+      u += (q == 0 || k != sk[q - 1]) ? 1 : 0;
+      a.run_rows[off + q] = (int32_t)k;
+      a.run_slots[off + q] = sv[q];
+      a.run_seg[off + q] = u;
     }
   }
+  if (t == NT - 1) reinterpret_cast<int4*>(a.run_info)[r] = make_int4(lo, hi, n, ex + cnt);
 }
 
-__global__ __launch_bounds__(kSortThreads) void plan2_seg_kernel(Plan2Args a) {
-  __shared__ int32_t s_w[kSortWaves];
-  __shared__ int s_tile;
-  __shared__ int32_t s_before;
+// the (row, slot) keys of run [o, o + len) smaller than (row, slot): binary search
+__device__ __forceinline__ int32_t colplan_rank_in(const ColArgs& a, int64_t o, int32_t len,
+                                                   int32_t row, int32_t slot) {
+  int32_t lo = 0, hi = len;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    const int32_t rm = a.run_rows[o + mid];
+    const bool less = rm < row || (rm == row && a.run_slots[o + mid] < slot);
+    if (less) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kSortThreads) void colplan_merge_kernel(ColArgs a) {
+  __shared__ int4 s_info[kColMaxRuns];
+  __shared__ int s_overlap;
   const int t = threadIdx.x;
-  if (t == 0)
-    s_tile = (int)__hip_atomic_fetch_add(&a.tickets[a.passes], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+  const int nr = a.n_runs;
+  if (t == 0) s_overlap = 0;
+  for (int g = t; g < nr; g += kSortThreads) s_info[g] = reinterpret_cast<const int4*>(a.run_info)[g];
   __syncthreads();
-  const int tile = s_tile;
-  const int64_t s0 = (int64_t)tile * kSegTile + (int64_t)t * kSegIPT;
-  int32_t r[kSegIPT];
-  bool head[kSegIPT];
-  int32_t cnt = 0;
-  int32_t prev = (s0 > 0 && s0 - 1 < a.S) ? a.rows[s0 - 1] : -1;
-#pragma unroll
-  for (int i = 0; i < kSegIPT; ++i) {
-    const int64_t s = s0 + i;
-    r[i] = s < a.S ? a.rows[s] : -1;
-    head[i] = s < a.S && (s == 0 || r[i] != prev);
-    prev = r[i];
-    cnt += head[i] ? 1 : 0;
-  }
-  const int32_t ex = block_exclusive_scan(cnt, s_w);
-  if (t == kSortThreads - 1) {
-    plan2_store_gran(a.seg_gran + tile, 1u, (uint32_t)(ex + cnt));
-  }
-  // heads of the tiles before this one: every thread sums a strided share of their
-  // granules (up to 256 in flight at once), then a block reduction
   {
-    int32_t part = 0;
-    bool ok = true;
-    for (int j = t; j < tile; j += kSortThreads) {
-      int32_t v = 0;
-      ok &= plan2_sum_grans(a.seg_gran + j, 1, 1, 1u, v);
-      part += v;
+    bool ov = false;
+    for (int g = t; g < nr; g += kSortThreads) {
+      const int4 x = s_info[g];
+      for (int h = g + 1; h < nr; ++h) {
+        const int4 y = s_info[h];
+        ov |= !(x.y < y.x || y.y < x.x);
+      }
     }
-    if (!ok && a.err) atomicOr(a.err, (int32_t)kPlanTimeoutFlag);
-    const int32_t pex = block_exclusive_scan(part, s_w);
-    if (t == kSortThreads - 1) s_before = pex + part;
+    if (ov) s_overlap = 1;  // benign race: every writer stores 1
   }
   __syncthreads();
-  int32_t u = s_before + ex - 1;
-#pragma unroll
-  for (int i = 0; i < kSegIPT; ++i) {
-    const int64_t s = s0 + i;
-    if (s < a.S) {
-      if (head[i]) {
-        ++u;
-        a.unique_rows[u] = r[i];
-        a.seg_offsets[u] = (int32_t)s;
-      }
-      a.pos_seg[s] = u;
-      if (s == a.S - 1) {
-        *a.num_unique = u + 1;
-        a.seg_offsets[u + 1] = (int32_t)a.S;
-      }
+  const bool disjoint = s_overlap == 0;
+  const int64_t e = (int64_t)blockIdx.x * kSortThreads + t;
+  if (blockIdx.x == 0 && t == 0) {
+    a.flags[0] = disjoint ? 0 : 1;
+    if (disjoint) {
+      int32_t U = 0;
+      for (int g = 0; g < nr; ++g) U += s_info[g].w;
+      *a.plan.num_unique = U;
+      a.plan.seg_offsets[U] = (int32_t)a.S;
     }
+  }
+  if (e >= a.S) return;
+  const int f = (int)(e / a.B);
+  const int64_t wi = e - (int64_t)f * a.B;
+  const int c = (int)(wi / a.RM);
+  const int p = (int)(wi - (int64_t)c * a.RM);
+  const int r = f * a.nc + c;
+  const int32_t row = a.run_rows[e], slot = a.run_slots[e];
+  int64_t pos = p;
+  int32_t segb = 0;
+  bool first_elsewhere = false;  // another run holds this row at a smaller slot
+  for (int g = 0; g < nr; ++g) {
+    if (g == r) continue;
+    const int4 x = s_info[g];
+    if (x.y < row) {
+      pos += x.z;
+      segb += x.w;
+    } else if (x.x <= row) {
+      const int gf = g / a.nc, gc = g - gf * a.nc;
+      const int64_t o = (int64_t)gf * a.B + (int64_t)gc * a.RM;
+      const int32_t below = colplan_rank_in(a, o, x.z, row, slot);
+      pos += below;
+      first_elsewhere |= below > 0 && a.run_rows[o + below - 1] == row;
+    }
+  }
+  a.plan.sorted_rows[pos] = row;
+  a.plan.sorted_slots[pos] = slot;
+  const bool local_head = p == 0 || a.run_rows[e - 1] != row;
+  if (disjoint) {
+    const int32_t seg = segb + a.run_seg[e];
+    a.plan.pos_seg[pos] = seg;
+    if (local_head) {
+      a.plan.unique_rows[seg] = row;
+      a.plan.seg_offsets[seg] = (int32_t)pos;
+    }
+  } else if (local_head && !first_elsewhere) {
+    // the first position of its row over every run: count it in its sorted tile (integer
+    // adds, order-free), seg_write turns the tile counts into the segments
+    atomicAdd(&a.tile_heads[pos / kSegTile], 1);
   }
 }
 
@@ -754,9 +779,8 @@ struct PlanLayout {
   int32_t* vals[2];
   int32_t* hist;
   int32_t* tile_heads;
-  u64g* gran;       // plan v2: [4][n_tiles][256]
-  u64g* seg_gran;   // plan v2: [n_seg]
-  uint32_t* tickets;
+  int32_t* run_info;  // column plan: [n_runs][4] {min row, max row, length, unique rows}
+  int32_t* flags;     // column plan: [0] = 1 while the segment launches still have work
   size_t total;
 };
 
@@ -774,69 +798,28 @@ static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
     L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
     L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
   }
-  // histograms sized for the widest digit (the plan's buffers do not know V); plan v2: one
-  // 256-bin histogram per pass (up to 4 passes of 8 bits)
-  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * std::max<int64_t>(Radix<11>::kBins, 4 * 256) * n_tiles));
+  // histograms sized for the widest digit (the plan's buffers do not know V)
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles));
   L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
-  L->gran = reinterpret_cast<u64g*>(take(sizeof(u64g) * 4 * 256 * n_tiles));
-  L->seg_gran = reinterpret_cast<u64g*>(take(sizeof(u64g) * n_seg));
-  L->tickets = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * 8));
+  // column plan: a run per (column, chunk of <= 8192 rows), at most kColMaxRuns
+  L->run_info = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4 * kColMaxRuns));
+  L->flags = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 64));
   L->total = off;
   return off;
 }
 
-// CTR_PLAN_V2=0: the two-launches-per-pass plan (A/B); default: v2
-static bool plan_v2() {
-  const char* e = getenv("CTR_PLAN_V2");
-  return !(e && e[0] == '0');
-}
-
-template <int IPT>
-static int run_plan_v2(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
-                       PlanLayout& L, int passes, int32_t* err, hipStream_t st) {
-  const int64_t S = plan->S;
-  Plan2Args a;
-  memset(&a, 0, sizeof(a));
-  a.idx = idx;
-  a.idx_type = idx_type;
-  a.V = V;
-  a.S = S;
-  a.n_tiles = (int)ceil_div(S, kSortThreads * IPT);
-  a.n_seg = (int)ceil_div(S, kSegTile);
-  a.passes = passes;
-  a.hist = L.hist;
-  a.gran = L.gran;
-  a.seg_gran = L.seg_gran;
-  a.tickets = L.tickets;
-  a.err = err;
-  const unsigned grid = (unsigned)a.n_tiles;
-  hipLaunchKernelGGL((plan2_hist_kernel<IPT>), grid, kSortThreads, 0, st, a);
-  CTR_LAUNCH_CHECK("plan2_hist_kernel");
-  for (int p = 0; p < passes; ++p) {
-    const bool first = p == 0, last = p == passes - 1;
-    a.pass = p;
-    a.shift = 8 * p;
-    a.keys_in = first ? nullptr : L.keys[(p - 1) & 1];
-    a.vals_in = first ? nullptr : L.vals[(p - 1) & 1];
-    a.keys_out = last ? reinterpret_cast<uint32_t*>(plan->sorted_rows) : L.keys[p & 1];
-    a.vals_out = last ? plan->sorted_slots : L.vals[p & 1];
-    if (first && last)
-      hipLaunchKernelGGL((plan2_pass_kernel<IPT, true, true>), grid, kSortThreads, 0, st, a);
-    else if (first)
-      hipLaunchKernelGGL((plan2_pass_kernel<IPT, true, false>), grid, kSortThreads, 0, st, a);
-    else if (last)
-      hipLaunchKernelGGL((plan2_pass_kernel<IPT, false, true>), grid, kSortThreads, 0, st, a);
-    else
-      hipLaunchKernelGGL((plan2_pass_kernel<IPT, false, false>), grid, kSortThreads, 0, st, a);
-    CTR_LAUNCH_CHECK("plan2_pass_kernel");
-  }
-  a.rows = plan->sorted_rows;
-  a.pos_seg = plan->pos_seg;
-  a.unique_rows = plan->unique_rows;
-  a.seg_offsets = plan->seg_offsets;
-  a.num_unique = plan->num_unique;
-  hipLaunchKernelGGL(plan2_seg_kernel, (unsigned)a.n_seg, kSortThreads, 0, st, a);
-  CTR_LAUNCH_CHECK("plan2_seg_kernel");
+template <int NT>
+static int run_colplan(ColArgs& a, const PlanLayout& L, hipStream_t st) {
+  hipLaunchKernelGGL((colplan_sort_kernel<NT, kColIPT>), (unsigned)a.n_runs, NT, 0, st, a);
+  CTR_LAUNCH_CHECK("colplan_sort_kernel");
+  hipLaunchKernelGGL(colplan_merge_kernel, (unsigned)ceil_div(a.S, kSortThreads), kSortThreads, 0,
+                     st, a);
+  CTR_LAUNCH_CHECK("colplan_merge_kernel");
+  const unsigned gs = (unsigned)ceil_div(a.S, kSegTile);
+  hipLaunchKernelGGL(seg_write_kernel, gs, kSortThreads, 0, st, a.plan.sorted_rows, a.S,
+                     L.tile_heads, (int)gs, a.plan.pos_seg, a.plan.unique_rows,
+                     a.plan.seg_offsets, a.plan.num_unique, a.flags);
+  CTR_LAUNCH_CHECK("seg_write_kernel");
   return CTR_OK;
 }
 
@@ -912,15 +895,6 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
     return CTR_ERR_WORKSPACE;
   }
   const int ipt = plan_ipt(S);
-  if (plan_v2()) {  // 8-bit digits: one histogram launch + one per pass + one for segments
-    const int passes = (int)ceil_div(key_bits(V), 8);
-    switch (ipt) {
-      case 4: return run_plan_v2<4>(idx, idx_type, V, plan, L, passes, err_flag, st);
-      case 8: return run_plan_v2<8>(idx, idx_type, V, plan, L, passes, err_flag, st);
-      case 16: return run_plan_v2<16>(idx, idx_type, V, plan, L, passes, err_flag, st);
-      default: return run_plan_v2<32>(idx, idx_type, V, plan, L, passes, err_flag, st);
-    }
-  }
   RadixPass a;
   memset(&a, 0, sizeof(a));
   a.idx = idx;
@@ -951,13 +925,65 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   if (rc != CTR_OK) return rc;
   const unsigned gs = (unsigned)ceil_div(S, kSegTile);
   hipLaunchKernelGGL(seg_count_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,
-                     L.tile_heads);
+                     L.tile_heads, nullptr);
   CTR_LAUNCH_CHECK("seg_count_kernel");
   hipLaunchKernelGGL(seg_write_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,
                      L.tile_heads, (int)gs, plan->pos_seg, plan->unique_rows, plan->seg_offsets,
-                     plan->num_unique);
+                     plan->num_unique, nullptr);
   CTR_LAUNCH_CHECK("seg_write_kernel");
   return CTR_OK;
+}
+
+extern "C" int ctr_sparse_plan_build_cols(const void* idx, int idx_type, int64_t V, int64_t F,
+                                          const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,
+                                          int32_t* err_flag, ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_sparse_plan_build_cols: incomplete plan");
+  CTR_REQUIRE(F > 0 && plan->S % F == 0, "ctr_sparse_plan_build_cols: S %% F != 0");
+  const int64_t S = plan->S, B = S / std::max<int64_t>(F, 1);
+  const int nt = B <= 2048 ? 256 : B <= 4096 ? 512 : 1024;  // threads of a run's block
+  const int RM = nt * kColIPT;
+  const int64_t nc = S == 0 ? 0 : ceil_div(B, (int64_t)RM);
+  // one run per column (a column of <= 8192 ids sorts in one block; chunks of a longer
+  // column would overlap, and the merge's binary searches grow with the overlapping runs),
+  // the run table in one block's LDS: otherwise the LSD plan
+  if (S == 0 || nc > 1 || F > kColMaxRuns)
+    return ctr_sparse_plan_build(idx, idx_type, V, plan, ws, ws_bytes, err_flag, stream);
+  CTR_REQUIRE(idx, "ctr_sparse_plan_build_cols: null idx");
+  CTR_REQUIRE(V > 0 && V < (int64_t(1) << 31) && S < (int64_t(1) << 24),
+              "ctr_sparse_plan_build_cols: bad sizes (need V < 2^31, S < 2^24)");
+  CTR_REQUIRE(idx_type == CTR_IDX_I32 || idx_type == CTR_IDX_I64, "bad idx_type %d", idx_type);
+  PlanLayout L;
+  const size_t need = plan_layout(S, static_cast<char*>(ws), &L);
+  if (!ws || ws_bytes < (int64_t)need) {
+    set_error("ctr_sparse_plan_build_cols: workspace %lld < %lld bytes", (long long)ws_bytes,
+              (long long)need);
+    return CTR_ERR_WORKSPACE;
+  }
+  ColArgs a;
+  memset(&a, 0, sizeof(a));
+  a.idx = idx;
+  a.idx_type = idx_type;
+  a.V = V;
+  a.S = S;
+  a.B = B;
+  a.F = (int)F;
+  a.RM = RM;
+  a.nc = (int)nc;
+  a.n_runs = (int)(F * nc);
+  a.run_rows = reinterpret_cast<int32_t*>(L.keys[0]);
+  a.run_slots = L.vals[0];
+  a.run_seg = reinterpret_cast<int32_t*>(L.keys[1]);
+  a.run_info = L.run_info;
+  a.tile_heads = L.tile_heads;
+  a.flags = L.flags;
+  a.err = err_flag;
+  a.plan = *plan;
+  hipStream_t st = as_stream(stream);
+  switch (nt) {
+    case 256: return run_colplan<256>(a, L, st);
+    case 512: return run_colplan<512>(a, L, st);
+    default: return run_colplan<1024>(a, L, st);
+  }
 }
 
 extern "C" int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique,

@@ -7,13 +7,14 @@ an error, never a silent fallback.
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes
 import threading
 from dataclasses import dataclass
 
 import torch
 
-from ._lib import (CTR_EFLAG_CAPACITY, CTR_EFLAG_INDEX, CTR_EFLAG_TIMEOUT, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
+from ._lib import (CTR_EFLAG_CAPACITY, CTR_EFLAG_INDEX, CTR_IDX_I32, CTR_IDX_I64, EPI_BIAS, EPI_BIAS_RELU,
                    EPI_BIAS_RELU_DROP, EPI_GRAD_MASK, EPI_NONE, PlanesDesc, PlaneViewDesc, SparsePlan,
                    lib)
 
@@ -133,9 +134,6 @@ def check_index_error(err_flag: torch.Tensor) -> None:
     if v & CTR_EFLAG_CAPACITY:  # a library invariant broke (the host sizes the capacity)
         err_flag.zero_()
         raise RuntimeError("row-sharded exchange: a run exceeded its capacity")
-    if v & CTR_EFLAG_TIMEOUT:  # a bounded in-launch hand-off gave up: results are invalid
-        err_flag.zero_()
-        raise RuntimeError("sparse plan: an in-launch hand-off timed out")
     if v & CTR_EFLAG_INDEX:
         err_flag.zero_()
         raise IndexError("index out of range in self")
@@ -457,6 +455,10 @@ def transpose(src: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
 
 
 # ---------------------------------------------------------------- scatter-add -------
+# CTR_PLAN_COLS=0: the LSD plan for [B, F] ids too (A/B)
+_PLAN_COLS = os.environ.get("CTR_PLAN_COLS", "1") != "0"
+
+
 class SparsePlanBuffers:
     """Device buffers of a ctr_sparse_plan for up to `capacity` slots."""
 
@@ -490,6 +492,9 @@ class SparsePlanBuffers:
         return s
 
     def build(self, idx: torch.Tensor, V: int, err_flag=None) -> "SparsePlanBuffers":
+        """idx [B, F] (a batch: the column plan, ctr_sparse_plan_build_cols) or flat ids
+        (the LSD plan); both give the same plan bit for bit."""
+        F = int(idx.shape[1]) if idx.dim() == 2 and _PLAN_COLS else 0
         idx, it = _idx(idx)
         S = idx.numel()
         if S > self.capacity:
@@ -504,8 +509,12 @@ class SparsePlanBuffers:
                                    "these buffers once eagerly first)")
             full = lib.ctr_sparse_plan_workspace_bytes(max(self.capacity, 1), int(V))
             self._ws = torch.empty(max(need, full, 256), dtype=torch.uint8, device=self.device)
-        lib.ctr_sparse_plan_build(_p(idx), it, int(V), self.struct(), _p(self._ws),
-                                  self._ws.numel(), _p(err_flag), _stream())
+        if F > 0:
+            lib.ctr_sparse_plan_build_cols(_p(idx), it, int(V), F, self.struct(), _p(self._ws),
+                                           self._ws.numel(), _p(err_flag), _stream())
+        else:
+            lib.ctr_sparse_plan_build(_p(idx), it, int(V), self.struct(), _p(self._ws),
+                                      self._ws.numel(), _p(err_flag), _stream())
         return self
 
     def num_unique_host(self) -> int:

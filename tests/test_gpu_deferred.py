@@ -103,18 +103,14 @@ def test_graph_replay_equals_eager_bitwise(cuda, kind, mode):
             assert torch.equal(ste[i][k], stg[i][k]), (i, k)
 
 
-@pytest.mark.parametrize("direct", ["1", "0"])
 @pytest.mark.parametrize("kind,K", [("FM", 16), ("FM", 32), ("DeepFM", 32), ("DeepFM", 64),
                                     ("IPNN", 32), ("IPNN", 64)])
-def test_fused_scatter_apply_equals_unfused(cuda, kind, K, direct, monkeypatch):
+def test_fused_scatter_apply_equals_unfused(cuda, kind, K):
     """The segmented sums with the Adam apply fused in (ctr_fm_embedding_grad_adam /
     ctr_segment_sum_rows_adam) == the separate sums + ctr_adam_deferred_rows, bitwise — the
     tables, the moments and (keep_grads) the per-row sums — on Zipf batches whose hot rows
     span many chunks. K 16 / 32 / 64: 16 / 8 / 4 rows per wave in the fused pass, so both
-    of its spanning-row paths (a row's own lane group, the whole wave for hot rows) run.
-    direct = 1 (opt-in): the rows inside one chunk summed by the apply pass itself
-    (seg_span_chunk + seg_apply_direct); 0 (default): the chunk pass + combine-apply pair."""
-    monkeypatch.setenv("CTR_SEG_DIRECT", direct)
+    of its spanning-row paths (a row's own lane group, the whole wave for hot rows) run."""
     import rl_ctr_prediction_amd as P
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
     V, F, B = 200_000, 26, 2048

@@ -20,7 +20,15 @@ def _hip():
     return hip_ops
 
 
-def _ids(rng, B, F, V, hot=True):
+def _ids(rng, B, F, V, hot=True, layout="uniform"):
+    """uniform: every column draws from [0, V) (column ranges overlap: the column plan's
+    binary-search merge and segment launches); fields: column f draws from a range of its
+    own, [f*card, (f+1)*card) with Zipf-skewed values (the CTR layout: the merge writes the
+    whole plan)."""
+    if layout == "fields":
+        card = V // F
+        x = np.minimum(rng.zipf(1.2, size=(B, F)) - 1, card - 1) + np.arange(F) * card
+        return x
     x = rng.integers(0, V, size=(B, F))
     if hot and B > 1 and F > 2:
         x[:, 0] = min(7, V - 1)
@@ -34,15 +42,19 @@ def _ids(rng, B, F, V, hot=True):
                                    (8192, 26, 10_000_000), (20165, 26, 2),
                                    (65536, 26, 40_000_000), (777, 22, 2**31 - 1)])
 @pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
-@pytest.mark.parametrize("v2", ["1", "0"])
-def test_sparse_plan_bit_exact(cuda, B, F, V, dtype, v2, monkeypatch):
-    """v2 = 1 (default): histogram + one launch per pass (tiles by ticket, the earlier tiles'
-    counts by in-launch granule hand-off) + one segment launch; 0: two launches per pass."""
-    monkeypatch.setenv("CTR_PLAN_V2", v2)
+@pytest.mark.parametrize("layout", ["uniform", "fields"])
+@pytest.mark.parametrize("cols", [True, False])
+def test_sparse_plan_bit_exact(cuda, B, F, V, dtype, layout, cols):
+    """cols: [B, F] ids (the column plan, ctr_sparse_plan_build_cols: per-column LDS sorts +
+    merge; B > 8192 falls back to the LSD plan); else the flat ids
+    (the LSD plan). Both bit-exact vs numpy's stable argsort / unique."""
+    if layout == "fields" and V < 2 * F:
+        pytest.skip("fields need V >= 2F")
     H = _hip()
     rng = np.random.default_rng(B * 31 + F)
-    x = _ids(rng, B, F, V)
-    plan = H.SparsePlanBuffers(B * F, cuda).build(torch.tensor(x, dtype=dtype, device=cuda), V)
+    x = _ids(rng, B, F, V, layout=layout)
+    xt = torch.tensor(x, dtype=dtype, device=cuda)
+    plan = H.SparsePlanBuffers(B * F, cuda).build(xt if cols else xt.reshape(-1), V)
     order, rows, pos_seg, uniq, off = O.sparse_plan(x)
     U = plan.num_unique_host()
     assert U == uniq.size
@@ -54,12 +66,14 @@ def test_sparse_plan_bit_exact(cuda, B, F, V, dtype, v2, monkeypatch):
 
 
 def test_sparse_plan_rebuilds_and_graph_replay(cuda):
-    """The same plan buffers rebuilt for different batches (every build resets the hand-off
-    state it polls), eagerly and as a replayed HIP graph, stay bit-exact; no timeout flag."""
+    """The same plan buffers rebuilt for batches of both layouts in turn (the column plan's
+    merge decides per build whether the segment launches run), eagerly and as a replayed
+    HIP graph, stay bit-exact; no error flag."""
     H = _hip()
     rng = np.random.default_rng(5)
     B, F, V = 4096, 26, 1_000_000
-    xs = [torch.tensor(_ids(rng, B, F, V), device=cuda) for _ in range(4)]
+    xs = [torch.tensor(_ids(rng, B, F, V, layout=("fields", "uniform")[j % 2]), device=cuda)
+          for j in range(4)]
     ids = torch.empty_like(xs[0])
     err = torch.zeros(1, dtype=torch.int32, device=cuda)
     plan = H.SparsePlanBuffers(B * F, cuda)
@@ -86,6 +100,32 @@ def test_sparse_plan_rebuilds_and_graph_replay(cuda):
         np.testing.assert_array_equal(plan.pos_seg.cpu().numpy()[: B * F], pos_seg)
         np.testing.assert_array_equal(plan.seg_offsets.cpu().numpy()[: U + 1], off)
     assert int(err.item()) == 0
+
+
+@pytest.mark.parametrize("layout", ["uniform", "fields"])
+def test_sparse_plan_invalid_ids(cuda, layout):
+    """Ids outside [0, V) raise the index flag and are grouped as row 0 by both builds
+    (nn.Embedding raises before any update; the trainers check the flag)."""
+    H = _hip()
+    rng = np.random.default_rng(9)
+    B, F, V = 1000, 26, 100_000
+    x = _ids(rng, B, F, V, layout=layout)
+    x[5, 3], x[700, 20], x[999, 25] = -1, V, V + 77
+    xt = torch.tensor(x, device=cuda)
+    out = []
+    for ids in (xt, xt.reshape(-1)):
+        err = torch.zeros(1, dtype=torch.int32, device=cuda)
+        plan = H.SparsePlanBuffers(B * F, cuda).build(ids, V, err_flag=err)
+        assert int(err.item()) & 1
+        U = plan.num_unique_host()
+        out.append([t.cpu().numpy().copy() for t in (plan.sorted_slots, plan.sorted_rows,
+                    plan.pos_seg)] + [plan.unique_rows[:U].cpu().numpy(),
+                                      plan.seg_offsets[:U + 1].cpu().numpy()])
+    xf = np.where((x < 0) | (x >= V), 0, x)
+    ref = O.sparse_plan(xf)
+    for got in out:
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a[:b.size], b)
 
 
 def test_sparse_plan_empty(cuda):

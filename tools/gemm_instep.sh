@@ -9,6 +9,6 @@ while IFS='|' read -r name cfg; do
   OUT=gpurun_out/instep_$name
   mkdir -p $OUT
   CTR_GEMM_PLANES_SHAPE_CFG="$cfg" timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- \
-    python3 bench.py --config c3 --steps 30 --warmup 3 --no-cpu-baseline > $OUT/bench.log 2>&1 || exit $?
+    python3 bench.py --config c3 --steps 30 --warmup 3 --no-cpu-baseline --no-driver-loop > $OUT/bench.log 2>&1 || exit $?
   echo "$name $(tail -1 $OUT/bench.log | grep -o '"value": [0-9.]*')"
 done <<< "$VARIANTS"

@@ -2,7 +2,8 @@
 
     python tools/plan_bench.py [--configs c2,c3,c5] [--n 200]
 
-Prints one JSON line per config: us per build, slots S, unique rows U, and a bit-exact
+Prints one JSON line per config and build (the column plan on the [B, F] ids, the LSD plan
+on the flat ids): us per build, slots S, unique rows U, and a bit-exact
 check of the plan against numpy's stable argsort / unique on the same batch.
 """
 from __future__ import annotations
@@ -28,11 +29,13 @@ def main():
     from rl_ctr_prediction_amd import hip_ops as H
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
     dev = torch.device("cuda:0")
-    for name in a.configs.split(","):
+    for name, cols in [(n, c) for n in a.configs.split(",") for c in (True, False)]:
         cfg = bench.CONFIGS[name]
         V, F, B = cfg["V"], cfg["F"], cfg["B"]
         x_np, _ = next(CriteoSynth(V, F, seed=1).batches(1, B))
         x = torch.from_numpy(x_np).to(dev)
+        if not cols:  # flat ids: the LSD plan
+            x = x.reshape(-1)
         P = H.SparsePlanBuffers(B * F, dev)
         P.build(x, V)
         torch.cuda.synchronize()
@@ -56,7 +59,7 @@ def main():
             g.replay()
         torch.cuda.synchronize()
         us = (time.perf_counter() - t0) / a.n * 1e6
-        print(json.dumps({"config": name, "us_per_build": us, "S": int(flat.size),
+        print(json.dumps({"config": name, "build": "columns" if cols else "lsd", "us_per_build": us, "S": int(flat.size),
                           "U": int(P.num_unique_host()), "bit_exact": bool(ok)}), flush=True)
 
 

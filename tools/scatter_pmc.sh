@@ -24,5 +24,5 @@ run() {  # $1 = tag, rest = program
 for C in $CFGS; do
   run alone_$C python3 tools/scatter_bench.py --config $C --reps 10 || exit 1
 done
-run step_c3 python3 bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline || exit 1
+run step_c3 python3 bench.py --config c3 --steps 5 --warmup 2 --no-cpu-baseline --no-driver-loop || exit 1
 python3 tools/scatter_pmc_summary.py $OUT | tee $OUT/summary.txt

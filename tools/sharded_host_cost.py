@@ -2,18 +2,18 @@
 
     python tools/sharded_host_cost.py [--config c3|c2] [--steps 20]
 
-At N = 1 the sharded step is the N > 1 launch sequence with every collective a local copy,
-so its captured HIP graph's node count is the per-step launch count of the eager N > 1 step
-minus its collectives (4 equal-split all-to-alls of ids / rows / gradients (+2 for the linear
-table) and one all-reduce of the dense gradient, plus the capacity all-reduce on its own
-stream). Prints one JSON line: graph nodes per step (hipGraphGetNodes on the captured step),
-host ms per step of eager steps (use_graphs off: every launch issued from Python, as at
-N > 1 by default) and of graph-replayed steps.
+At N = 1 the sharded step is the N > 1 launch sequence with every collective a local copy.
+Prints one JSON line: host ms per step of eager steps (use_graphs off: every launch issued
+from Python, as at N > 1 by default) and of graph-replayed steps, and the wall ms per step of
+each. The launch count per step comes from a kernel trace of the same run
+(rocprofv3 --kernel-trace, then tools/timeline.py --marker step_end_kernel: the kernels
+between two step ends; the N > 1 step adds its collectives: 4 equal-split all-to-alls of
+ids / rows / gradients (+2 for the linear table), one all-reduce of the dense gradient, and
+the capacity all-reduce on its own stream).
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import sys
 import time
@@ -25,19 +25,11 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
-def graph_nodes(g) -> int:
-    hip = ctypes.CDLL("libamdhip64.so")
-    n = ctypes.c_size_t(0)
-    rc = hip.hipGraphGetNodes(ctypes.c_void_p(g.raw_cuda_graph()), None, ctypes.byref(n))
-    if rc != 0:
-        raise RuntimeError(f"hipGraphGetNodes: {rc}")
-    return int(n.value)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=["c2", "c3"])
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--modes", default="eager,graphs")
     args = ap.parse_args()
     import bench
     import rl_ctr_prediction_amd as P
@@ -50,7 +42,7 @@ def main():
     xs = [torch.from_numpy(x).to(dev) for x, _ in host]
     ys = [torch.from_numpy(y).to(dev) for _, y in host]
     res = {"config": args.config}
-    for graphs in (False, True):
+    for graphs in [m == "graphs" for m in args.modes.split(",")]:
         torch.manual_seed(1)
         with torch.device(dev):
             m = P.FM(V, K) if cfg["kind"] == "FM" else P.DeepFM(V, F, K)
@@ -71,9 +63,6 @@ def main():
         key = "graphs" if graphs else "eager"
         res[f"{key}_host_ms_per_step"] = t_host / args.steps * 1e3
         res[f"{key}_ms_per_step"] = (time.perf_counter() - t0) / args.steps * 1e3
-        if graphs:
-            g = next(iter(tr._graphs.values()))[0]
-            res["graph_nodes_per_step"] = graph_nodes(g)
         del tr, m
     print(json.dumps(res), flush=True)
 

@@ -59,10 +59,11 @@ def main():
     for s, e, q, n in seg:
         print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {(e - t0) / 1e3:8.1f} {q:>2}  {n}")
     print()
-    print("per step: wall / busy (us)")
-    for j, t0, t1, busy, _ in steps:
-        print(f"  {j:3d} {(t1 - t0) / 1e3:8.1f} {busy / 1e3:8.1f}")
-    print(f"median wall {statistics.median(walls) / 1e3:.1f} us")
+    print("per step: wall / busy (us), kernels launched")
+    for j, t0, t1, busy, sg in steps:
+        print(f"  {j:3d} {(t1 - t0) / 1e3:8.1f} {busy / 1e3:8.1f} {len(sg):5d}")
+    print(f"median wall {statistics.median(walls) / 1e3:.1f} us, "
+          f"median kernels per step {statistics.median(len(s[4]) for s in steps)}")
 
 
 if __name__ == "__main__":
