@@ -421,7 +421,8 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   const int r = blockIdx.x;
   const int f = r / a.nc, c = r - f * a.nc;
   const int64_t b0 = (int64_t)c * RM;
-  for (int64_t j = (int64_t)r * NT + t; j < ceil_div(a.S, (int64_t)kSegTile); j += (int64_t)a.n_runs * NT)
+  const int64_t n_seg = (a.S + kSegTile - 1) / kSegTile;
+  for (int64_t j = (int64_t)r * NT + t; j < n_seg; j += (int64_t)a.n_runs * NT)
     a.tile_heads[j] = 0;
   const int n = (int)min<int64_t>(RM, a.B - b0);
   uint32_t key[IPT];
