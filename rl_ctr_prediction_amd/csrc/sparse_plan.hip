@@ -324,11 +324,11 @@ __global__ __launch_bounds__(kSortThreads) void seg_write_kernel(
 // order of the whole batch is then the concatenation of each column's own stable order, and
 // a column of B <= 8192 ids sorts inside one workgroup's LDS. So:
 //   colplan_sort  one block per run (a column of B <= 8192 ids; 256 / 512 / 1024 threads x 8):
-//                 the run's ids are loaded striped, sorted by a stable LSD radix on
-//                 (row - run min) in LDS — 8-bit digits, only as many passes as the run's
-//                 row range needs, each ranked with wave ballots in (item, wave, lane) order
-//                 as radix_scatter ranks — and written out with each position's ordinal among
-//                 the run's distinct rows; run_info = {min, max, length, distinct rows}.
+//                 the run's ids sorted by a stable LSD radix on (row - run min) in LDS —
+//                 8-bit digits, only as many passes as the run's row range needs, each
+//                 ranked with wave ballots, the ids blocked by wave — and written out with
+//                 each position's ordinal among the run's distinct rows;
+//                 run_info = {min, max, length, distinct rows}.
 //   colplan_merge one thread per slot: its sorted position is its position in its run plus,
 //                 for every other run, how many of that run's (row, slot) keys are smaller —
 //                 the whole run when its max row is below the slot's row, none when its min
@@ -395,42 +395,39 @@ __device__ __forceinline__ int32_t col_block_exscan(int32_t v, int32_t* s_w) {
   return off + x - v;
 }
 
-// One run per block of NT threads x IPT ids (striped: item i of thread t = i*NT + t, so
-// (item, wave, lane) order is slot order). Per 8-bit pass: every item's rank among the
-// equal digits of its wave-instruction by 8 ballots; the (item row, wave) counts of a group
-// of G item rows -> per digit exclusive prefixes carried across groups (no histogram
-// atomics: the counts after the last group ARE the histogram — a Zipf-hot row would
-// serialise LDS atomics on one bin); then the digit bases (a scan of those totals) and the
-// scatter into LDS.
+// One run per block of NT threads x IPT ids, BLOCKED by wave: wave w holds the run's ids
+// [w*IPT*64, (w+1)*IPT*64), item i of lane l being id w*IPT*64 + i*64 + l — so (wave, item,
+// lane) order is slot order. Per 8-bit pass each wave ranks its items in order with no
+// barrier: 8 ballots give an item's equal-digit peers in its wave-instruction, its place
+// is the wave's running count of that digit (a wave-private LDS histogram) plus its rank
+// among the peers, and the peer group's lowest lane adds the group to the histogram. Then
+// one barrier, the digit bases (a scan of the digit totals) and per digit the waves'
+// exclusive prefix, one barrier, the scatter into LDS. 4 barriers per pass.
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   constexpr int NW = NT / kWave;
   constexpr int RM = NT * IPT;
+  constexpr int WR = IPT * kWave;  // ids per wave
   constexpr int R = 256;
-  constexpr int G = 2;  // item rows ranked per barrier pair (2 x 2 x NW KB of counts)
-  static_assert(IPT % G == 0, "whole groups");
   __shared__ uint32_t sk[RM];
   __shared__ int32_t sv[RM];
-  __shared__ int32_t s_base[R];
-  __shared__ int32_t s_run[R];
-  __shared__ int32_t s_cnt[G][NW][R];
-  __shared__ int32_t s_pre[G][NW][R];
+  __shared__ int32_t s_wh[NW][R];  // per wave: running digit counts, then its bases
   __shared__ int32_t s_w[NW];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
   const int r = blockIdx.x;
   const int f = r / a.nc, c = r - f * a.nc;
   const int64_t b0 = (int64_t)c * RM;
+  const int n = (int)min<int64_t>(RM, a.B - b0);
   const int64_t n_seg = (a.S + kSegTile - 1) / kSegTile;
   for (int64_t j = (int64_t)r * NT + t; j < n_seg; j += (int64_t)a.n_runs * NT)
     a.tile_heads[j] = 0;
-  const int n = (int)min<int64_t>(RM, a.B - b0);
   uint32_t key[IPT];
   int32_t val[IPT];
   int32_t lo = INT32_MAX, hi = 0;
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
-    const int q = i * NT + t;
+    const int q = w * WR + i * kWave + lane;
     key[i] = 0;
     val[i] = 0;
     if (q < n) {
@@ -444,87 +441,77 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
       hi = max(hi, (int32_t)row);
     }
   }
-  for (int d = t; d < R; d += NT)
-#pragma unroll
-    for (int i = 0; i < G; ++i)
-#pragma unroll
-      for (int j = 0; j < NW; ++j) s_cnt[i][j][d] = 0;
   lo = col_block_reduce<NW>(lo, false, s_w);
   hi = col_block_reduce<NW>(hi, true, s_w);
   const uint32_t span = (uint32_t)(hi - lo);
   const int bits = span == 0 ? 0 : 32 - __builtin_clz(span);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
+  int32_t* wh = s_wh[w];
   for (int shift = 0; shift < bits; shift += 8) {
-    if (t < R) s_run[t] = 0;
-    __syncthreads();
+    for (int d = lane; d < R; d += kWave) wh[d] = 0;  // wave-private: no barrier
     int32_t loc[IPT];
 #pragma unroll
-    for (int g0 = 0; g0 < IPT; g0 += G) {
-      int rank[G];
+    for (int i = 0; i < IPT; ++i) {
+      const bool ok = w * WR + i * kWave + lane < n;
+      const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
+      uint64_t peers = __ballot(ok);
 #pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const bool ok = (g0 + i) * NT + t < n;
-        const uint32_t d = ((key[g0 + i] - (uint32_t)lo) >> shift) & (R - 1);
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int bb = 0; bb < 8; ++bb) {
-          const uint64_t m = __ballot((d >> bb) & 1u);
-          peers &= ((d >> bb) & 1u) ? m : ~m;
-        }
-        rank[i] = __popcll(peers & lt);
-        if (ok && rank[i] == 0) s_cnt[i][w][d] = __popcll(peers);
+      for (int bb = 0; bb < 8; ++bb) {
+        const uint64_t m = __ballot((d >> bb) & 1u);
+        peers &= ((d >> bb) & 1u) ? m : ~m;
       }
-      __syncthreads();
-      for (int d = t; d < R; d += NT) {  // digit d: prefix over (item row, wave), after s_run
-        int32_t run = s_run[d];
-#pragma unroll
-        for (int i = 0; i < G; ++i)
-#pragma unroll
-          for (int j = 0; j < NW; ++j) {
-            const int32_t cn = s_cnt[i][j][d];
-            s_pre[i][j][d] = run;
-            s_cnt[i][j][d] = 0;
-            run += cn;
-          }
-        s_run[d] = run;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const uint32_t d = ((key[g0 + i] - (uint32_t)lo) >> shift) & (R - 1);
-        loc[g0 + i] = s_pre[i][w][d] + rank[i];
-      }
+      const int rank = __popcll(peers & lt);
+      const int32_t before = ok ? wh[d] : 0;
+      loc[i] = before + rank;
+      __builtin_amdgcn_wave_barrier();
+      if (ok && rank == 0) wh[d] = before + __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
     }
-    // s_run = the pass's digit histogram: bases by one scan of it
+    __syncthreads();
+    // digit d: its total over the waves -> base of the digit (scan of the totals), then
+    // each wave's base = digit base + the earlier waves' counts
     {
-      const int32_t h = t < R ? s_run[t] : 0;
-      const int32_t ex = col_block_exscan<NW>(h, s_w);
-      if (t < R) s_base[t] = ex;
+      int32_t tot = 0;
+      if (t < R)
+#pragma unroll
+        for (int j = 0; j < NW; ++j) tot += s_wh[j][t];
+      const int32_t base = col_block_exscan<NW>(tot, s_w);  // (barriers inside)
+      if (t < R) {
+        int32_t run = base;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+          const int32_t cn = s_wh[j][t];
+          s_wh[j][t] = run;
+          run += cn;
+        }
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < IPT; ++i)
-      if (i * NT + t < n) {
+      if (w * WR + i * kWave + lane < n) {
         const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
-        const int p = s_base[d] + loc[i];
+        const int p = wh[d] + loc[i];
         sk[p] = key[i];
         sv[p] = val[i];
       }
     __syncthreads();
+    if (shift + 8 < bits) {  // the next pass ranks in the new order (the last leaves it in LDS)
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const int q = i * NT + t;
-      if (q < n) {
-        key[i] = sk[q];
-        val[i] = sv[q];
+      for (int i = 0; i < IPT; ++i) {
+        const int q = w * WR + i * kWave + lane;
+        if (q < n) {
+          key[i] = sk[q];
+          val[i] = sv[q];
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
   if (bits == 0) {  // one row value: already in slot order
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const int q = i * NT + t;
+      const int q = w * WR + i * kWave + lane;
       if (q < n) {
         sk[q] = key[i];
         sv[q] = val[i];
