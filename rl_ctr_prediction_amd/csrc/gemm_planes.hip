@@ -585,12 +585,6 @@ static const PlDef kPl[] = {
     {256, 64, 4, 2, 2, 1, 0.60},   // 26: 120 KB (dW1: M = 200)
     {192, 64, 4, 2, 2, 1, 0.60},   // 27: 96 KB
     {320, 64, 2, 2, 2, 1, 0.60},   // 28: 144 KB, 4 waves (TM 10)
-    // tall tiles for the wide-N backward products (dX: M = B, N = 1664, K = 300): fewer,
-    // larger blocks, each operand tile read by fewer blocks (half the LDS-DMA fill per flop
-    // of the 64 x 64 tiles); 8 waves in a column, each 32 x BN (KC A only: A tiles of 256)
-    {256, 128, 8, 1, 2, 1, 0.70},  // 29: 147 KB, 1 block per CU
-    {256, 64, 8, 1, 2, 1, 0.65},   // 30: 123 KB
-    {128, 128, 8, 1, 2, 1, 0.65},  // 31: 96 KB
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -602,7 +596,6 @@ struct PlCfg {
 
 static bool pl_valid(int ti, bool a_rc, bool b_rc) {
   const PlDef& d = kPl[ti];
-  if (a_rc && ti >= 29) return false;  // the tall tilings: KC A only
   return (!a_rc || d.bm == 128 || d.bm % 64 == 0) && (!b_rc || d.bn == 128 || d.bn % 64 == 0);
 }
 
@@ -720,8 +713,8 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   PlCfg best = mk(0, 1);
   double best_t = 1e30;
   for (int ti = 0; ti < kNumPl; ++ti) {
-    // the model: KS = 1 only, not the tall tilings (chosen by measurement, above)
-    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1 || ti >= 29) continue;
+    // the model: KS = 1 only
+    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1) continue;
     const PlDef& d = kPl[ti];
     const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
     for (int s = 1; s <= 32; ++s) {
@@ -755,9 +748,6 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   else if (!b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, true, false, KS);      \
   else CTR_PL_K(BM, BN, WMW, WNW, NS, true, true, KS);
 #define CTR_PL_ALL4(BM, BN, WMW, WNW, NS) CTR_PL_ALL4K(BM, BN, WMW, WNW, NS, 1)
-#define CTR_PL_KCA(BM, BN, WMW, WNW, NS)                            \
-  if (!b_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false, 1);       \
-  else CTR_PL_K(BM, BN, WMW, WNW, NS, false, true, 1);
 #define CTR_PL_AONLY(BM, BN, WMW, WNW, NS)                          \
   if (!a_rc) CTR_PL_K(BM, BN, WMW, WNW, NS, false, false, 1);       \
   else CTR_PL_K(BM, BN, WMW, WNW, NS, true, false, 1);
@@ -794,13 +784,9 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 26: CTR_PL_ALL4(256, 64, 4, 2, 2) break;
     case 27: CTR_PL_ALL4(192, 64, 4, 2, 2) break;
     case 28: CTR_PL_ALL4(320, 64, 2, 2, 2) break;
-    case 29: CTR_PL_KCA(256, 128, 8, 1, 2) break;
-    case 30: CTR_PL_KCA(256, 64, 8, 1, 2) break;
-    case 31: CTR_PL_KCA(128, 128, 8, 1, 2) break;
   }
 }
 #undef CTR_PL_AONLY
-#undef CTR_PL_KCA
 #undef CTR_PL_ALL4
 #undef CTR_PL_ALL4K
 #undef CTR_PL_K

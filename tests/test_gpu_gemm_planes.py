@@ -17,10 +17,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-N_TILES = 32
+N_TILES = 29
 # tilings whose B operand must be KC (160 is not an RC tile width)
 AONLY = {0, 6, 8, 9}
-KCA = {29, 30, 31}  # tall tilings: KC A only
 
 
 def _H():
@@ -118,7 +117,7 @@ def test_gemm_planes_every_tiling(cuda, tile, monkeypatch):
             bound = A.double().abs() @ Bm.double().abs()
             for a_rc in (False, True):
                 for b_rc in (False, True):
-                    if (b_rc and tile in AONLY) or (a_rc and tile in KCA):
+                    if b_rc and tile in AONLY:
                         continue
                     cfg = H.gemm_planes_config(a_rc, b_rc, M, N, K)
                     assert cfg["tile"] == tile and cfg["splits"] == splits, cfg
