@@ -673,12 +673,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     return c;
   }
   if (!a_rc && b_rc && M >= 2048) return mk(7, 1);
-  static const int wide_wg = [] {  // 0 off, 1 (default) wide operands of N >= 768, 2 any N
-    const char* e = getenv("CTR_GEMM_PLANES_WIDE");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
-  }();
-  if (wide_wg && a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320 &&
-      (wide_wg == 2 || N >= 768)) {
+  if (a_rc && b_rc && Kp >= 2048 && M > 128 && M <= 320 && N >= 768) {
     // whole-M tile (the wide operand read once), split-K to about one block per CU.
     // Standalone (operands MALL-warm) it is no faster than 64x64 tiles (dW0 71 vs 66 us
     // with the compiler's transpose reads); in the step, where dW0 runs beside the scatter
@@ -686,21 +681,16 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     // 64-row M tile measured C3 11.94 -> 12.32 M ex/s (12.48 -> 12.75 with plan lookahead;
     // two alternating runs each). Not for narrower N: the policy net's 256 x 512 weight
     // gradient (C4) measured 8.49 wide vs 8.72 M transitions/s on the 64x64 tiles.
-    // CTR_GEMM_PLANES_WIDE=0: the 64x64 tiles everywhere; 2: wide for any N
     const int ti = M <= 192 ? 27 : M <= 256 ? 26 : 25;
     const int64_t tiles = ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(256 / tiles, Kp / 256), 64));
     return mk(ti, s);
   }
   if (a_rc && b_rc && Kp >= 2048) {
-    // target block count of the weight-gradient GEMMs (A/B: CTR_GEMM_PLANES_WG_BLOCKS):
-    // ~1170 (4.5 per CU) with the split-major XCD map — measured dW0 (130 tiles) 9 splits
-    // 66 us vs 4 splits 73, dW1 (20 tiles) 24-32 splits 22.5-23 us vs 16 24
-    static const int64_t wg_blocks = [] {
-      const char* e = getenv("CTR_GEMM_PLANES_WG_BLOCKS");
-      const long v = e ? atol(e) : 0;
-      return (int64_t)(v >= 64 && v <= 8192 ? v : 1170);
-    }();
+    // target block count of the weight-gradient GEMMs: ~1170 (4.5 per CU) with the
+    // split-major XCD map — measured dW0 (130 tiles) 9 splits 66 us vs 4 splits 73, dW1
+    // (20 tiles) 24-32 splits 22.5-23 us vs 16 24
+    constexpr int64_t wg_blocks = 1170;
     const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(
                       ceil_div(wg_blocks, tiles), Kp / 256), 64));

@@ -7,7 +7,7 @@
 // Two builds, the same plan bit for bit: the column plan (ctr_sparse_plan_build_cols, below:
 // a batch's [B][F] ids sorted per column in LDS, then merged — what the trainers use) and the
 // flat LSD plan (ctr_sparse_plan_build: any id vector). The flat plan is an
-// LSD radix sort, 8- or 10-bit digits (plan_bits; 11 for A/B runs), two launches per pass and no
+// LSD radix sort, 8-bit digits (kPlanBits), two launches per pass and no
 // inter-workgroup hand-off inside a launch (a cross-XCD look-back chain costs ~1 us per hop
 // on gfx950; a kernel boundary ~1.5 us):
 //   radix_hist:    per tile (256 threads x IPT keys) the 256-bin digit histogram, LDS
@@ -28,9 +28,7 @@ namespace ctr {
 constexpr int kSortThreads = 256;
 constexpr int kSortWaves = kSortThreads / kWave;
 
-// Digit width: 8 bits (256 bins) or 11 bits (2048 bins). The plan picks the width that
-// needs fewer passes for the key range (V = 1M: 20 bits = 3 x 8 or 2 x 11; V = 10M: 24 bits
-// = 3 x 8 = 3 x 11, so 8): one pass less is two launches less on a latency-bound path.
+// Digit width (8 bits = 256 bins: kPlanBits below).
 template <int BITS>
 struct Radix {
   static constexpr int kBins = 1 << BITS;
@@ -741,26 +739,12 @@ static int key_bits(int64_t V) {
 
 // Items per thread: 8 (2048-key tiles) while that keeps the per-block histogram scan short
 // (<= 256 tiles); larger batches (data-parallel gathered plans) use 32 (8192-key tiles).
-static int plan_ipt(int64_t S) {
-  if (const char* env = getenv("CTR_PLAN_IPT")) {  // A/B runs
-    const int v = atoi(env);
-    if (v == 4 || v == 8 || v == 16 || v == 32) return v;
-  }
-  return S <= 256 * 2048 ? 8 : 32;
-}
+static int plan_ipt(int64_t S) { return S <= 256 * 2048 ? 8 : 32; }
 
-// digit width for a key range: 11 bits where that takes fewer passes than 8
-static int plan_bits(int64_t V) {
-  if (const char* env = getenv("CTR_PLAN_BITS")) {  // A/B runs
-    const int b = atoi(env);
-    if (b == 8 || b == 10 || b == 11) return b;
-  }
-  // 8 bits: measured on MI355X (tools/plan_ab2.sh, us per plan), wider digits save a pass
-  // but each pass costs more than the pass saved — 10 bits: C2 (V = 1M, 2 vs 3 passes)
-  // 53.7 vs 55.0, C5 (V = 40M, 3 vs 4 passes) 85.0 vs 75.6; 11 bits: C2 69
-  (void)V;
-  return 8;
-}
+// Digits of 8 bits: measured on MI355X (tools/plan_ab2.sh, us per plan, round 2), wider
+// digits save a pass but each pass costs more than the pass saved — 10 bits: C2 (V = 1M, 2
+// vs 3 passes) 53.7 vs 55.0, C5 (V = 40M, 3 vs 4 passes) 85.0 vs 75.6; 11 bits: C2 69
+constexpr int kPlanBits = 8;
 
 struct PlanLayout {
   uint32_t* keys[2];
@@ -786,8 +770,7 @@ static size_t plan_layout(int64_t S, char* base, PlanLayout* L) {
     L->keys[j] = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * S));
     L->vals[j] = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * S));
   }
-  // histograms sized for the widest digit (the plan's buffers do not know V)
-  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<11>::kBins * n_tiles));
+  L->hist = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * Radix<kPlanBits>::kBins * n_tiles));
   L->tile_heads = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * n_seg));
   // column plan: a run per (column, chunk of <= 8192 rows), at most kColMaxRuns
   L->run_info = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4 * kColMaxRuns));
@@ -892,24 +875,9 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   a.S = S;
   a.n_tiles = (int)ceil_div(S, kSortThreads * ipt);
   a.err = err_flag;
-  const int bits = plan_bits(V);
-  const int passes = (int)ceil_div(key_bits(V), bits);
-  int rc;
-  if (bits == 10)
-    rc = ipt == 4 ? run_passes<4, 10>(a, passes, plan, L, st)
-       : ipt == 8 ? run_passes<8, 10>(a, passes, plan, L, st)
-       : ipt == 16 ? run_passes<16, 10>(a, passes, plan, L, st)
-                  : run_passes<32, 10>(a, passes, plan, L, st);
-  else if (bits == 11)
-    rc = ipt == 4 ? run_passes<4, 11>(a, passes, plan, L, st)
-       : ipt == 8 ? run_passes<8, 11>(a, passes, plan, L, st)
-       : ipt == 16 ? run_passes<16, 11>(a, passes, plan, L, st)
-                  : run_passes<32, 11>(a, passes, plan, L, st);
-  else
-    rc = ipt == 4 ? run_passes<4, 8>(a, passes, plan, L, st)
-       : ipt == 8 ? run_passes<8, 8>(a, passes, plan, L, st)
-       : ipt == 16 ? run_passes<16, 8>(a, passes, plan, L, st)
-                  : run_passes<32, 8>(a, passes, plan, L, st);
+  const int passes = (int)ceil_div(key_bits(V), kPlanBits);
+  const int rc = ipt == 8 ? run_passes<8, kPlanBits>(a, passes, plan, L, st)
+                          : run_passes<32, kPlanBits>(a, passes, plan, L, st);
   if (rc != CTR_OK) return rc;
   const unsigned gs = (unsigned)ceil_div(S, kSegTile);
   hipLaunchKernelGGL(seg_count_kernel, gs, kSortThreads, 0, st, plan->sorted_rows, S,

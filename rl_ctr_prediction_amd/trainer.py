@@ -229,13 +229,6 @@ class FusedCTRTrainer:
         self.max_slots = 8
         self.captures = 0          # step graphs captured (tests: bounded, batch-independent)
         self._ev_start = None
-        self._dw0_fork = os.environ.get("CTR_DW0_FORK", "dx")
-        self._db0_last = os.environ.get("CTR_DB0_LAST", "0") == "1"
-        # the weight-gradient side list: "ones" (default) — dW1 alone from the head; from dX
-        # on the column-sum pair (loss, FM bias, mlp.6) then dW0 with db0 as its ones-column
-        # output (the MLP input planes carry a ones column, as H1's do for db1); "colsum" —
-        # the column-sum pair and dW1 from the head, db0 by its own column sum before dW0
-        self._wgrad_order = os.environ.get("CTR_WGRAD_ORDER", "ones")
         # lookahead (every kind): the next batches' ids are staged and planned on the plan
         # stream, so the step graph starts with no copy and no plan branch, and catches its
         # rows up over the plan's unique rows in one launch. FM: C2 35.5 -> 50.9 M ex/s; C3
@@ -249,13 +242,6 @@ class FusedCTRTrainer:
         # of fresh batches (0: only at forward / state_dict / epoch end)
         self.flush_every = int(os.environ.get("CTR_FLUSH_EVERY", "32"))
         self._flushed_at = 0
-        # FM's dense tail fused into one launch (ctr_fm_step_tail); CTR_FM_TAIL=0: the four
-        # separate launches (A/B)
-        self.fm_tail = os.environ.get("CTR_FM_TAIL", "1") != "0"
-        # a step whose plan was built ahead catches its rows up over the plan's unique rows
-        # (ctr_adam_deferred_rows, one launch) instead of marking owners from the ids first
-        # (CTR_CATCHUP_BY_PLAN=0: the id-driven pair, A/B)
-        self.catchup_by_plan = os.environ.get("CTR_CATCHUP_BY_PLAN", "1") != "0"
         self._vec_ok = self.K % 4 == 0 and 64 % (self.K // 4 or 1) == 0 and self.K <= 256
         # every stream of this trainer has a HIP handle of its own (_new_stream): the scratch
         # buffers of hip_ops.Workspace are per stream handle, and torch hands streams out of
@@ -296,11 +282,10 @@ class FusedCTRTrainer:
         # C2 two streams 50.5 / 54.8 / 53.4 vs one 50.5 / 48.9 / 47.3 M ex/s (alternating
         # runs, tools/c2_knobs3.sh); while the host paced the step one stream measured faster
         self.n_plan_streams = int(os.environ.get("CTR_PLAN_STREAMS", "2"))
-        # which plan stream a staged batch's copy + plan run on: "seq" — alternate in staging
-        # order, so two consecutive plans never queue on one stream (with a ring of three
-        # slots, the slot-index rule put slots 0 and 2 on one stream: their plans ran back to
-        # back, two in one step and none in the next); "slot" — the slot's own stream
-        self._plan_stream_by = os.environ.get("CTR_PLAN_STREAM_BY", "seq")
+        # a staged batch's copy + plan alternate over the plan streams in staging order, so
+        # two consecutive plans never queue on one stream (with a ring of three slots, a
+        # slot-index rule put slots 0 and 2 on one stream: their plans ran back to back, two
+        # in one step and none in the next)
         self._stage_seq = 0
         self._extra_plan_streams: list = []
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
@@ -474,7 +459,7 @@ class FusedCTRTrainer:
             # H1 carries a ones column in its padding: dW1 then returns the bias gradient
             # db1 = colsum dH2 as one more output column
             # ... and so does the MLP input X (db0 = colsum dH1 from dW0, CTR_WGRAD_ORDER)
-            b.xp = P(B, W, dev, ones_col=self._wgrad_order == "ones")
+            b.xp = P(B, W, dev, ones_col=True)
             b.h1p = P(B, H1, dev, ones_col=True)
             b.dh2p, b.dh1p = P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
@@ -670,14 +655,11 @@ class FusedCTRTrainer:
         self._staged[key] = s
 
     def _stage_stream(self, s: InputSlot):
-        """The plan stream of the next staged batch (slot s): see _plan_stream_by. Every
+        """The plan stream of the next staged batch (slot s), in staging order. Every
         slot owns its buffers and plan scratch, so any plan stream may serve it; the slot's
         readers wait for its staging event, whichever stream recorded it."""
-        if self._plan_stream_by == "slot":
-            s.stage_stream = self._slot_stream(s.stream_i)
-        else:
-            s.stage_stream = self._slot_stream(self._stage_seq % max(1, self.n_plan_streams))
-            self._stage_seq += 1
+        s.stage_stream = self._slot_stream(self._stage_seq % max(1, self.n_plan_streams))
+        self._stage_seq += 1
         return s.stage_stream
 
     def _slot_event(self, s: InputSlot):
@@ -795,7 +777,7 @@ class FusedCTRTrainer:
             if self.plan_first:
                 plan()
             t = self._mark("catchup")
-            if have_plan and self.catchup_by_plan:
+            if have_plan:
                 # the plan built ahead lists the batch's unique rows: one launch over
                 # them instead of the owner-marking pass + the id-driven catch-up
                 hip_ops.adam_deferred_rows(E, self.m_E, self.v_E, w, self.m_w, self.v_w,
@@ -831,7 +813,7 @@ class FusedCTRTrainer:
             gz = self._deepfm_forward_backward(x, y, b, E, w, bias, mean_div)
         # FM, one process: the bias gradient, the batch loss, the dense Adam and the step
         # counter in one launch at the end of the step (ctr_fm_step_tail)
-        tail = self.kind == "FM" and ws == 1 and self.fm_tail and self._wplanes is None
+        tail = self.kind == "FM" and ws == 1 and self._wplanes is None
         if self.kind == "FM" and not tail:  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         if self._side is not None and not have_plan:
@@ -1001,7 +983,6 @@ class FusedCTRTrainer:
         H1, H2, W = b.h1.shape[1], b.h2.shape[1], b.dx.shape[1]
         if side is not None:
             side.wait_event(b.ev_head)
-        ones = self._wgrad_order == "ones" and b.xp.ones_col
         with torch.cuda.stream(side) if side is not None else _nullctx():
             jobs = [(b.fm.loss_elem.view(B, 1), None, b.loss, 1.0 / B)]  # batch mean BCE
             if "bias" in gv:  # DeepFM's FM bias: sum gz
@@ -1009,30 +990,19 @@ class FusedCTRTrainer:
             # Linear(200,1): dW = gz^T H2, db = sum gz
             jobs += [(b.h2, gz, gv["mlp.6.weight"].view(-1)),
                      (gz.view(B, 1), None, gv["mlp.6.bias"].view(1))]
-            if not ones:
-                hip_ops.colsum_multi(jobs)
             # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2 (H1's ones column)
             self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B,
                               out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
-            if side is not None:  # from dX on (CTR_DW0_FORK=dh1: from dH1 on, A/B)
-                side.wait_event(b.ev_dh1 if self._dw0_fork == "dh1" else b.ev_dx)
-            if ones:
-                # the column-sum pair here, ahead of dW0: seg_chunk takes the CUs before dW0
-                # does (the role db0's own column sum played), and db0 = colsum dH1 comes out
-                # of dW0 as the ones column of X
-                hip_ops.colsum_multi(jobs)
-                self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
-                                  out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
-                return
-            # Linear(F*K,300): db0 = colsum dH1, dW0 = dH1^T X. The column sum stays here:
-            # it lets seg_chunk take the CUs before dW0 does (measured at C3 with db0 moved
-            # before the dX fork: dW0 and seg_chunk start together, seg_chunk 38 -> 106 us,
-            # the step +20 us; CTR_DB0_LAST=1: after dW0, A/B)
-            if not self._db0_last:
-                hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
-            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B, out=gv["mlp.0.weight"])
-            if self._db0_last:
-                hip_ops.colsum(b.dh1, out=gv["mlp.0.bias"])
+            if side is not None:  # from dX on
+                side.wait_event(b.ev_dx)
+            # the column-sum pair here, ahead of dW0: seg_chunk takes the CUs before dW0
+            # does (measured at C3: db0's column sum moved before the dX fork let dW0 and
+            # seg_chunk start together, seg_chunk 38 -> 106 us, the step +20 us); and
+            # Linear(F*K,300)'s db0 = colsum dH1 comes out of dW0 = dH1^T X as the ones
+            # column of X
+            hip_ops.colsum_multi(jobs)
+            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
+                              out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""
