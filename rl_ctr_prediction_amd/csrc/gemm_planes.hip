@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
                        m0 + wm0, n0 + wn0, lane, split);
 }
 
-// split-K: sum the fp32 slabs in split order (4 independent loads in flight per step of
+// split-K: sum the fp32 slabs in split order (8 independent loads in flight per step of
 // the chain), then the epilogue (fp32 out and/or planes); one thread per 4 columns
 // slabs: [splits][M][sld], sld = align_up(N, 4) (the padding columns are never read as
 // results), so every row starts 16-B aligned and the float4 path always applies
@@ -471,15 +471,17 @@ __global__ __launch_bounds__(64) void planes_reduce_kernel(PlanesArgs a, const f
     if (vec) {
       float4 s = *reinterpret_cast<const float4*>(slabs + o);
       int z = 1;
-      for (; z + 3 < splits; z += 4) {
-        const float4 v1 = *reinterpret_cast<const float4*>(slabs + (int64_t)z * slab + o);
-        const float4 v2 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 1) * slab + o);
-        const float4 v3 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 2) * slab + o);
-        const float4 v4 = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + 3) * slab + o);
-        s.x += v1.x; s.y += v1.y; s.z += v1.z; s.w += v1.w;
-        s.x += v2.x; s.y += v2.y; s.z += v2.z; s.w += v2.w;
-        s.x += v3.x; s.y += v3.y; s.z += v3.z; s.w += v3.w;
-        s.x += v4.x; s.y += v4.y; s.z += v4.z; s.w += v4.w;
+      // 8 slabs' loads in flight per step of the (ordered) sum chain: the weight-gradient
+      // reduces run 9-32 slabs, so 4 in flight left them latency-bound (dW1's at C3 12 us)
+      for (; z + 7 < splits; z += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + j) * slab + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w;
+        }
       }
       for (; z < splits; ++z) {
         const float4 v = *reinterpret_cast<const float4*>(slabs + (int64_t)z * slab + o);

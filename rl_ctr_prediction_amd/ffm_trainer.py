@@ -30,7 +30,7 @@ import torch.nn as nn
 
 from . import hip_ops
 from .p_model import FFM
-from .trainer import flush_hooks, graph_capture
+from .trainer import flush_hooks, graph_capture, live_pool
 
 
 @dataclass
@@ -257,7 +257,7 @@ class FusedFFMTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
+                with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
                     self._launch(xs, ys)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1

@@ -329,11 +329,11 @@ class PolicyGradient:
         key = ((n, F), b["x"].dtype, net.training, drops, self.planes_layers)
         hit = self._graphs.get(key)
         if hit is None:
-            from .trainer import graph_capture
+            from .trainer import graph_capture, live_pool
             loss = self._fused_learn(b["x"], b["a"], b["vt"])  # the real learn
             self._step += 1
             g = torch.cuda.CUDAGraph()
-            with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
+            with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
                 static = self._fused_learn(b["x"], b["a"], b["vt"])  # captured, not executed
             self._graphs[key] = (g, static)
             return loss

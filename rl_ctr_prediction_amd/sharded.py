@@ -50,7 +50,7 @@ import torch.distributed as dist
 
 from . import hip_ops
 from .distributed import allreduce_sum_, alltoall_equal, alltoallv, exchange_counts, world
-from .trainer import FusedCTRTrainer, InputSlot, graph_capture
+from .trainer import FusedCTRTrainer, InputSlot, graph_capture, live_pool
 
 CAP_QUANTUM = 1024  # exchange capacities are multiples of this many rows
 
@@ -380,7 +380,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
+                with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
                     self._launch_sharded(slot, mean_div, C)  # captured, not executed
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1

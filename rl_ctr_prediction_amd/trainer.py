@@ -57,6 +57,16 @@ def graph_capture(g, **kw):
             gc.enable()
 
 
+def live_pool(owner):
+    """The graph memory pool handle of `owner` (a trainer / PolicyGradient) for its next
+    capture: torch frees a shared pool once every graph captured into it is gone, and a
+    capture into the freed pool's handle trips an allocator assert (and leaves the RNG in
+    capture state), so an owner whose step graphs were all dropped starts a new pool."""
+    if not owner._graphs:
+        owner._graph_pool = torch.cuda.graph_pool_handle()
+    return owner._graph_pool
+
+
 def flush_hooks(model: nn.Module, trainer) -> None:
     """forward / state_dict pre-hooks that flush the trainer's deferred rows, holding the
     trainer weakly (no model <-> trainer cycle: a dropped trainer is freed at once)."""
@@ -643,7 +653,7 @@ class FusedCTRTrainer:
                 s.plan.build(s.ids, self.V)
                 if self.use_graphs and self.timing is None:
                     g = torch.cuda.CUDAGraph()
-                    with graph_capture(g, pool=self._graph_pool, stream=ps):
+                    with graph_capture(g, pool=live_pool(self), stream=ps):
                         s.plan.build(s.ids, self.V)  # captured, not executed
                     s.plan_graph = g
             self._span("plan", t)
@@ -718,7 +728,7 @@ class FusedCTRTrainer:
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=self._graph_pool, stream=self._capture_stream):
+                with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
                     self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1
