@@ -8,9 +8,9 @@ TAG=${TAG:-r01}
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_trace.log 2>&1 || exit $?
+  python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-driver-loop > $OUT/bench_trace.log 2>&1 || exit $?
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- \
-    python3 bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_$C.log 2>&1 || exit $?
+    python3 bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-driver-loop > $OUT/bench_$C.log 2>&1 || exit $?
 done
 find $OUT -name "*.csv" | head -20
