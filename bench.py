@@ -612,7 +612,7 @@ def main():
             "ms_per_step": per_step["gemm"],
             "TFLOP/s": gemm_flops_bd / (total_ms(bd["gemm"]) * 1e-3) / 1e12 if bd["gemm"] else None},
         "gather (fm_forward_vec)": {"ms_per_step": per_step["gather"]},
-        "sparse plan (radix sort + scan)": {"ms_per_step": per_step["plan"]},
+        "sparse plan (column plan: per-field LDS sorts + merge)": {"ms_per_step": per_step["plan"]},
         "scatter (fm_embedding_grad segmented sums)": {"ms_per_step": per_step["scatter"]},
         "exchange (RCCL collectives + row gathers, N>1)": {"ms_per_step": per_step["exchange"]},
     }
@@ -659,15 +659,14 @@ def main():
                      "seg_chunk_kernel + seg_combine_kernel (per-row gradient sums)")
         else:
             nbytes = plan_bytes(S, U)
-            kname = "sparse plan (keys + radix sort + scan + scatter)"
+            kname = "sparse plan (colplan_sort + colplan_merge + seg_write)"
         achieved = nbytes / (launch_ms * 1e-3) / 1e9
         roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": nbytes}
-        if dominant == "plan":  # the plan's launches: per pass a histogram and a scatter
-            passes = -(-max(1, (V - 1).bit_length()) // 8)
-            parts = [("radix_hist_kernel", passes), ("radix_scatter_kernel", passes),
-                     ("seg_count_kernel", 1), ("seg_write_kernel", 1)]
+        if dominant == "plan":  # the column plan's three launches
+            parts = [("colplan_sort_kernel", 1), ("colplan_merge_kernel", 1),
+                     ("seg_write_kernel", 1)]
             got = [(load_traffic(args.config, k), n) for k, n in parts]
             traffic = (sum(t * n for (t, _), n in got) if all(t for (t, _), _ in got)
                        else None)
