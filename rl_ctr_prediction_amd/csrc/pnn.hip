@@ -215,18 +215,78 @@ __global__ __launch_bounds__(256) void ipnn_backward_reg(const IdxT* __restrict_
     }
 }
 
+// The register walk for a compile-time field count (the CTR layouts: F = 26 Criteo, 22
+// Avazu): every pair slot is static, so the pair values are wave-uniform loads at fixed
+// offsets of the example's dcat row — scalar loads into SGPRs, batched by the compiler — and
+// each update is one VALU multiply by an SGPR operand plus one add: no LDS, no per-pair
+// branch or wait. The same pair walk and operations as ipnn_backward_reg (bitwise equal).
+template <typename IdxT, int F>
+__global__ __launch_bounds__(256) void ipnn_backward_sreg(const IdxT* __restrict__ idx,
+                                                          int64_t B, int K, int64_t V,
+                                                          const float* __restrict__ emb,
+                                                          const float* __restrict__ dcat,
+                                                          int64_t ldd,
+                                                          float* __restrict__ dslot) {
+#pragma clang fp contract(off)  // torch.mul, then the index_put accumulation: rounded apart
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
+  if (b >= B) return;
+  const float* db = dcat + b * ldd;
+  const float* dp = db + (int64_t)F * K;  // the F(F-1)/2 pair gradients, wave-uniform
+  const long long my_row = lane < F ? (long long)load_row(idx, b * F + lane, V, (int32_t*)nullptr)
+                                    : 0ll;
+  const bool ok = lane < K;
+  float e[F], g[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    const long long row = __shfl(my_row, j, kWave);
+    e[j] = ok ? emb[(int64_t)row * K + lane] : 0.f;
+    g[j] = ok ? db[(int64_t)j * K + lane] : 0.f;
+  }
+  int p = 0;
+#pragma unroll
+  for (int i = 0; i < F - 1; ++i) {
+#pragma unroll
+    for (int j = i + 1; j < F; ++j) {
+      const float d = dp[p++];
+      g[i] += d * e[j];
+      g[j] += d * e[i];
+    }
+  }
+  if (ok) {
+    float* out = dslot + b * (int64_t)F * K + lane;
+#pragma unroll
+    for (int f = 0; f < F; ++f) out[(int64_t)f * K] = g[f];
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
 
-// CTR_IPNN_BWD=lds selects the LDS-tile kernel (A/B runs); default: the register kernel
-// where F <= 32 and K <= 64 (one column per lane; wider rows take the LDS-tile kernel)
+// CTR_IPNN_BWD=lds selects the LDS-tile kernel, =reg the LDS-broadcast register walk (A/B runs
+// and the bitwise tests); default: the scalar-operand walk for F = 26 / 22, the register walk
+// otherwise where F <= 32 and K <= 64 (one column per lane), the LDS-tile kernel beyond
 template <typename IdxT>
 static bool launch_ipnn_backward_reg(const IdxT* idx, int64_t B, int F, int K, int64_t V,
                                      const float* emb, const float* dcat, int64_t ldd,
                                      float* dslot, hipStream_t st) {
   const char* env = getenv("CTR_IPNN_BWD");
   if ((env && env[0] == 'l') || F > 32 || K > 64) return false;
+  if (!(env && env[0] == 'r')) {  // CTR_IPNN_BWD=reg: the LDS-broadcast register walk
+    const unsigned grid = (unsigned)ceil_div(B, 4);
+    if (F == 26) {
+      hipLaunchKernelGGL((ipnn_backward_sreg<IdxT, 26>), grid, 256, 0, st, idx, B, K, V, emb,
+                         dcat, ldd, dslot);
+      return true;
+    }
+    if (F == 22) {
+      hipLaunchKernelGGL((ipnn_backward_sreg<IdxT, 22>), grid, 256, 0, st, idx, B, K, V, emb,
+                         dcat, ldd, dslot);
+      return true;
+    }
+  }
   constexpr int FM = 32;
   hipLaunchKernelGGL((ipnn_backward_reg<IdxT, FM, 1>), (unsigned)ceil_div(B, 4), 256,
                      4 * (FM * (FM - 1) / 2) * sizeof(float), st, idx, B, F, K, V, emb, dcat,

@@ -462,11 +462,13 @@ def test_ipnn_forward_and_backward_vs_oracle(cuda, F, K, B):
 
 
 @pytest.mark.parametrize("F,K,B", [(2, 1, 3), (8, 16, 64), (26, 64, 300), (5, 3, 7),
-                                   (32, 64, 33), (33, 8, 9), (22, 128, 50)])
+                                   (32, 64, 33), (33, 8, 9), (22, 128, 50), (26, 16, 77),
+                                   (22, 64, 41)])
 def test_ipnn_planes_and_register_backward_bitwise(cuda, F, K, B, monkeypatch):
     """ipnn_forward writing the MLP input's planes directly == split_planes of the fp32
     forward, bit for bit (with and without the fp32 copy); the register backward (F <= 32,
-    K <= 64) == the LDS-tile backward (CTR_IPNN_BWD=lds), bit for bit."""
+    K <= 64; CTR_IPNN_BWD=reg) and the default (the scalar-operand walk for F = 26 / 22) ==
+    the LDS-tile backward (CTR_IPNN_BWD=lds), bit for bit."""
     H = _hip()
     g = torch.Generator().manual_seed(F + 7 * K + B)
     V = 500
@@ -483,10 +485,13 @@ def test_ipnn_planes_and_register_backward_bitwise(cuda, F, K, B, monkeypatch):
         if keep:
             assert torch.equal(out, cat)
     dcat = torch.randn(B, W, generator=g).to(cuda)
+    dflt = H.ipnn_backward(x, E, dcat)  # F = 26 / 22: the scalar-operand walk
+    monkeypatch.setenv("CTR_IPNN_BWD", "reg")
     reg = H.ipnn_backward(x, E, dcat)
     monkeypatch.setenv("CTR_IPNN_BWD", "lds")
     lds = H.ipnn_backward(x, E, dcat)
     assert torch.equal(reg, lds)
+    assert torch.equal(dflt, lds)
 
 
 # ------------------------------------------------------------------------ REINFORCE ---

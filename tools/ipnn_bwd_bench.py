@@ -1,0 +1,62 @@
+"""Time the IPNN backward (per-slot embedding gradients from dL/dcat) at the C3 IPNN shape:
+
+    python tools/ipnn_bwd_bench.py [--B 8192] [--F 26] [--K 64] [--V 10000000] [--reps 20]
+
+Prints one JSON line per kernel (the default — scalar-operand walk for F = 26 / 22 —, the
+LDS-broadcast register walk, the LDS tile; CTR_IPNN_BWD): us per launch,
+algorithmic bytes (the F rows gathered, the dcat row read, the F x K gradient written) and GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=8192)
+    ap.add_argument("--F", type=int, default=26)
+    ap.add_argument("--K", type=int, default=64)
+    ap.add_argument("--V", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from rl_ctr_prediction_amd import hip_ops as H
+    from rl_ctr_prediction_amd.synthetic import CriteoSynth
+    dev = torch.device("cuda:0")
+    B, F, K, V = a.B, a.F, a.K, a.V
+    x = torch.from_numpy(next(CriteoSynth(V, F, seed=2).batches(1, B))[0]).to(dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    emb = torch.randn(V, K, device=dev, generator=g) * 0.05
+    W = F * K + F * (F - 1) // 2
+    dcat = torch.randn(B, W, device=dev, generator=g)
+    out = torch.empty(B * F, K, device=dev)
+    nbytes = B * (F * K * 4 + W * 4 + F * K * 4 + F * 8)
+    outs = {}
+    for kern in ("default", "reg", "lds"):
+        os.environ["CTR_IPNN_BWD"] = {"default": "", "reg": "reg", "lds": "lds"}[kern]
+        ts = []
+        for r in range(a.reps + 2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            H.ipnn_backward(x, emb, dcat, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            if r >= 2:
+                ts.append(e0.elapsed_time(e1) * 1e3)
+        us = sorted(ts)[len(ts) // 2]
+        outs[kern] = out.clone()
+        print(json.dumps({"kernel": kern, "us": us, "bytes": nbytes,
+                          "GBps": nbytes / (us * 1e-6) / 1e9,
+                          "bitwise_vs_lds": None}), flush=True)
+    print(json.dumps({"bitwise": {k: bool(torch.equal(v, outs["lds"])) for k, v in outs.items()}}))
+
+
+if __name__ == "__main__":
+    main()
