@@ -216,10 +216,11 @@ __global__ __launch_bounds__(256) void ipnn_backward_reg(const IdxT* __restrict_
 }
 
 // The register walk for a compile-time field count (the CTR layouts: F = 26 Criteo, 22
-// Avazu): every pair slot is static, so the pair values are wave-uniform loads at fixed
-// offsets of the example's dcat row — scalar loads into SGPRs, batched by the compiler — and
-// each update is one VALU multiply by an SGPR operand plus one add: no LDS, no per-pair
-// branch or wait. The same pair walk and operations as ipnn_backward_reg (bitwise equal).
+// Avazu): every pair slot is static, so each pair value is read into an SGPR at a fixed lane
+// of a fixed register, and each update is one VALU multiply by that SGPR operand plus one
+// add: no LDS, no per-pair
+// branch or wait (the pair values come in by coalesced vector loads, then v_readlane). The same
+// pair walk and operations as ipnn_backward_reg (bitwise equal).
 template <typename IdxT, int F>
 __global__ __launch_bounds__(256) void ipnn_backward_sreg(const IdxT* __restrict__ idx,
                                                           int64_t B, int K, int64_t V,
@@ -233,9 +234,15 @@ __global__ __launch_bounds__(256) void ipnn_backward_sreg(const IdxT* __restrict
   const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
   if (b >= B) return;
   const float* db = dcat + b * ldd;
-  const float* dp = db + (int64_t)F * K;  // the F(F-1)/2 pair gradients, wave-uniform
+  const float* dp = db + (int64_t)F * K;  // the F(F-1)/2 pair gradients
+  constexpr int P = F * (F - 1) / 2, ND = (P + kWave - 1) / kWave;
   const long long my_row = lane < F ? (long long)load_row(idx, b * F + lane, V, (int32_t*)nullptr)
                                     : 0ll;
+  // the pair values: one coalesced vector load per 64 pairs (lane l holds pair c*64 + l),
+  // in flight with the rows; each pair's value then reaches the wave by v_readlane
+  float vd[ND];
+#pragma unroll
+  for (int c = 0; c < ND; ++c) vd[c] = c * kWave + lane < P ? dp[c * kWave + lane] : 0.f;
   const bool ok = lane < K;
   float e[F], g[F];
 #pragma unroll
@@ -248,10 +255,14 @@ __global__ __launch_bounds__(256) void ipnn_backward_sreg(const IdxT* __restrict
 #pragma unroll
   for (int i = 0; i < F - 1; ++i) {
 #pragma unroll
-    for (int j = i + 1; j < F; ++j) {
-      const float d = dp[p++];
+    for (int j = i + 1; j < F; ++j, ++p) {
+      const float d = __builtin_bit_cast(
+          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vd[p / kWave]), p % kWave));
       g[i] += d * e[j];
       g[j] += d * e[i];
+      // no scheduling across 32-pair groups: the readlanes of a group stay beside its
+      // updates (hoisted, 325 SGPR values spill)
+      if (p % 32 == 31) __builtin_amdgcn_sched_barrier(0);
     }
   }
   if (ok) {
