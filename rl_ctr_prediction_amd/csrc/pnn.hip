@@ -272,21 +272,94 @@ __global__ __launch_bounds__(256) void ipnn_backward_sreg(const IdxT* __restrict
   }
 }
 
+// The backward as one small product per example on the fp32 matrix cores: with D the
+// symmetric F x F matrix of the pair gradients (zero diagonal) and E the example's F
+// embedding rows, the slot gradients are G = dflat + D E. One wave per example, one
+// v_mfma_f32_32x32x2_f32 chain per 32 columns: F padded to 32, the chain starts from dflat
+// (the accumulator's initial value) and runs 16 k-steps of two fields each. Lane l holds
+// A = D[l & 31][2i + (l >> 5)] (gathered from the pair row of dcat) and B = E[2i + (l >> 5)]
+// [32 nb + (l & 31)] (the rows' 128-B halves). The products accumulate inside the matrix
+// core, so the sums are not in the LDS / register walks' order (within fp32 rounding of
+// them; tests/test_gpu_kernels.py) — the same result for every run and launch shape.
+typedef float pnnf32x16 __attribute__((ext_vector_type(16)));
+
+template <typename IdxT>
+__global__ __launch_bounds__(256) void ipnn_backward_mfma(const IdxT* __restrict__ idx,
+                                                          int64_t B, int F, int K, int64_t V,
+                                                          const float* __restrict__ emb,
+                                                          const float* __restrict__ dcat,
+                                                          int64_t ldd,
+                                                          float* __restrict__ dslot) {
+  const int wave = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + wave;
+  if (b >= B) return;  // wave-uniform
+  const float* db = dcat + b * ldd;
+  const float* dp = db + (int64_t)F * K;
+  const long long my_row = lane < F ? (long long)load_row(idx, b * F + lane, V, (int32_t*)nullptr)
+                                    : 0ll;
+  const int f = lane & 31, kk = lane >> 5;
+  // A fragments: D[f][j], j = 2i + kk (the pair (min, max) in row-major order; 0 on the
+  // diagonal and past F)
+  float a[16];
+  long long rj[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int j = 2 * i + kk;
+    const int lo = f < j ? f : j, hi = f < j ? j : f;
+    const bool on = f < F && j < F && f != j;
+    a[i] = on ? dp[lo * (2 * F - lo - 1) / 2 + (hi - lo - 1)] : 0.f;
+    rj[i] = __shfl(my_row, j < F ? j : 0, kWave);
+  }
+  float* out = dslot + b * (int64_t)F * K;
+  for (int nb = 0; nb < K / 32; ++nb) {
+    const int n = 32 * nb + f;
+    pnnf32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kk;
+      acc[r] = row < F ? db[(int64_t)row * K + n] : 0.f;
+    }
+    float e[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int j = 2 * i + kk;
+      e[i] = j < F ? emb[rj[i] * K + n] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], e[i], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kk;
+      if (row < F) out[(int64_t)row * K + n] = acc[r];
+    }
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
 
-// CTR_IPNN_BWD=lds selects the LDS-tile kernel, =reg the LDS-broadcast register walk (A/B runs
-// and the bitwise tests); default: the scalar-operand walk for F = 26 / 22, the register walk
-// otherwise where F <= 32 and K <= 64 (one column per lane), the LDS-tile kernel beyond
+// Default: the matrix-core product where F <= 32 and K % 32 == 0 (40.7 us at the C3 IPNN
+// shape against 53.8 for the scalar-operand walk, profiles/r04_ipnn_bwd.txt), else the
+// scalar-operand walk for F = 26 / 22 (K <= 64), the register walk where F <= 32 and K <= 64
+// (one column per lane), the LDS-tile kernel beyond. CTR_IPNN_BWD=lds / reg / sreg / m forces
+// one (A/B runs and the tests: the three walks are bitwise one another, the product within
+// fp32 rounding of them).
 template <typename IdxT>
 static bool launch_ipnn_backward_reg(const IdxT* idx, int64_t B, int F, int K, int64_t V,
                                      const float* emb, const float* dcat, int64_t ldd,
                                      float* dslot, hipStream_t st) {
   const char* env = getenv("CTR_IPNN_BWD");
-  if ((env && env[0] == 'l') || F > 32 || K > 64) return false;
-  if (!(env && env[0] == 'r')) {  // CTR_IPNN_BWD=reg: the LDS-broadcast register walk
-    const unsigned grid = (unsigned)ceil_div(B, 4);
+  const char e = env ? env[0] : '\0';
+  const unsigned grid = (unsigned)ceil_div(B, 4);
+  if ((e == '\0' || e == 'm') && F <= 32 && K % 32 == 0) {  // the matrix-core product
+    hipLaunchKernelGGL((ipnn_backward_mfma<IdxT>), grid, 256, 0, st, idx, B, F, K, V, emb, dcat,
+                       ldd, dslot);
+    return true;
+  }
+  if (e == 'l' || F > 32 || K > 64) return false;
+  if (e != 'r') {  // the scalar-operand walk
     if (F == 26) {
       hipLaunchKernelGGL((ipnn_backward_sreg<IdxT, 26>), grid, 256, 0, st, idx, B, K, V, emb,
                          dcat, ldd, dslot);

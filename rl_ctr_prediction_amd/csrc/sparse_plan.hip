@@ -393,6 +393,30 @@ __device__ __forceinline__ int32_t col_block_exscan(int32_t v, int32_t* s_w) {
   return off + x - v;
 }
 
+#ifndef CTR_COLPLAN_TRACE
+#define CTR_COLPLAN_TRACE 0
+#endif
+#if CTR_COLPLAN_TRACE
+// tuning builds only: per sort block wall_clock64 at [start, bits known, end of passes 1..3,
+// end], then bits and n
+__device__ unsigned long long g_colplan_trace[kColMaxRuns * 8];
+#define COLPLAN_MARK(slot, v) \
+  if (t == 0) g_colplan_trace[r * 8 + (slot)] = (v)
+#else
+#define COLPLAN_MARK(slot, v)
+#endif
+
+// ids q0 + i*64 (i < IPT) of column f, rows b0.. (q >= n: a clamped load, value unused)
+template <int IPT, typename IdxT>
+__device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64_t b0, int F,
+                                             int f, int n, int q0, int64_t (&raw)[IPT]) {
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const int q = min(q0 + i * kWave, n - 1);
+    raw[i] = static_cast<int64_t>(idx[(b0 + q) * F + f]);
+  }
+}
+
 // One run per block of NT threads x IPT ids, BLOCKED by wave: wave w holds the run's ids
 // [w*IPT*64, (w+1)*IPT*64), item i of lane l being id w*IPT*64 + i*64 + l — so (wave, item,
 // lane) order is slot order. Per 8-bit pass each wave ranks its items in order with no
@@ -417,24 +441,34 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   const int f = r / a.nc, c = r - f * a.nc;
   const int64_t b0 = (int64_t)c * RM;
   const int n = (int)min<int64_t>(RM, a.B - b0);
+  COLPLAN_MARK(0, wall_clock64());
   const int64_t n_seg = (a.S + kSegTile - 1) / kSegTile;
   for (int64_t j = (int64_t)r * NT + t; j < n_seg; j += (int64_t)a.n_runs * NT)
     a.tile_heads[j] = 0;
   uint32_t key[IPT];
   int32_t val[IPT];
   int32_t lo = INT32_MAX, hi = 0;
+  // all IPT loads in flight before the first range check: one index type per loop and no
+  // branch per item (a per-item type branch, or a check's error atomic that may alias idx,
+  // serialises the loads on their full latency)
+  int64_t raw[IPT];
+  if (a.idx_type == CTR_IDX_I64)
+    col_load_ids<IPT>(static_cast<const int64_t*>(a.idx), b0, a.F, f, n, w * WR + lane, raw);
+  else
+    col_load_ids<IPT>(static_cast<const int32_t*>(a.idx), b0, a.F, f, n, w * WR + lane, raw);
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const int q = w * WR + i * kWave + lane;
     key[i] = 0;
     val[i] = 0;
     if (q < n) {
-      const int64_t slot = (b0 + q) * a.F + f;
-      const int64_t row = a.idx_type == CTR_IDX_I64
-                              ? load_row(static_cast<const int64_t*>(a.idx), slot, a.V, a.err)
-                              : load_row(static_cast<const int32_t*>(a.idx), slot, a.V, a.err);
+      int64_t row = raw[i];
+      if (row < 0 || row >= a.V) {
+        if (a.err) atomicOr(a.err, (int32_t)CTR_EFLAG_INDEX);
+        row = 0;
+      }
       key[i] = (uint32_t)row;
-      val[i] = (int32_t)slot;
+      val[i] = (int32_t)((b0 + q) * a.F + f);
       lo = min(lo, (int32_t)row);
       hi = max(hi, (int32_t)row);
     }
@@ -445,6 +479,9 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   const int bits = span == 0 ? 0 : 32 - __builtin_clz(span);
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
   int32_t* wh = s_wh[w];
+  COLPLAN_MARK(1, wall_clock64());
+  COLPLAN_MARK(6, bits);
+  COLPLAN_MARK(7, n);
   for (int shift = 0; shift < bits; shift += 8) {
     for (int d = lane; d < R; d += kWave) wh[d] = 0;  // wave-private: no barrier
     int32_t loc[IPT];
@@ -452,17 +489,22 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
     for (int i = 0; i < IPT; ++i) {
       const bool ok = w * WR + i * kWave + lane < n;
       const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
-      uint64_t peers = __ballot(ok);
+      const uint64_t okm = __ballot(ok);
+      uint32_t plo = (uint32_t)okm, phi = (uint32_t)(okm >> 32);
 #pragma unroll
       for (int bb = 0; bb < 8; ++bb) {
-        const uint64_t m = __ballot((d >> bb) & 1u);
-        peers &= ((d >> bb) & 1u) ? m : ~m;
+        // bit set: keep the lanes whose bit is set (m), else those whose bit is clear (~m)
+        const int32_t sb = (int32_t)(d << (31 - bb)) >> 31;  // v_bfe_i32: 0 / all ones
+        const uint32_t bm = (uint32_t)sb;
+        const uint64_t m = __ballot(sb < 0);
+        plo &= ~((uint32_t)m ^ bm);
+        phi &= ~((uint32_t)(m >> 32) ^ bm);
       }
-      const int rank = __popcll(peers & lt);
+      const int rank = (int)__builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
       const int32_t before = ok ? wh[d] : 0;
       loc[i] = before + rank;
       __builtin_amdgcn_wave_barrier();
-      if (ok && rank == 0) wh[d] = before + __popcll(peers);
+      if (ok && rank == 0) wh[d] = before + __popc(plo) + __popc(phi);
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
@@ -505,6 +547,7 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
       }
       __syncthreads();
     }
+    COLPLAN_MARK(2 + min(shift / 8, 2), wall_clock64());
   }
   if (bits == 0) {  // one row value: already in slot order
 #pragma unroll
@@ -528,18 +571,40 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   const int32_t ex = col_block_exscan<NW>(cnt, s_w);
   int32_t u = ex - 1;
   const int64_t off = (int64_t)f * a.B + b0;
+  const bool al = ((reinterpret_cast<uintptr_t>(a.run_rows + off) |
+                    reinterpret_cast<uintptr_t>(a.run_slots + off) |
+                    reinterpret_cast<uintptr_t>(a.run_seg + off)) & 15) == 0;
+  if (IPT % 4 == 0 && al && q0 + IPT <= n) {  // 16-B LDS reads and stores
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const int q = q0 + i;
-    if (q < n) {
-      const uint32_t k = sk[q];
-      u += (q == 0 || k != sk[q - 1]) ? 1 : 0;
-      a.run_rows[off + q] = (int32_t)k;
-      a.run_slots[off + q] = sv[q];
-      a.run_seg[off + q] = u;
+    for (int i = 0; i < IPT; i += 4) {
+      const uint4 k4 = *reinterpret_cast<const uint4*>(sk + q0 + i);
+      const int4 v4 = *reinterpret_cast<const int4*>(sv + q0 + i);
+      const uint32_t kp = (q0 + i == 0) ? ~k4.x : sk[q0 + i - 1];
+      int4 u4;
+      u4.x = u += k4.x != kp ? 1 : 0;
+      u4.y = u += k4.y != k4.x ? 1 : 0;
+      u4.z = u += k4.z != k4.y ? 1 : 0;
+      u4.w = u += k4.w != k4.z ? 1 : 0;
+      *reinterpret_cast<int4*>(a.run_rows + off + q0 + i) =
+          make_int4((int32_t)k4.x, (int32_t)k4.y, (int32_t)k4.z, (int32_t)k4.w);
+      *reinterpret_cast<int4*>(a.run_slots + off + q0 + i) = v4;
+      *reinterpret_cast<int4*>(a.run_seg + off + q0 + i) = u4;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int q = q0 + i;
+      if (q < n) {
+        const uint32_t k = sk[q];
+        u += (q == 0 || k != sk[q - 1]) ? 1 : 0;
+        a.run_rows[off + q] = (int32_t)k;
+        a.run_slots[off + q] = sv[q];
+        a.run_seg[off + q] = u;
+      }
     }
   }
   if (t == NT - 1) reinterpret_cast<int4*>(a.run_info)[r] = make_int4(lo, hi, n, ex + cnt);
+  COLPLAN_MARK(5, wall_clock64());
 }
 
 // the (row, slot) keys of run [o, o + len) smaller than (row, slot): binary search
@@ -889,6 +954,13 @@ extern "C" int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V,
   CTR_LAUNCH_CHECK("seg_write_kernel");
   return CTR_OK;
 }
+
+#if CTR_COLPLAN_TRACE
+extern "C" int ctr_debug_colplan_trace(unsigned long long* host, int n_blocks) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_colplan_trace),
+                                  sizeof(unsigned long long) * 8 * std::min(n_blocks, kColMaxRuns));
+}
+#endif
 
 extern "C" int ctr_sparse_plan_build_cols(const void* idx, int idx_type, int64_t V, int64_t F,
                                           const ctr_sparse_plan* plan, void* ws, int64_t ws_bytes,

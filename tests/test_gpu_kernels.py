@@ -463,12 +463,13 @@ def test_ipnn_forward_and_backward_vs_oracle(cuda, F, K, B):
 
 @pytest.mark.parametrize("F,K,B", [(2, 1, 3), (8, 16, 64), (26, 64, 300), (5, 3, 7),
                                    (32, 64, 33), (33, 8, 9), (22, 128, 50), (26, 16, 77),
-                                   (22, 64, 41)])
+                                   (22, 64, 41), (8, 32, 5)])
 def test_ipnn_planes_and_register_backward_bitwise(cuda, F, K, B, monkeypatch):
     """ipnn_forward writing the MLP input's planes directly == split_planes of the fp32
     forward, bit for bit (with and without the fp32 copy); the register backward (F <= 32,
-    K <= 64; CTR_IPNN_BWD=reg) and the default (the scalar-operand walk for F = 26 / 22) ==
-    the LDS-tile backward (CTR_IPNN_BWD=lds), bit for bit."""
+    K <= 64; CTR_IPNN_BWD=reg) and the scalar-operand walk (sreg, F = 26 / 22) == the
+    LDS-tile backward (CTR_IPNN_BWD=lds), bit for bit; the default (the matrix-core product
+    where F <= 32 and K % 32 == 0) == it within fp32 rounding, bitwise elsewhere."""
     H = _hip()
     g = torch.Generator().manual_seed(F + 7 * K + B)
     V = 500
@@ -485,13 +486,22 @@ def test_ipnn_planes_and_register_backward_bitwise(cuda, F, K, B, monkeypatch):
         if keep:
             assert torch.equal(out, cat)
     dcat = torch.randn(B, W, generator=g).to(cuda)
-    dflt = H.ipnn_backward(x, E, dcat)  # F = 26 / 22: the scalar-operand walk
-    monkeypatch.setenv("CTR_IPNN_BWD", "reg")
-    reg = H.ipnn_backward(x, E, dcat)
-    monkeypatch.setenv("CTR_IPNN_BWD", "lds")
-    lds = H.ipnn_backward(x, E, dcat)
-    assert torch.equal(reg, lds)
-    assert torch.equal(dflt, lds)
+    dflt = H.ipnn_backward(x, E, dcat)
+    got = {}
+    for mode in ("reg", "sreg", "lds"):  # sreg: the scalar-operand walk for F = 26 / 22
+        monkeypatch.setenv("CTR_IPNN_BWD", mode)
+        got[mode] = H.ipnn_backward(x, E, dcat)
+    assert torch.equal(got["reg"], got["lds"])
+    assert torch.equal(got["sreg"], got["lds"])
+    lds = got["lds"]
+    if F <= 32 and K % 32 == 0:
+        # the matrix-core product (the default here; CTR_IPNN_BWD=m) sums in the matrix
+        # core's order: within fp32 rounding of the walks (1e-5 of the largest gradient)
+        torch.testing.assert_close(dflt, lds, rtol=1e-5, atol=1e-5 * float(lds.abs().max()))
+        monkeypatch.setenv("CTR_IPNN_BWD", "m")
+        assert torch.equal(H.ipnn_backward(x, E, dcat), dflt)  # the same on every launch
+    else:
+        assert torch.equal(dflt, lds)
 
 
 # ------------------------------------------------------------------------ REINFORCE ---

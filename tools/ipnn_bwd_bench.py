@@ -2,8 +2,9 @@
 
     python tools/ipnn_bwd_bench.py [--B 8192] [--F 26] [--K 64] [--V 10000000] [--reps 20]
 
-Prints one JSON line per kernel (the default — scalar-operand walk for F = 26 / 22 —, the
-LDS-broadcast register walk, the LDS tile; CTR_IPNN_BWD): us per launch,
+Prints one JSON line per kernel (the default — the matrix-core product for F <= 32 and
+K % 32 == 0 —, the scalar-operand walk for F = 26 / 22, the LDS-broadcast register walk, the
+LDS tile, the matrix-core product forced; CTR_IPNN_BWD): us per launch,
 algorithmic bytes (the F rows gathered, the dcat row read, the F x K gradient written) and GB/s.
 """
 from __future__ import annotations
@@ -26,7 +27,7 @@ def main():
     ap.add_argument("--K", type=int, default=64)
     ap.add_argument("--V", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--kernels", default="default,reg,lds")
+    ap.add_argument("--kernels", default="default,sreg,reg,lds,mfma")
     a = ap.parse_args()
     from rl_ctr_prediction_amd import hip_ops as H
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
@@ -41,7 +42,7 @@ def main():
     nbytes = B * (F * K * 4 + W * 4 + F * K * 4 + F * 8)
     outs = {}
     for kern in a.kernels.split(","):
-        os.environ["CTR_IPNN_BWD"] = {"default": "", "reg": "reg", "lds": "lds"}[kern]
+        os.environ["CTR_IPNN_BWD"] = {"default": "", "sreg": "sreg", "reg": "reg", "lds": "lds", "mfma": "m"}[kern]
         ts = []
         for r in range(a.reps + 2):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -54,10 +55,11 @@ def main():
         us = sorted(ts)[len(ts) // 2]
         outs[kern] = out.clone()
         print(json.dumps({"kernel": kern, "us": us, "bytes": nbytes,
-                          "GBps": nbytes / (us * 1e-6) / 1e9,
-                          "bitwise_vs_lds": None}), flush=True)
+                          "GBps": nbytes / (us * 1e-6) / 1e9}), flush=True)
     if "lds" in outs:
-        print(json.dumps({"bitwise": {k: bool(torch.equal(v, outs["lds"])) for k, v in outs.items()}}))
+        print(json.dumps({"bitwise": {k: bool(torch.equal(v, outs["lds"])) for k, v in outs.items()},
+                          "max_abs_diff": {k: float((v - outs["lds"]).abs().max())
+                                           for k, v in outs.items()}}))
 
 
 if __name__ == "__main__":
