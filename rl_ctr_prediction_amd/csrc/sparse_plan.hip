@@ -406,6 +406,30 @@ __device__ unsigned long long g_colplan_trace[kColMaxRuns * 8];
 #define COLPLAN_MARK(slot, v)
 #endif
 
+// exclusive scan as col_block_exscan, plus the block total
+template <int NW>
+__device__ __forceinline__ int32_t col_block_exscan_total(int32_t v, int32_t* s_w,
+                                                          int32_t& total) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  int32_t x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) s_w[w] = x;
+  __syncthreads();
+  int32_t off = 0, tot = 0;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    off += j < w ? s_w[j] : 0;
+    tot += s_w[j];
+  }
+  __syncthreads();
+  total = tot;
+  return off + x - v;
+}
+
 // ids q0 + i*64 (i < IPT) of column f, rows b0.. (q >= n: a clamped load, value unused)
 template <int IPT, typename IdxT>
 __device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64_t b0, int F,
@@ -419,21 +443,26 @@ __device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64
 
 // One run per block of NT threads x IPT ids, BLOCKED by wave: wave w holds the run's ids
 // [w*IPT*64, (w+1)*IPT*64), item i of lane l being id w*IPT*64 + i*64 + l — so (wave, item,
-// lane) order is slot order. Per 8-bit pass each wave ranks its items in order with no
-// barrier: 8 ballots give an item's equal-digit peers in its wave-instruction, its place
-// is the wave's running count of that digit (a wave-private LDS histogram) plus its rank
-// among the peers, and the peer group's lowest lane adds the group to the histogram. Then
-// one barrier, the digit bases (a scan of the digit totals) and per digit the waves'
-// exclusive prefix, one barrier, the scatter into LDS. 4 barriers per pass.
+// lane) order is slot order. The column's row span (max - min) takes ceil(bits / 11) LSD
+// passes of W = ceil(bits / passes) bits (C2's 18-bit columns: 2 x 9, C3's 21-bit: 2 x 11).
+// Per pass each wave ranks its items in order with no barrier: W ballots give an item's
+// equal-digit peers in its wave-instruction, its place is the wave's running count of that
+// digit (a wave-private 16-bit LDS histogram) plus its rank among the peers, and the peer
+// group's lowest lane adds the group to the histogram. Then one barrier, the digit bases
+// (a scan of the digit totals, NT digits at a time) and per digit the waves' exclusive
+// prefix, one barrier, the scatter into LDS.
+constexpr int kColMaxDigit = 11;
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   constexpr int NW = NT / kWave;
   constexpr int RM = NT * IPT;
   constexpr int WR = IPT * kWave;  // ids per wave
-  constexpr int R = 256;
+  constexpr int RMAX = 1 << kColMaxDigit;
+  static_assert(RM <= 65535, "16-bit digit counts");
   __shared__ uint32_t sk[RM];
   __shared__ int32_t sv[RM];
-  __shared__ int32_t s_wh[NW][R];  // per wave: running digit counts, then its bases
+  __shared__ __attribute__((aligned(16))) uint16_t s_wh[NW][RMAX];  // per wave: running digit
+                                                                      // counts, then its bases
   __shared__ int32_t s_w[NW];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
@@ -477,51 +506,61 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   hi = col_block_reduce<NW>(hi, true, s_w);
   const uint32_t span = (uint32_t)(hi - lo);
   const int bits = span == 0 ? 0 : 32 - __builtin_clz(span);
-  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (kWave - lane));
-  int32_t* wh = s_wh[w];
+  const int passes = (bits + kColMaxDigit - 1) / kColMaxDigit;
+  const int W = passes == 0 ? 0 : (bits + passes - 1) / passes;  // digit bits of every pass
+  const int R = 1 << W;
+  uint16_t* wh = s_wh[w];
   COLPLAN_MARK(1, wall_clock64());
   COLPLAN_MARK(6, bits);
   COLPLAN_MARK(7, n);
-  for (int shift = 0; shift < bits; shift += 8) {
-    for (int d = lane; d < R; d += kWave) wh[d] = 0;  // wave-private: no barrier
+  for (int shift = 0; shift < bits; shift += W) {
+    // wave-private: no barrier (16-B stores over max(R, 512) counters)
+    for (int d = lane; d < max(R, 512) / 8; d += kWave)
+      reinterpret_cast<uint4*>(wh)[d] = make_uint4(0u, 0u, 0u, 0u);
     int32_t loc[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const bool ok = w * WR + i * kWave + lane < n;
-      const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
+      const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (uint32_t)(R - 1);
       const uint64_t okm = __ballot(ok);
       uint32_t plo = (uint32_t)okm, phi = (uint32_t)(okm >> 32);
 #pragma unroll
-      for (int bb = 0; bb < 8; ++bb) {
-        // bit set: keep the lanes whose bit is set (m), else those whose bit is clear (~m)
-        const int32_t sb = (int32_t)(d << (31 - bb)) >> 31;  // v_bfe_i32: 0 / all ones
-        const uint32_t bm = (uint32_t)sb;
-        const uint64_t m = __ballot(sb < 0);
-        plo &= ~((uint32_t)m ^ bm);
-        phi &= ~((uint32_t)(m >> 32) ^ bm);
+      for (int bb = 0; bb < kColMaxDigit; ++bb) {
+        if (bb < W) {  // uniform
+          // bit set: keep the lanes whose bit is set (m), else those whose bit is clear (~m)
+          const int32_t sb = (int32_t)(d << (31 - bb)) >> 31;  // v_bfe_i32: 0 / all ones
+          const uint32_t bm = (uint32_t)sb;
+          const uint64_t m = __ballot(sb < 0);
+          plo &= ~((uint32_t)m ^ bm);
+          phi &= ~((uint32_t)(m >> 32) ^ bm);
+        }
       }
       const int rank = (int)__builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
-      const int32_t before = ok ? wh[d] : 0;
+      const int32_t before = ok ? (int32_t)wh[d] : 0;
       loc[i] = before + rank;
       __builtin_amdgcn_wave_barrier();
-      if (ok && rank == 0) wh[d] = before + __popc(plo) + __popc(phi);
+      if (ok && rank == 0) wh[d] = (uint16_t)(before + __popc(plo) + __popc(phi));
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // digit d: its total over the waves -> base of the digit (scan of the totals), then
-    // each wave's base = digit base + the earlier waves' counts
-    {
+    // digit d: its total over the waves -> base of the digit (scan of the totals, NT digits
+    // at a time), then each wave's base = digit base + the earlier waves' counts
+    int32_t carry = 0;
+    for (int d0 = 0; d0 < R; d0 += NT) {  // uniform
+      const int d = d0 + t;
       int32_t tot = 0;
-      if (t < R)
+      if (d < R)
 #pragma unroll
-        for (int j = 0; j < NW; ++j) tot += s_wh[j][t];
-      const int32_t base = col_block_exscan<NW>(tot, s_w);  // (barriers inside)
-      if (t < R) {
+        for (int j = 0; j < NW; ++j) tot += s_wh[j][d];
+      int32_t chunk;
+      const int32_t base = carry + col_block_exscan_total<NW>(tot, s_w, chunk);
+      carry += chunk;
+      if (d < R) {
         int32_t run = base;
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
-          const int32_t cn = s_wh[j][t];
-          s_wh[j][t] = run;
+          const int32_t cn = s_wh[j][d];
+          s_wh[j][d] = (uint16_t)run;
           run += cn;
         }
       }
@@ -530,13 +569,13 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
 #pragma unroll
     for (int i = 0; i < IPT; ++i)
       if (w * WR + i * kWave + lane < n) {
-        const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
-        const int p = wh[d] + loc[i];
+        const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (uint32_t)(R - 1);
+        const int p = (int)wh[d] + loc[i];
         sk[p] = key[i];
         sv[p] = val[i];
       }
     __syncthreads();
-    if (shift + 8 < bits) {  // the next pass ranks in the new order (the last leaves it in LDS)
+    if (shift + W < bits) {  // the next pass ranks in the new order (the last leaves it in LDS)
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         const int q = w * WR + i * kWave + lane;
@@ -547,7 +586,7 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
       }
       __syncthreads();
     }
-    COLPLAN_MARK(2 + min(shift / 8, 2), wall_clock64());
+    COLPLAN_MARK(2 + min(shift / W, 2), wall_clock64());
   }
   if (bits == 0) {  // one row value: already in slot order
 #pragma unroll
