@@ -72,6 +72,49 @@ __device__ __forceinline__ void stage_rows_wave(const IdxT* __restrict__ idx, in
                                                 const float* __restrict__ emb, float* tile,
                                                 int ld, float* __restrict__ flat,
                                                 int32_t* err, int lane) {
+  // F <= 64, K % 4 == 0, F*K <= 2048 (the CTR shapes: 26 x 64, 22 x 64 ...): float4 pieces,
+  // all of a lane's (<= 8) loads in flight before the first LDS store — the loop below, not
+  // unrolled, waits for each load before its store (one memory round trip per 64 elements)
+  constexpr int kMaxV4 = 8;
+  if (F <= 64 && (K & 3) == 0 && F * K <= 4 * 64 * kMaxV4) {
+    const int K4 = K >> 2, n4 = F * K4;
+    const long long my_row = lane < F ? (long long)load_row(idx, b * F + lane, V, err) : 0ll;
+    const bool fvec = flat && (reinterpret_cast<uintptr_t>(flat) & 15) == 0;
+    float4 v[kMaxV4];
+#pragma unroll
+    for (int it = 0; it < kMaxV4; ++it) {
+      const int t = lane + 64 * it;  // float4 piece
+      int f = t / K4;
+      f = f < F ? f : F - 1;
+      const long long row = __shfl(my_row, f, 64);
+      if (t < n4) v[it] = *reinterpret_cast<const float4*>(emb + row * K + 4 * (t - f * K4));
+    }
+#pragma unroll
+    for (int it = 0; it < kMaxV4; ++it) {
+      const int t = lane + 64 * it;
+      if (t < n4) {
+        const int f = t / K4, k = 4 * (t - f * K4);
+        float* tr = tile + f * ld + k;
+        if ((ld & 3) == 0) {
+          *reinterpret_cast<float4*>(tr) = v[it];
+        } else {
+          tr[0] = v[it].x;
+          tr[1] = v[it].y;
+          tr[2] = v[it].z;
+          tr[3] = v[it].w;
+        }
+        if (fvec) {
+          *reinterpret_cast<float4*>(flat + 4 * t) = v[it];
+        } else if (flat) {
+          flat[4 * t] = v[it].x;
+          flat[4 * t + 1] = v[it].y;
+          flat[4 * t + 2] = v[it].z;
+          flat[4 * t + 3] = v[it].w;
+        }
+      }
+    }
+    return;
+  }
   for (int f0 = 0; f0 < F; f0 += 64) {
     const int nf = F - f0 < 64 ? F - f0 : 64;
     long long my_row = 0;

@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void fm_forward_vec(
   if (b >= B) return;  // wave-uniform
   const int c = lane % K4;
   const int r0 = lane / K4;
+  const float yb = labels ? labels[b] : 0.f;  // in flight with the id loads
 
   // One id per lane (lane f < F), range-checked once, then broadcast by ds_bpermute.
   int my_row = 0;
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void fm_forward_vec(
     if (z_out) z_out[b] = z;
     if (labels) {
       float p, l, g;
-      bce_sigmoid_head(z, labels[b], mean_div, p, l, g);
+      bce_sigmoid_head(z, yb, mean_div, p, l, g);
       if (p_out) p_out[b] = p;
       if (loss_out) loss_out[b] = l;
       if (gz_out) gz_out[b] = g;
@@ -200,13 +201,32 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
   const int64_t b = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
   if (b >= B) return;
   const float* hb = h + b * H;
+  const float zfm = z_fm[b], yb = y ? y[b] : 0.f;  // in flight with the row loads
+  // H <= 256 (the reference's 200): the lane's <= 4 h / w values loaded together and kept for
+  // the gradient below (a loop with a load -> use chain per 64 columns was ~4 dependent
+  // memory round trips per example: 11.4 us at C3 for 6.5 MB); the same sums in the same order
+  constexpr int kMaxJ = 4;
+  const bool held = H <= kMaxJ * kWave;
+  float hv[kMaxJ], wv[kMaxJ];
   float part = 0.f;
-  for (int j = lane; j < H; j += kWave) part += hb[j] * w[j];
+  if (held) {
+#pragma unroll
+    for (int q = 0; q < kMaxJ; ++q) {
+      const int j = lane + q * kWave;
+      hv[q] = j < H ? hb[j] : 0.f;
+      wv[q] = j < H ? w[j] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxJ; ++q)
+      if (lane + q * kWave < H) part += hv[q] * wv[q];
+  } else {
+    for (int j = lane; j < H; j += kWave) part += hb[j] * w[j];
+  }
   const float dot = wave_sum(part);
-  const float z = z_fm[b] + (dot + bo[0]);  // p_model.py:322 (to_fm(x) + mlp(...))
+  const float z = zfm + (dot + bo[0]);  // p_model.py:322 (to_fm(x) + mlp(...))
   float p, l, g;
   if (y) {
-    bce_sigmoid_head(z, y[b], mean_div, p, l, g);
+    bce_sigmoid_head(z, yb, mean_div, p, l, g);
   } else {
     p = sigmoidf_ref(z);
     l = 0.f;
@@ -220,8 +240,8 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
   }
   if (dh_pre && y) {
     float* d = dh_pre + b * H;
-    for (int j = lane; j < H; j += kWave) {
-      const float v = hb[j] > 0.f ? (g * w[j]) * drop_scale : 0.f;
+    auto put = [&](int j, float hj, float wj) {
+      const float v = hj > 0.f ? (g * wj) * drop_scale : 0.f;
       d[j] = v;
       if (dpl) {  // dH2's planes for the dH1 / dW1 GEMMs (csrc/gemm_planes.hip)
         uint16_t h3[3];
@@ -229,6 +249,13 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
 #pragma unroll
         for (int p = 0; p < 3; ++p) dpl[p * dpl_ps + b * dpl_ld + j] = h3[p];
       }
+    };
+    if (held) {
+#pragma unroll
+      for (int q = 0; q < kMaxJ; ++q)
+        if (lane + q * kWave < H) put(lane + q * kWave, hv[q], wv[q]);
+    } else {
+      for (int j = lane; j < H; j += kWave) put(j, hb[j], w[j]);
     }
   }
 }

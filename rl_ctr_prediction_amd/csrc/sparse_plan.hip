@@ -443,15 +443,19 @@ __device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64
 
 // One run per block of NT threads x IPT ids, BLOCKED by wave: wave w holds the run's ids
 // [w*IPT*64, (w+1)*IPT*64), item i of lane l being id w*IPT*64 + i*64 + l — so (wave, item,
-// lane) order is slot order. The column's row span (max - min) takes ceil(bits / 11) LSD
-// passes of W = ceil(bits / passes) bits (C2's 18-bit columns: 2 x 9, C3's 21-bit: 2 x 11).
+// lane) order is slot order. The column's row span (max - min) takes ceil(bits / 8) LSD
+// passes of the same width W = ceil(bits / passes) <= 8 (C2's 18-bit columns: 3 x 6, its
+// 10-bit ones 2 x 5; C3's 21-bit 3 x 7). A narrower digit is cheaper per pass (fewer ballots,
+// a smaller histogram to clear and scan); wider digits with fewer passes measured slower per
+// column (2 x 11 bits: 17.6 us of passes against 14.8 for 3 x 8 at C3,
+// profiles/r04_colplan_trace2.txt).
 // Per pass each wave ranks its items in order with no barrier: W ballots give an item's
 // equal-digit peers in its wave-instruction, its place is the wave's running count of that
 // digit (a wave-private 16-bit LDS histogram) plus its rank among the peers, and the peer
 // group's lowest lane adds the group to the histogram. Then one barrier, the digit bases
 // (a scan of the digit totals, NT digits at a time) and per digit the waves' exclusive
 // prefix, one barrier, the scatter into LDS.
-constexpr int kColMaxDigit = 11;
+constexpr int kColMaxDigit = 8;
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   constexpr int NW = NT / kWave;

@@ -41,7 +41,7 @@ def main():
         assert fn(buf.ctypes.data, F) == 0
         t = buf[:, :6].astype(np.int64)
         bits = buf[:, 6].astype(np.int64)
-        passes = (bits + 10) // 11
+        passes = (bits + 7) // 8
         ph = {"load_reduce": t[:, 1] - t[:, 0]}
         prev = t[:, 1]
         for k in range(3):

@@ -5,7 +5,8 @@
 Prints one JSON line per kernel (the default — the matrix-core product for F <= 32 and
 K % 32 == 0 —, the scalar-operand walk for F = 26 / 22, the LDS-broadcast register walk, the
 LDS tile, the matrix-core product forced; CTR_IPNN_BWD): us per launch,
-algorithmic bytes (the F rows gathered, the dcat row read, the F x K gradient written) and GB/s.
+algorithmic bytes (the F rows gathered, the dcat row read, the F x K gradient written) and GB/s;
+then the forward (planes output, as the trainer runs it).
 """
 from __future__ import annotations
 
@@ -56,6 +57,21 @@ def main():
         outs[kern] = out.clone()
         print(json.dumps({"kernel": kern, "us": us, "bytes": nbytes,
                           "GBps": nbytes / (us * 1e-6) / 1e9}), flush=True)
+    # the forward as the trainer runs it: MLP input written straight as bf16 planes
+    pl = H.Planes(B, W, dev)
+    ts = []
+    for r in range(a.reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        H.ipnn_forward(x, emb, planes=pl)
+        e1.record()
+        torch.cuda.synchronize()
+        if r >= 2:
+            ts.append(e0.elapsed_time(e1) * 1e3)
+    us = sorted(ts)[len(ts) // 2]
+    fbytes = B * (F * 8 + F * K * 4 + W * 6)  # ids, gathered rows, three bf16 planes
+    print(json.dumps({"kernel": "forward_planes", "us": us, "bytes": fbytes,
+                      "GBps": fbytes / (us * 1e-6) / 1e9}), flush=True)
     if "lds" in outs:
         print(json.dumps({"bitwise": {k: bool(torch.equal(v, outs["lds"])) for k, v in outs.items()},
                           "max_abs_diff": {k: float((v - outs["lds"]).abs().max())
