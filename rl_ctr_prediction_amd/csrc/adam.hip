@@ -225,13 +225,8 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
     }
     if (!APPLY && from >= target) continue;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    // step s's table entry is loaded one replayed step ahead (its latency under step s-1)
-    const float2* tab2 = reinterpret_cast<const float2*>(tab);
-    float2 nxt = from + 1 <= target ? tab2[from + 1] : make_float2(0.f, 0.f);
     for (int s = from + 1; s <= target; ++s) {
-      h.neg_step_size = nxt.x;
-      h.inv_bc2_sqrt = nxt.y;
-      if (s + 1 <= target) nxt = tab2[s + 1];
+      load_step(h, tab, s);
       adam_vec(pp, z4, mm, vv, h);
       if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
     }

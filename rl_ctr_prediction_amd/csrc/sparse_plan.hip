@@ -406,30 +406,6 @@ __device__ unsigned long long g_colplan_trace[kColMaxRuns * 8];
 #define COLPLAN_MARK(slot, v)
 #endif
 
-// exclusive scan as col_block_exscan, plus the block total
-template <int NW>
-__device__ __forceinline__ int32_t col_block_exscan_total(int32_t v, int32_t* s_w,
-                                                          int32_t& total) {
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  int32_t x = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int32_t y = __shfl_up(x, o, kWave);
-    if (lane >= o) x += y;
-  }
-  if (lane == kWave - 1) s_w[w] = x;
-  __syncthreads();
-  int32_t off = 0, tot = 0;
-#pragma unroll
-  for (int j = 0; j < NW; ++j) {
-    off += j < w ? s_w[j] : 0;
-    tot += s_w[j];
-  }
-  __syncthreads();
-  total = tot;
-  return off + x - v;
-}
-
 // ids q0 + i*64 (i < IPT) of column f, rows b0.. (q >= n: a clamped load, value unused)
 template <int IPT, typename IdxT>
 __device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64_t b0, int F,
@@ -443,30 +419,25 @@ __device__ __forceinline__ void col_load_ids(const IdxT* __restrict__ idx, int64
 
 // One run per block of NT threads x IPT ids, BLOCKED by wave: wave w holds the run's ids
 // [w*IPT*64, (w+1)*IPT*64), item i of lane l being id w*IPT*64 + i*64 + l — so (wave, item,
-// lane) order is slot order. The column's row span (max - min) takes ceil(bits / 8) LSD
-// passes of the same width W = ceil(bits / passes) <= 8 (C2's 18-bit columns: 3 x 6, its
-// 10-bit ones 2 x 5; C3's 21-bit 3 x 7). A narrower digit is cheaper per pass (fewer ballots,
-// a smaller histogram to clear and scan); wider digits with fewer passes measured slower per
-// column (2 x 11 bits: 17.6 us of passes against 14.8 for 3 x 8 at C3,
-// profiles/r04_colplan_trace2.txt).
-// Per pass each wave ranks its items in order with no barrier: W ballots give an item's
-// equal-digit peers in its wave-instruction, its place is the wave's running count of that
-// digit (a wave-private 16-bit LDS histogram) plus its rank among the peers, and the peer
-// group's lowest lane adds the group to the histogram. Then one barrier, the digit bases
-// (a scan of the digit totals, NT digits at a time) and per digit the waves' exclusive
-// prefix, one barrier, the scatter into LDS.
-constexpr int kColMaxDigit = 8;
+// lane) order is slot order. Per 8-bit pass each wave ranks its items in order with no
+// barrier: 8 ballots give an item's equal-digit peers in its wave-instruction, its place
+// is the wave's running count of that digit (a wave-private LDS histogram) plus its rank
+// among the peers, and the peer group's lowest lane adds the group to the histogram. Then
+// one barrier, the digit bases (a scan of the digit totals) and per digit the waves'
+// exclusive prefix, one barrier, the scatter into LDS. 4 barriers per pass. Measured and not
+// kept (profiles/r04_colplan_trace{2,3}.txt, sort phase trace): ceil(bits/11) equal-width
+// passes on 16-bit wave counters (C2 13.2 us, C3 25.7: an 11-bit pass costs 1.7x an 8-bit
+// one) and ceil(bits/8) equal-width passes <= 8 bits (C2 15.0, C3 23.3) against this
+// kernel's 13.9 / 23.0.
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   constexpr int NW = NT / kWave;
   constexpr int RM = NT * IPT;
   constexpr int WR = IPT * kWave;  // ids per wave
-  constexpr int RMAX = 1 << kColMaxDigit;
-  static_assert(RM <= 65535, "16-bit digit counts");
+  constexpr int R = 256;
   __shared__ uint32_t sk[RM];
   __shared__ int32_t sv[RM];
-  __shared__ __attribute__((aligned(16))) uint16_t s_wh[NW][RMAX];  // per wave: running digit
-                                                                      // counts, then its bases
+  __shared__ int32_t s_wh[NW][R];  // per wave: running digit counts, then its bases
   __shared__ int32_t s_w[NW];
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1), w = t / kWave;
@@ -510,61 +481,50 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
   hi = col_block_reduce<NW>(hi, true, s_w);
   const uint32_t span = (uint32_t)(hi - lo);
   const int bits = span == 0 ? 0 : 32 - __builtin_clz(span);
-  const int passes = (bits + kColMaxDigit - 1) / kColMaxDigit;
-  const int W = passes == 0 ? 0 : (bits + passes - 1) / passes;  // digit bits of every pass
-  const int R = 1 << W;
-  uint16_t* wh = s_wh[w];
+  int32_t* wh = s_wh[w];
   COLPLAN_MARK(1, wall_clock64());
   COLPLAN_MARK(6, bits);
   COLPLAN_MARK(7, n);
-  for (int shift = 0; shift < bits; shift += W) {
-    // wave-private: no barrier (16-B stores over max(R, 512) counters)
-    for (int d = lane; d < max(R, 512) / 8; d += kWave)
-      reinterpret_cast<uint4*>(wh)[d] = make_uint4(0u, 0u, 0u, 0u);
+  for (int shift = 0; shift < bits; shift += 8) {
+    for (int d = lane; d < R; d += kWave) wh[d] = 0;  // wave-private: no barrier
     int32_t loc[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const bool ok = w * WR + i * kWave + lane < n;
-      const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (uint32_t)(R - 1);
+      const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
       const uint64_t okm = __ballot(ok);
       uint32_t plo = (uint32_t)okm, phi = (uint32_t)(okm >> 32);
 #pragma unroll
-      for (int bb = 0; bb < kColMaxDigit; ++bb) {
-        if (bb < W) {  // uniform
-          // bit set: keep the lanes whose bit is set (m), else those whose bit is clear (~m)
-          const int32_t sb = (int32_t)(d << (31 - bb)) >> 31;  // v_bfe_i32: 0 / all ones
-          const uint32_t bm = (uint32_t)sb;
-          const uint64_t m = __ballot(sb < 0);
-          plo &= ~((uint32_t)m ^ bm);
-          phi &= ~((uint32_t)(m >> 32) ^ bm);
-        }
+      for (int bb = 0; bb < 8; ++bb) {
+        // bit set: keep the lanes whose bit is set (m), else those whose bit is clear (~m)
+        const int32_t sb = (int32_t)(d << (31 - bb)) >> 31;  // v_bfe_i32: 0 / all ones
+        const uint32_t bm = (uint32_t)sb;
+        const uint64_t m = __ballot(sb < 0);
+        plo &= ~((uint32_t)m ^ bm);
+        phi &= ~((uint32_t)(m >> 32) ^ bm);
       }
       const int rank = (int)__builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
-      const int32_t before = ok ? (int32_t)wh[d] : 0;
+      const int32_t before = ok ? wh[d] : 0;
       loc[i] = before + rank;
       __builtin_amdgcn_wave_barrier();
-      if (ok && rank == 0) wh[d] = (uint16_t)(before + __popc(plo) + __popc(phi));
+      if (ok && rank == 0) wh[d] = before + __popc(plo) + __popc(phi);
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // digit d: its total over the waves -> base of the digit (scan of the totals, NT digits
-    // at a time), then each wave's base = digit base + the earlier waves' counts
-    int32_t carry = 0;
-    for (int d0 = 0; d0 < R; d0 += NT) {  // uniform
-      const int d = d0 + t;
+    // digit d: its total over the waves -> base of the digit (scan of the totals), then
+    // each wave's base = digit base + the earlier waves' counts
+    {
       int32_t tot = 0;
-      if (d < R)
+      if (t < R)
 #pragma unroll
-        for (int j = 0; j < NW; ++j) tot += s_wh[j][d];
-      int32_t chunk;
-      const int32_t base = carry + col_block_exscan_total<NW>(tot, s_w, chunk);
-      carry += chunk;
-      if (d < R) {
+        for (int j = 0; j < NW; ++j) tot += s_wh[j][t];
+      const int32_t base = col_block_exscan<NW>(tot, s_w);  // (barriers inside)
+      if (t < R) {
         int32_t run = base;
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
-          const int32_t cn = s_wh[j][d];
-          s_wh[j][d] = (uint16_t)run;
+          const int32_t cn = s_wh[j][t];
+          s_wh[j][t] = run;
           run += cn;
         }
       }
@@ -573,13 +533,13 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
 #pragma unroll
     for (int i = 0; i < IPT; ++i)
       if (w * WR + i * kWave + lane < n) {
-        const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (uint32_t)(R - 1);
-        const int p = (int)wh[d] + loc[i];
+        const uint32_t d = ((key[i] - (uint32_t)lo) >> shift) & (R - 1);
+        const int p = wh[d] + loc[i];
         sk[p] = key[i];
         sv[p] = val[i];
       }
     __syncthreads();
-    if (shift + W < bits) {  // the next pass ranks in the new order (the last leaves it in LDS)
+    if (shift + 8 < bits) {  // the next pass ranks in the new order (the last leaves it in LDS)
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         const int q = w * WR + i * kWave + lane;
@@ -590,7 +550,7 @@ __global__ __launch_bounds__(NT) void colplan_sort_kernel(ColArgs a) {
       }
       __syncthreads();
     }
-    COLPLAN_MARK(2 + min(shift / W, 2), wall_clock64());
+    COLPLAN_MARK(2 + min(shift / 8, 2), wall_clock64());
   }
   if (bits == 0) {  // one row value: already in slot order
 #pragma unroll
@@ -669,6 +629,16 @@ __global__ __launch_bounds__(kSortThreads) void colplan_merge_kernel(ColArgs a) 
   __shared__ int s_overlap;
   const int t = threadIdx.x;
   const int nr = a.n_runs;
+  // this slot's run entries, loaded with the run table (one memory round trip for both)
+  const int64_t e = (int64_t)blockIdx.x * kSortThreads + t;
+  const bool live = e < a.S;
+  const int f = (int)((live ? e : 0) / a.B);
+  const int64_t wi = (live ? e : 0) - (int64_t)f * a.B;
+  const int c = (int)(wi / a.RM);
+  const int p = (int)(wi - (int64_t)c * a.RM);
+  const int32_t row = live ? a.run_rows[e] : 0, slot = live ? a.run_slots[e] : 0;
+  const int32_t lseg = live ? a.run_seg[e] : 0;
+  const int32_t prev_row = live && p > 0 ? a.run_rows[e - 1] : -1;
   if (t == 0) s_overlap = 0;
   for (int g = t; g < nr; g += kSortThreads) s_info[g] = reinterpret_cast<const int4*>(a.run_info)[g];
   __syncthreads();
@@ -685,7 +655,6 @@ __global__ __launch_bounds__(kSortThreads) void colplan_merge_kernel(ColArgs a) 
   }
   __syncthreads();
   const bool disjoint = s_overlap == 0;
-  const int64_t e = (int64_t)blockIdx.x * kSortThreads + t;
   if (blockIdx.x == 0 && t == 0) {
     a.flags[0] = disjoint ? 0 : 1;
     if (disjoint) {
@@ -695,13 +664,8 @@ __global__ __launch_bounds__(kSortThreads) void colplan_merge_kernel(ColArgs a) 
       a.plan.seg_offsets[U] = (int32_t)a.S;
     }
   }
-  if (e >= a.S) return;
-  const int f = (int)(e / a.B);
-  const int64_t wi = e - (int64_t)f * a.B;
-  const int c = (int)(wi / a.RM);
-  const int p = (int)(wi - (int64_t)c * a.RM);
+  if (!live) return;
   const int r = f * a.nc + c;
-  const int32_t row = a.run_rows[e], slot = a.run_slots[e];
   int64_t pos = p;
   int32_t segb = 0;
   bool first_elsewhere = false;  // another run holds this row at a smaller slot
@@ -721,9 +685,9 @@ __global__ __launch_bounds__(kSortThreads) void colplan_merge_kernel(ColArgs a) 
   }
   a.plan.sorted_rows[pos] = row;
   a.plan.sorted_slots[pos] = slot;
-  const bool local_head = p == 0 || a.run_rows[e - 1] != row;
+  const bool local_head = p == 0 || prev_row != row;
   if (disjoint) {
-    const int32_t seg = segb + a.run_seg[e];
+    const int32_t seg = segb + lseg;
     a.plan.pos_seg[pos] = seg;
     if (local_head) {
       a.plan.unique_rows[seg] = row;
