@@ -451,7 +451,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
                        m0 + wm0, n0 + wn0, lane, split);
 }
 
-// split-K: sum the fp32 slabs in split order (8 independent loads in flight per step of
+// split-K: sum the fp32 slabs in split order (16 independent loads in flight per step of
 // the chain), then the epilogue (fp32 out and/or planes); one thread per 4 columns
 // slabs: [splits][M][sld], sld = align_up(N, 4) (the padding columns are never read as
 // results), so every row starts 16-B aligned and the float4 path always applies
@@ -469,23 +469,25 @@ __global__ __launch_bounds__(64) void planes_reduce_kernel(PlanesArgs a, const f
     const int64_t o = m * sld + n;
     float e[4];
     if (vec) {
-      float4 s = *reinterpret_cast<const float4*>(slabs + o);
-      int z = 1;
-      // 8 slabs' loads in flight per step of the (ordered) sum chain: the weight-gradient
-      // reduces run 9-32 slabs, so 4 in flight left them latency-bound (dW1's at C3 12 us)
-      for (; z + 7 < splits; z += 8) {
-        float4 v[8];
+      // up to 16 slabs' loads in flight per step of the (ordered) sum chain: dW0's 9 slabs in
+      // one memory round trip, dW1's 32 in two (a first load, then batches of 8, took 2 and
+      // 5: 11 us per reduce at C3)
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z = 0; z < splits; z += 16) {
+        float4 v[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = *reinterpret_cast<const float4*>(slabs + (int64_t)(z + j) * slab + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w;
+        for (int j = 0; j < 16; ++j) {  // past the last slab: a clamped (unused) load, no branch
+          const int zj = min(z + j, splits - 1);
+          v[j] = *reinterpret_cast<const float4*>(slabs + (int64_t)zj * slab + o);
         }
-      }
-      for (; z < splits; ++z) {
-        const float4 v = *reinterpret_cast<const float4*>(slabs + (int64_t)z * slab + o);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {  // selects, not branches (the loads stay batched)
+          const bool first = z + j == 0, add = z + j < splits && !first;
+          s.x = first ? v[j].x : add ? s.x + v[j].x : s.x;
+          s.y = first ? v[j].y : add ? s.y + v[j].y : s.y;
+          s.z = first ? v[j].z : add ? s.z + v[j].z : s.z;
+          s.w = first ? v[j].w : add ? s.w + v[j].w : s.w;
+        }
       }
       e[0] = s.x; e[1] = s.y; e[2] = s.z; e[3] = s.w;
     } else {

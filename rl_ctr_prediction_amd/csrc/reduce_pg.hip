@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void sum_stage1(const float* __restrict__ x, i
   const int64_t lo = blockIdx.x * per_block;
   const int64_t hi = min(n, lo + per_block);
   float acc = 0.f;
-#pragma unroll 8
+#pragma unroll 32
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += x[i];
   const float r = block_sum_256(acc, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = r;
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(1024) void sum_small(const float* __restrict__ x, i
                                                   float scale, float* __restrict__ out) {
   __shared__ float sh[16];
   float acc = 0.f;
-#pragma unroll 8
+#pragma unroll 32
   for (int64_t i = threadIdx.x; i < n; i += 1024) acc += x[i];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
@@ -76,10 +76,10 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ X
   // memory round trip per row); the additions stay in row order (deterministic)
   if (n < N) {
     if (w) {
-#pragma unroll 8
+#pragma unroll 32
       for (int64_t m = lo + ry; m < hi; m += 4) acc += w[m] * X[m * ldx + n];
     } else {
-#pragma unroll 8
+#pragma unroll 32
       for (int64_t m = lo + ry; m < hi; m += 4) acc += X[m * ldx + n];
     }
   }
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ p
   for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
        n += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
-#pragma unroll 8
+#pragma unroll 32
     for (int r = 0; r < rs; ++r) s += part[(int64_t)r * N + n];
     out[n] = s * scale;
   }
@@ -131,10 +131,10 @@ __global__ __launch_bounds__(256) void colsum_multi_stage1(ColsumJobs J, float* 
   float acc = 0.f;
   if (n < N) {
     if (w) {
-#pragma unroll 8
+#pragma unroll 32
       for (int64_t m = lo + ry; m < hi; m += 4) acc += w[m] * X[m * ldx + n];
     } else {
-#pragma unroll 8
+#pragma unroll 32
       for (int64_t m = lo + ry; m < hi; m += 4) acc += X[m * ldx + n];
     }
   }
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void colsum_multi_stage2(ColsumJobs J,
     for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < N;
          n += (int64_t)gridDim.x * blockDim.x) {
       float s = 0.f;
-#pragma unroll 8
+#pragma unroll 32
       for (int r = 0; r < J.rs[j]; ++r) s += pj[(int64_t)r * N + n];
       J.out[j][n] = s * J.scale[j];
     }
