@@ -418,6 +418,9 @@ def main():
     ap.add_argument("--lookahead", type=int, default=2,
                     help="sparse plans built this many batches ahead, concurrently with the "
                          "step (FusedCTRTrainer next_x); 0 = every plan in its own step")
+    ap.add_argument("--no-stage-labels", action="store_true",
+                    help="lookahead stages the next batches' ids only (next_y not passed): "
+                         "every step copies its labels on the main stream")
     ap.add_argument("--optimizer", default="deferred", choices=["deferred", "dense"],
                     help="deferred-exact dense Adam (default) or the dense streaming pass; "
                          "bitwise-identical results (tests/test_gpu_deferred.py)")
@@ -492,7 +495,10 @@ def main():
         i = seq[0]
         seq[0] += 1
         nxt = [xs[(i + j) % len(xs)] for j in range(1, args.lookahead + 1)]
-        trainer.step(xs[i % len(xs)], ys[i % len(ys)], next_x=nxt, return_loss=False)
+        nyt = None if args.no_stage_labels else [ys[(i + j) % len(ys)]
+                                                 for j in range(1, args.lookahead + 1)]
+        trainer.step(xs[i % len(xs)], ys[i % len(ys)], next_x=nxt, return_loss=False,
+                     next_y=nyt)
 
     for i in range(args.warmup):
         step(i)
@@ -576,7 +582,7 @@ def main():
         tot = 0.0
         for j, (x_j, y_j) in enumerate(dl):
             nxt = [b[0] for b in dl[j + 1:j + 3]]
-            tot += trainer.step(x_j, y_j, next_x=nxt).item()
+            tot += trainer.step(x_j, y_j, next_x=nxt, next_y=[b[1] for b in dl[j + 1:j + 3]]).item()
         trainer.flush()
         torch.cuda.synchronize()
         dt_item = time.perf_counter() - t0

@@ -147,8 +147,9 @@ def run_epoch(optimizer, batches) -> float:
         optimizer.reset_loss_sum()
     for i, (features, labels) in enumerate(batches):
         if lookahead:  # the next two batches' sparse plans are built during this step
-            nxt = [b[0] for b in batches[i + 1:i + 3]]
-            optimizer.step(features, labels, next_x=nxt, return_loss=False)
+            nxt = batches[i + 1:i + 3]
+            optimizer.step(features, labels, next_x=[b[0] for b in nxt], return_loss=False,
+                           next_y=[b[1] for b in nxt])
         elif device_sum:
             optimizer.step(features, labels, return_loss=False)
         else:  # AutogradTrainer: the reference's per-step host read

@@ -243,11 +243,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
 
     # ------------------------------------------------------------------ the step ------
     def _step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-              next_x=None) -> torch.Tensor:
+              next_x=None, next_y=None) -> torch.Tensor:
         """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches are
         staged and their plans and per-owner run maxima built on the plan stream during this
         step. Purely local (the capacity agreement is made when a batch's step comes), so
-        ranks may pass different next_x."""
+        ranks may pass different next_x. next_y is accepted and not used here (the labels
+        are copied with each step)."""
         if self.exchange == "varsplit":
             return self._step_varsplit(x, y, global_batch, next_x)
         B, F = x.shape

@@ -101,7 +101,7 @@ class InputSlot:
     passes through the slot, so a stream of fresh batches replays the same graphs (the
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
-    __slots__ = ("shape", "index", "ids", "y", "plan", "ev", "plan_graph",
+    __slots__ = ("shape", "index", "ids", "y", "y_key", "plan", "ev", "plan_graph",
                  "done_ev", "stream_i", "stage_stream", "cap", "counts")
 
     def __init__(self, shape, index: int, device):
@@ -109,6 +109,7 @@ class InputSlot:
         self.shape, self.index = shape, index
         self.ids = torch.empty(B, F, dtype=dtype, device=device)
         self.y = torch.empty(B, dtype=torch.float32, device=device)
+        self.y_key = None       # staged ahead with the labels too: the labels tensor's key
         self.plan = hip_ops.SparsePlanBuffers(B * F, device)
         self.ev = None          # staged ahead: the copy + plan on the plan stream recorded here
         self.plan_graph = None  # the plan build of this slot, captured on its plan stream
@@ -486,7 +487,7 @@ class FusedCTRTrainer:
 
     # ------------------------------------------------------------------------ step ----
     def step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-             next_x=None, return_loss: bool = True) -> torch.Tensor | None:
+             next_x=None, return_loss: bool = True, next_y=None) -> torch.Tensor | None:
         """One training step on batch (x [B,F] int64/int32, y [B] 0/1). Returns the
         batch's mean BCE as a fresh 1-element device tensor (no host sync), or None with
         return_loss=False (no copy launch; the loss still goes into ``loss_sum``).
@@ -507,13 +508,16 @@ class FusedCTRTrainer:
         then long past when the step waits for it (a cross-queue wait that is still
         pending costs ~15 us). next_x is read on the plan stream after everything enqueued
         before this call: its contents must stay valid until this call's work has run; a
-        step with other ids builds its plan as usual.
+        step with other ids builds its plan as usual. next_y (optional, aligned with next_x):
+        those batches' labels, copied into their slots on the plan stream as well, so the
+        step that trains on them skips its label copy (the same tensor must then be passed
+        as that step's y; any other y is copied as usual).
 
         Every step also adds its loss (fp64) to the device accumulator ``loss_sum`` inside
         the step's last launch — the driver's epoch loss without a host sync per step
         (read_loss_sum / reset_loss_sum)."""
         with self._scratch.scope():  # this trainer's own scratch (hip_ops.Workspace)
-            loss = self._step(x, y, global_batch, next_x)
+            loss = self._step(x, y, global_batch, next_x, next_y)
             return loss.clone() if return_loss else None
 
     def reset_loss_sum(self) -> None:
@@ -527,7 +531,7 @@ class FusedCTRTrainer:
         return float(self.loss_sum.item())
 
     def _step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
-              next_x=None) -> torch.Tensor:
+              next_x=None, next_y=None) -> torch.Tensor:
         """step() without the copy of the loss: returns the persistent loss buffer of the
         batch shape (the captured graph writes it in place)."""
         B, F = x.shape
@@ -546,11 +550,17 @@ class FusedCTRTrainer:
         shape = (B, F, x.dtype)
         xkey = self._xkey(x)
         nk = []
+        ny = {}  # staged labels by ids key
         if next_x is not None and self.plan_lookahead and self._plan_stream is not None:
-            for n in ([next_x] if isinstance(next_x, torch.Tensor) else next_x):
+            xs_ = [next_x] if isinstance(next_x, torch.Tensor) else list(next_x)
+            ys_ = ([next_y] if isinstance(next_y, torch.Tensor) else list(next_y)
+                   ) if next_y is not None else []
+            for j, n in enumerate(xs_):
                 k = self._xkey(n)
                 if k[1:3] == xkey[1:3] and k != xkey and all(k != kk for _, kk in nk):
                     nk.append((n, k))
+                    if j < len(ys_) and ys_[j] is not None and ys_[j].numel() == n.shape[0]:
+                        ny[k] = ys_[j]
         main = torch.cuda.current_stream()
         slot = self._staged.pop(xkey, None)
         if self._staged:  # staged for batches that did not come next: free their slots
@@ -569,7 +579,9 @@ class FusedCTRTrainer:
         else:
             slot = self._acquire_slot(shape)
             slot.ids.copy_(x, non_blocking=True)
-        slot.y.copy_(y.reshape(-1), non_blocking=True)
+        if not (have and slot.y_key is not None and slot.y_key == self._xkey(y)):
+            slot.y.copy_(y.reshape(-1), non_blocking=True)
+        slot.y_key = None
         if self.use_graphs and self.timing is None:
             loss = self._graph_step(slot, mean_div, have)
         else:
@@ -577,7 +589,7 @@ class FusedCTRTrainer:
             loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
             self._after_step()
         for n, k in todo:
-            self._stage_ahead(n, k, shape, slot, ev_start, main)
+            self._stage_ahead(n, k, shape, slot, ev_start, main, ny.get(k))
         return loss
 
     def _ring(self, shape) -> list:
@@ -632,7 +644,7 @@ class FusedCTRTrainer:
         return s
 
     def _stage_ahead(self, nx: torch.Tensor, key, shape, current: InputSlot, ev_start,
-                     main) -> None:
+                     main, ny: torch.Tensor | None = None) -> None:
         """Copy ids nx into a free slot and build its sparse plan there, on the slot's plan
         stream, concurrently with the step just enqueued (replayed from the slot's own
         plan graph once captured)."""
@@ -646,6 +658,12 @@ class FusedCTRTrainer:
             s.ids.copy_(nx, non_blocking=True)
             if nx.is_cuda:
                 nx.record_stream(ps)
+            s.y_key = None
+            if ny is not None:  # the labels too: the step on this batch skips its copy
+                s.y.copy_(ny.reshape(-1), non_blocking=True)
+                if ny.is_cuda:
+                    ny.record_stream(ps)
+                s.y_key = self._xkey(ny)
             t = self._mark("plan")
             if s.plan_graph is not None and self.timing is None:
                 s.plan_graph.replay()

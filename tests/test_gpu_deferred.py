@@ -202,7 +202,8 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     step (one or two ahead, the second one a guess the order sometimes breaks): bitwise the same
     losses, tables and moments as building every plan in its own step — over graph captures
     and replays, a lookahead the next step does not use (order changed), next_x == x, a step
-    without next_x in between, and eager (no-graph) steps."""
+    without next_x in between, eager (no-graph) steps, and labels staged with next_y (the
+    batch's own: its label copy skipped; a decoy: its own labels still copied)."""
     import rl_ctr_prediction_amd as P
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
     F = 26
@@ -213,10 +214,15 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     # lookahead (next 2, then batch 1), next == x, no next, then cycles again
     order = [(0, 1), (1, 2), (2, 0), (0, 1), (1, 2), (2, 0), (0, 2), (1, 1), (1, None),
              (2, 0), (0, 1), (1, 2), (2, 0), (0, 1)]
+    decoy = [1.0 - y for y in ys]  # staged labels the steps then do not train on
     out = []
-    # (batches ahead, HIP graphs, plan lookahead)
-    for ahead, graphs, pla in ((0, True, False), (1, True, True), (2, True, True),
-                               (2, False, True), (2, True, False), (1, False, True)):
+    # (batches ahead, HIP graphs, plan lookahead, labels staged too: None / the batch's own
+    # (its step skips the label copy) / a decoy (its step must copy its own y))
+    for ahead, graphs, pla, ymode in ((0, True, False, None), (1, True, True, None),
+                                      (2, True, True, None), (2, False, True, None),
+                                      (2, True, False, None), (1, False, True, None),
+                                      (2, True, True, "own"), (1, False, True, "own"),
+                                      (2, True, True, "decoy")):
         torch.manual_seed(8)
         with torch.device(cuda):
             m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
@@ -229,9 +235,14 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         losses = []
         for j, (i, n) in enumerate(order):
             nxt = xs[n] if (ahead and n is not None) else None
+            nb = [n] if (ahead and n is not None) else []
             if ahead == 2 and n is not None:  # the next two batches of the order
-                nxt = [xs[n]] + ([xs[order[j + 2][0]]] if j + 2 < len(order) else [])
-            losses.append(tr.step(xs[i], ys[i], next_x=nxt).item())
+                nb = [n] + ([order[j + 2][0]] if j + 2 < len(order) else [])
+                nxt = [xs[q] for q in nb]
+            nyt = None
+            if ymode is not None and nb:
+                nyt = [(ys if ymode == "own" else decoy)[q] for q in nb]
+            losses.append(tr.step(xs[i], ys[i], next_x=nxt, next_y=nyt).item())
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
         st = tr.optimizer_state_dict()["state"]
         out.append((losses, sd, st))
