@@ -112,6 +112,48 @@ def plan_bytes(S, U):
     return S * 20 + U * 8
 
 
+def gemm_planes_bytes(M, N, K, out_planes=False, aux=False):
+    """One MLP GEMM on pre-split operands, algorithmic: both operands' three bf16 planes read
+    once (6 B per element), the fp32 output written (4 B), its planes too when the next GEMM
+    reads them (6 B), the epilogue's fp32 aux operand read (4 B)."""
+    return 6 * (M * K + K * N) + M * N * (4 + (6 if out_planes else 0) + (4 if aux else 0))
+
+
+def step_model(kind, B, F, K, U, H1=300, H2=200, flush_bytes_per_step=0.0, lin=True):
+    """Algorithmic HBM bytes and flops of one training step as the timed region runs it
+    (N = 1, deferred-exact Adam, plan built ahead; DESIGN.md §5 "step roofline"): the plan
+    (S·20 + U·8), the catch-up of the batch's U rows (U·(24(K+1) + 8): p, m, v of the row
+    and of its linear weight read + written, last[] read + written), the gather + forward,
+    the MLP GEMMs (planes bytes, 2·M·N·K flops), the head, the per-row sums with the fused
+    Adam apply of the U rows, the dense Adam and the flush amortised over the region's
+    steps. Returns {part: bytes}, flops."""
+    S = B * F
+    deep = kind in MLP_KINDS
+    parts = {"plan": plan_bytes(S, U),
+             "catchup": U * (24 * (K + (1 if lin else 0)) + 8)}
+    flops = 0.0
+    if kind == "IPNN":
+        W = F * K + F * (F - 1) // 2
+        parts["gather"] = S * (8 + 4 * K) + B * W * 6
+    else:
+        W = F * K
+        parts["gather"] = gather_bytes(S, K, B, deep)
+    if deep:
+        g = [(B, H1, W, True, False), (B, H2, H1, False, False),   # fwd0, fwd1
+             (B, H1, H2, True, True), (B, W, H1, False, False),    # dH1 (mask aux), dX
+             (H2, H1, B, False, False), (H1, W, B, False, False)]  # dW1, dW0
+        parts["gemm"] = sum(gemm_planes_bytes(*a) for a in g)
+        flops = sum(2.0 * a[0] * a[1] * a[2] for a in g)
+        parts["head"] = B * H2 * (4 + 6) + B * 16
+        dense = W * H1 + H1 + H1 * H2 + H2 + H2 + 2
+        parts["dense_adam"] = dense * 28 + (W * H1 + H1 * H2) * 6
+        if kind == "IPNN":  # per-slot gradients through the pair products
+            parts["ipnn_backward"] = S * 8 + S * 4 * K * 2 + B * W * 4
+    parts["scatter_apply"] = scatter_bytes(S, K, U, deep and kind != "IPNN", apply=True)
+    parts["flush_amortised"] = flush_bytes_per_step
+    return parts, flops
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -697,6 +739,30 @@ def main():
         g_kernel, g_bytes = "fm_forward_vec (gather + FM" + (
             ", MLP input as bf16 planes)" if deep else ")"), gather_bytes(S, K, B, deep)
     value = world * B * args.steps / elapsed
+    # the step against the machine: every byte and flop of the algorithm the region times
+    # (deferred-exact dense Adam; the flushes inside the region amortised over its steps)
+    n_flush = len(timing["flush"])
+    fb = flush_bytes(trainer.V_tab, K, lin=trainer.w_tab is not None) * n_flush / args.steps
+    parts, sflops = step_model(cfg["kind"], B, F, K, U, flush_bytes_per_step=fb,
+                               lin=trainer.w_tab is not None)
+    sbytes = sum(parts.values())
+    step_s = elapsed / args.steps
+    step_roofline = {
+        "bytes_per_step": sbytes, "flops_per_step": sflops,
+        "hbm_GBps": sbytes / step_s / 1e9, "hbm_frac": sbytes / step_s / 1e9 / HBM_PEAK_GBS,
+        "mfma_TFps": sflops / step_s / 1e12 if sflops else None,
+        "mfma_frac": sflops / step_s / 1e12 / MFMA_F32_PEAK_TFS if sflops else None,
+        "bound_ms": max(sbytes / (HBM_PEAK_GBS * 1e9), sflops / (MFMA_F32_PEAK_TFS * 1e12)) * 1e3,
+        "serial_bound_ms": (sbytes / (HBM_PEAK_GBS * 1e9)
+                            + sflops / (MFMA_F32_PEAK_TFS * 1e12)) * 1e3,
+        "parts_bytes": parts, "unique_rows": U, "flushes_in_region": n_flush,
+        "model": "algorithmic bytes of the deferred-exact step (bench.step_model, DESIGN.md §5):"
+                 " plan + catch-up of the U batch rows + gather/forward + MLP GEMMs (planes) +"
+                 " head + row sums with the fused Adam apply + dense Adam + the region's "
+                 "flushes / K; flops = the six MLP GEMMs; hbm_frac / mfma_frac over the "
+                 "timed ms_per_step, bound_ms = max(bytes/8 TB/s, flops/157.3 TF)"}
+    if world > 1:
+        step_roofline["_note"] = "N > 1: per rank; the exchange's bytes are not in the model"
     result = {
         "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -718,6 +784,7 @@ def main():
                                       or (getattr(trainer, "plan_lookahead", False)
                                           and args.optimizer == "deferred") else 0)},
         "roofline": roofline,
+        "step_roofline": step_roofline,
         "kernels": kernels,
         "host_ms_per_step": host_s / args.steps * 1e3,  # inside step(): the enqueue cost
         "driver_loop": driver,

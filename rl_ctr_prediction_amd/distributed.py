@@ -22,8 +22,10 @@ def world() -> tuple[int, int]:
     return 0, 1
 
 
-def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
-    if world()[1] > 1:
+def allreduce_sum_(t: torch.Tensor, group=None, force: bool = False) -> torch.Tensor:
+    """In-place sum over the group's ranks. force: issue the collective at world size 1 too
+    (a one-rank RCCL communicator: the N > 1 launch sequence exercised on one GPU)."""
+    if world()[1] > 1 or force:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
 
@@ -112,12 +114,14 @@ def alltoallv(send: torch.Tensor, send_counts: list[int], recv_counts: list[int]
     return out
 
 
-def alltoall_equal(out: torch.Tensor, send: torch.Tensor, group=None) -> torch.Tensor:
+def alltoall_equal(out: torch.Tensor, send: torch.Tensor, group=None,
+                   force: bool = False) -> torch.Tensor:
     """Equal-split all-to-all along dim 0 (N equal blocks of the same rows each way): sizes
     fixed by the shapes, no host-side counts — the row-sharded exchange at a fixed capacity.
-    One process: a copy. gloo (CPU test runs) stages device tensors through host memory."""
+    One process: a copy, unless force (the collective on a one-rank communicator). gloo (CPU
+    test runs) stages device tensors through host memory."""
     rank, ws = world()
-    if ws == 1:
+    if ws == 1 and not force:
         out.copy_(send)
         return out
     if send.is_cuda and dist.get_backend(group) == "gloo":

@@ -856,6 +856,12 @@ def ipnn_forward(idx: torch.Tensor, emb: torch.Tensor, out: torch.Tensor | None 
     B, F = idx.shape
     V, K = emb.shape
     W = F * K + F * (F - 1) // 2
+    if out is not None:  # the same checks with or without planes: the C side knows ldc only
+        _dev(out, "out")
+        if (out.dtype != torch.float32 or out.dim() != 2 or out.shape[0] < B
+                or out.shape[1] < W or out.stride(1) != 1):
+            raise ValueError(f"ipnn_forward: out must be float32 [>= {B}, >= {W}], unit "
+                             "column stride")
     if planes is not None:
         if planes.rows < B or planes.cols < W:
             raise ValueError(f"ipnn_forward: planes [{planes.rows}, {planes.cols}] < [{B}, {W}]")
@@ -865,8 +871,6 @@ def ipnn_forward(idx: torch.Tensor, emb: torch.Tensor, out: torch.Tensor | None 
         return out
     if out is None:
         out = torch.empty(B, W, dtype=torch.float32, device=emb.device)
-    elif out.dtype != torch.float32 or out.shape[0] < B or out.shape[1] < W or out.stride(1) != 1:
-        raise ValueError(f"ipnn_forward: out must be float32 [>= {B}, >= {W}], unit column stride")
     lib.ctr_ipnn_forward(_p(idx), it, B, F, K, V, _p(emb), _p(out), out.stride(0), _p(err_flag),
                          _stream())
     return out

@@ -44,6 +44,7 @@ from __future__ import annotations
 
 import os
 import weakref
+from time import perf_counter
 
 import torch
 import torch.distributed as dist
@@ -80,6 +81,30 @@ class _XBufs:
         self.slot2u = torch.empty(max(S, 1), **i32)
 
 
+def _host_span(acc: dict, key: str, t0: float) -> float:
+    t1 = perf_counter()
+    acc[key] = acc.get(key, 0.0) + (t1 - t0)
+    return t1
+
+
+UNKNOWN_RUN = 1 << 62  # an agreement entry whose batch some rank has not staged (MAX wins)
+
+
+class _Agreement:
+    """One capacity agreement: the largest per-owner run of the batches each rank staged for
+    the next LOOKAHEAD steps (entry j: step t + 1 + j; UNKNOWN_RUN where not staged), all-
+    reduced MAX over the count group (N > 1), copied to pinned host memory, an event after."""
+
+    __slots__ = ("dev", "host", "ev", "keys", "call")
+
+    def __init__(self, n: int, dev):
+        self.dev = torch.empty(n, dtype=torch.int64, device=dev)
+        self.host = torch.empty(n, dtype=torch.int64, pin_memory=True)
+        self.ev = torch.cuda.Event()
+        self.keys = [None] * n  # this rank's batch (ids key) behind each entry
+        self.call = -1          # the step() call that issued it
+
+
 class ShardedCTRTrainer(FusedCTRTrainer):
     """FusedCTRTrainer over this rank's row shard of the embedding tables (deferred-exact
     Adam). The shard is all this rank keeps: at construction the model's
@@ -89,16 +114,19 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     target), never the whole table. The model may be built on the host (the reference's own
     init: ``get_model(...)`` then ``.to(device)``, all_main/pretrain_main.py:137), so a
     vocabulary larger than one GPU is never materialised on any device.
-    ``model.state_dict()`` is local (no collective): this rank's rows of the tables and the
-    replicated dense parameters, so ``if rank == 0: torch.save(model.state_dict())`` never
-    blocks, and every rank resumes from its own file with ``model.load_state_dict`` (a
-    full-size table in the loaded dict is cut to the rank's rows). full_state_dict() and
+    ``model.state_dict()`` is local (no collective): this rank's rows of the tables (their
+    row range in the dict's metadata) and the replicated dense parameters; every rank saves
+    and resumes from its own file with ``model.load_state_dict`` (a full-size table in the
+    loaded dict is cut to the rank's rows; another rank's shard is refused). full_state_dict() and
     gather_tables() — collectives, every rank calls them — assemble the full tables; the
     sharded model's own forward needs them and refuses to run on a shard (N > 1)."""
 
+    LOOKAHEAD = 2  # steps ahead a capacity agreement covers
+
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None,
-                 count_group=None, device=None, exchange: str = "padded"):
+                 count_group=None, device=None, exchange: str = "padded",
+                 force_collectives: bool = False):
         """process_group: the ranks sharing the table (default: the world). count_group: a
         second communicator over the same ranks for the per-step capacity / counts
         agreement (it runs on the plan stream beside the data collectives). Default:
@@ -106,7 +134,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         default process_group every rank builds its trainer at the same point; trainers
         over a sub-group must pass a count_group that every rank of the world created in
         the same order (e.g. one of dist.new_subgroups()). exchange: "padded" (fixed
-        capacity, the default) or "varsplit"."""
+        capacity, the default) or "varsplit". force_collectives: at world size 1, send every
+        exchange through the collectives of a one-rank process group (dist initialised,
+        e.g. RCCL on one GPU) instead of local copies — the N > 1 launch sequence, RCCL
+        kernels and their graph capture included, on one device (tests)."""
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:
@@ -125,20 +156,34 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
         # the plans (and per-owner counts / run maxima) are built on the plan stream, ahead
-        # of the step with next_x; the per-step agreement runs there on a communicator of
-        # its own, so the host waits for that stream only, never for the previous step
+        # of the step with next_x; the capacity agreements run on a stream and (N > 1) a
+        # communicator of their own (_capacity)
         if self._plan_stream is None:
             self._plan_stream = self._new_stream()
         self._count_group = count_group
-        if self.world_size > 1 and count_group is None:
+        # collectives in the step: always at N > 1; at N = 1 only when forced
+        self._coll = self.world_size > 1 or bool(force_collectives)
+        if self._coll and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("force_collectives needs an initialised process group")
+        if self._coll and count_group is None:
             if process_group is not None:
                 raise ValueError("ShardedCTRTrainer over a process_group needs a count_group "
                                  "over the same ranks, created by every rank of the world "
                                  "(dist.new_group is collective over the whole world)")
             self._count_group = dist.new_group()
         self._ahead_counts: dict = {}
-        self._cap_stream = None  # the capacity agreement's stream (_agree_capacity)
-        self.cap_reads = 0
+        # the capacity agreements (see _capacity): one per step() call, issued at the end of
+        # the call for the batches staged for the next LOOKAHEAD steps, read back two calls
+        # later at the latest; a ring of four (a record is reused four calls after its issue)
+        self._cap_stream = self._new_stream()
+        self._agree = [_Agreement(self.LOOKAHEAD, self.device) for _ in range(4)]
+        self._calls = 0           # step() calls so far (the index of the next step)
+        self._agree_last_ev = None
+        self._now = None          # the blocking agreement's record (no lookahead)
+        self.cap_reads = 0        # host reads of an agreement (one per step)
+        self.cap_blocking = 0     # of those, agreements made in the step itself
+        # host seconds per section of step() (tools/sharded_host_cost.py), when a dict
+        self.host_sections: dict | None = None
         self._xbufs: dict = {}
         self._cap = 0  # the exchange capacity in use (rows per (requester, owner) pair)
         # graph replay of the fixed-capacity step: at one process always (no collective), at
@@ -180,19 +225,40 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                    "tables; assemble them with trainer.gather_tables() (or "
                                    "model.state_dict() on every rank) for inference")
 
+            def save_rows(module, state_dict, prefix, local_metadata):
+                """The shard's row range goes into the state dict's metadata (the keys stay
+                the reference's): [row_lo, row_hi, V]."""
+                t = ref()
+                if t is not None:
+                    local_metadata["ctr_rows"] = [t.row_lo, t.row_hi, t._V_full]
+
             def load_rows(state_dict, prefix, local_metadata, strict, missing, unexpected,
                           errors):
                 """A full-size table in the loaded dict (a checkpoint of the unsharded model
-                or of full_state_dict()) is cut to this rank's rows; a shard-size one (this
-                rank's own model.state_dict()) loads as it is."""
+                or of full_state_dict()) is cut to this rank's rows; a shard-size one loads as
+                it is only if its metadata names this rank's rows (a shard saved by another
+                rank, or without its row range, is refused: equal shard sizes would otherwise
+                load another rank's rows without an error)."""
                 t = ref()
                 if t is None:
                     return
                 for name in ("feature_embedding.weight", "linear.weight"):
                     v = state_dict.get(prefix + name)
-                    if v is not None and v.dim() >= 1 and v.shape[0] == t._V_full != t.V_tab:
+                    if v is None or v.dim() < 1:
+                        continue
+                    if v.shape[0] == t._V_full != t.V_tab:
                         state_dict[prefix + name] = v[t.row_lo:t.row_hi]
+                        continue
+                    got = local_metadata.get("ctr_rows")
+                    want = [t.row_lo, t.row_hi, t._V_full]
+                    if got is None or list(got) != want:
+                        raise RuntimeError(
+                            f"ShardedCTRTrainer: {prefix + name} holds {v.shape[0]} rows with "
+                            f"row range {got} in its metadata; this rank owns rows "
+                            f"[{want[0]}, {want[1]}) of {want[2]} — load this rank's own "
+                            "state_dict() or a full-size table (full_state_dict())")
             model.register_forward_pre_hook(no_forward)
+            model._register_state_dict_hook(save_rows)
             model._register_load_state_dict_pre_hook(load_rows)
 
     def _vocab_size(self, E) -> int:
@@ -244,13 +310,18 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     # ------------------------------------------------------------------ the step ------
     def _step(self, x: torch.Tensor, y: torch.Tensor, global_batch: int | None = None,
               next_x=None, next_y=None) -> torch.Tensor:
-        """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the next batches are
-        staged and their plans and per-owner run maxima built on the plan stream during this
-        step. Purely local (the capacity agreement is made when a batch's step comes), so
-        ranks may pass different next_x. next_y is accepted and not used here (the labels
-        are copied with each step)."""
+        """next_x (one tensor or a sequence, as FusedCTRTrainer.step): the batches of the next
+        steps, in step order. They are staged and their plans and per-owner run maxima built
+        on the plan stream during this step, and the capacity for the next LOOKAHEAD steps is
+        agreed at the end of this call (_capacity). At N > 1 a batch passed as next_x[j]
+        must be the batch of step + 1 + j once that step comes (the ranks agreed on its
+        capacity; any rank may pass None or fewer batches, and every rank then agrees in
+        the step instead). next_y is accepted and not used here (the labels are copied with
+        each step)."""
         if self.exchange == "varsplit":
             return self._step_varsplit(x, y, global_batch, next_x)
+        hs = self.host_sections
+        h0 = perf_counter() if hs is not None else 0.0
         B, F = x.shape
         ws = self.world_size
         mean_div = float(global_batch if global_batch is not None else B * ws)
@@ -259,39 +330,35 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         main, ps = torch.cuda.current_stream(), self._plan_stream
         shape = (B, F, x.dtype)
         xkey = self._xkey(x)
+        t_call = self._calls
+        # the next batches by position (entry j: step t_call + 1 + j); None where a batch
+        # cannot be staged (another shape, the current batch, a repeat)
         ahead = []
         if next_x is not None:
             for n in ([next_x] if isinstance(next_x, torch.Tensor) else next_x):
                 k = self._xkey(n)
-                if k[1:3] == xkey[1:3] and k != xkey and all(k != kk for _, kk in ahead):
-                    ahead.append((n, k))
+                ok = (k[1:3] == xkey[1:3] and k != xkey
+                      and all(a is None or k != a[1] for a in ahead))
+                ahead.append((n, k) if ok else None)
         slot = self._staged.pop(xkey, None)
         if self._staged:
-            keep = {k for _, k in ahead}
+            keep = {a[1] for a in ahead if a is not None}
             for k in [k for k in self._staged if k not in keep]:
                 main.wait_event(self._staged.pop(k).ev)
-        todo = [(n, k) for n, k in ahead if k not in self._staged]
-        ev_start = torch.cuda.Event()
+        todo = [a for a in ahead if a is not None and a[1] not in self._staged]
+        ev_start = self._start_event()
         ev_start.record(main)  # everything enqueued before this step
         if slot is None:  # copy and plan now, on the plan stream
             slot = self._acquire_slot(shape, ahead=True)
-            ps.wait_event(ev_start)
-            torch.cuda.set_stream(ps)
-            try:
-                slot.ids.copy_(x, non_blocking=True)
-                if x.is_cuda:
-                    x.record_stream(ps)
-                self._plan_slot(slot)
-            finally:
-                torch.cuda.set_stream(main)
+            self._stage_slot(slot, x, ev_start, main)
         slot.y.copy_(y.reshape(-1), non_blocking=True)
-        # the capacity: every rank's largest run, agreed on a stream of its own that waits for
-        # this slot's plan only (built one or two steps ahead with next_x) — never for the
-        # main stream — so the host's read waits for the all-reduce alone while the GPU still
-        # runs the steps already enqueued
+        if hs is not None:
+            h0 = _host_span(hs, "prologue", h0)
         t = self._mark("plan")
-        cmax = self._agree_capacity(slot)
+        cmax = self._capacity(t_call, xkey, slot)
         self._span("plan", t)
+        if hs is not None:
+            h0 = _host_span(hs, "capacity_read", h0)
         if cmax > self._cap:  # grows only (every rank sees the same cmax: the same C)
             grown = cmax + cmax // 32  # headroom: a later, slightly larger batch still fits
             C = max(CAP_QUANTUM, -(-grown // CAP_QUANTUM) * CAP_QUANTUM)
@@ -308,54 +375,149 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self.step_table.ensure(self.step_count + 1)
             loss = self._launch_sharded(slot, mean_div, C)
             self._after_step()
+        if hs is not None:
+            h0 = _host_span(hs, "step_launch", h0)
         for n, k in todo:
             s = self._acquire_slot(shape, exclude=slot, ahead=True)
-            ps.wait_event(ev_start)
-            torch.cuda.set_stream(ps)
-            try:
-                s.ids.copy_(n, non_blocking=True)
-                if n.is_cuda:
-                    n.record_stream(ps)
-                self._plan_slot(s)
-            finally:
-                torch.cuda.set_stream(main)
+            self._stage_slot(s, n, ev_start, main)
             self._staged[k] = s
+        if hs is not None:
+            h0 = _host_span(hs, "stage_ahead", h0)
+        self._issue_agreement(t_call, ahead)
+        self._calls += 1
+        if hs is not None:
+            _host_span(hs, "agreement_issue", h0)
         return loss
 
-    def _agree_capacity(self, slot: InputSlot) -> int:
-        """The largest per-owner run of this step's batches over every rank (an all-reduce
-        MAX over the count group), read by the host. On the capacity stream: it waits for
-        the slot's plan event only, so the read never waits for the main stream's work (the
-        previous steps), and the all-reduce result travels to pinned host memory."""
-        if self._cap_stream is None:
-            self._cap_stream = self._new_stream()
-            self._cap_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-            self._cap_ev = torch.cuda.Event()
-        cs = self._cap_stream
+    # ----------------------------------------------------------- the capacity ---------
+    # The step's one host read is the exchange capacity C: every rank's largest per-owner
+    # run, agreed before the step's collectives can be sized. Where the read is enqueued
+    # decides what it waits for: a process has GPU_MAX_HW_QUEUES (4) hardware queues and the
+    # HIP runtime maps every further stream onto one of them (least used at creation), so a
+    # stream of its own is no guarantee that a read does not queue behind the main stream's
+    # steps (round 4: the capacity stream landed on the plan stream's queue in one process
+    # and, in the test suite's process with more streams created before, on main's). So the
+    # agreement for a step is enqueued in an EARLIER call: at the end of call t (after its
+    # step and staging), for the batches staged for steps t+1 and t+2; the read at step t
+    # takes the agreement of call t-2 (entry 1) or else of call t-1 (entry 0). In FIFO order
+    # on whatever queue it lands, that agreement sits behind at most the work enqueued up to
+    # call t-1's end — never behind anything enqueued after (test_capacity_read_never_waits_
+    # for_main: a sleep kernel queued on main between two calls). With two batches of
+    # lookahead the read waits for step t-2 at worst, so the host runs up to two steps ahead
+    # of the GPU. A step whose capacity nobody agreed ahead (no lookahead on some rank: every
+    # rank sees the same UNKNOWN_RUN) agrees in the step itself (_agree_now).
+
+    def _capacity(self, t: int, xkey, slot: InputSlot) -> int:
+        """The agreed capacity need (largest run) of step t."""
+        for a, j in ((self._agree[(t - 2) % 4], 1), (self._agree[(t - 1) % 4], 0)):
+            if a.call != t - 1 - j or j >= len(a.keys):
+                continue
+            a.ev.synchronize()
+            v = int(a.host[j])
+            if v == UNKNOWN_RUN:
+                continue
+            if a.keys[j] == xkey:
+                self.cap_reads += 1
+                return v
+            if self._coll:  # the other ranks sized this step by that agreement
+                raise RuntimeError(
+                    "ShardedCTRTrainer: step trained on a batch other than the one passed as "
+                    "next_x for it; with collectives every rank sized this step's exchange by "
+                    "the agreed capacity of the announced batches (pass next_x=None instead)")
+            break  # one process: agree on this batch now
+        return self._agree_now(slot)
+
+    def _agree_now(self, slot: InputSlot) -> int:
+        """The capacity of this step's batch alone, agreed now (blocking)."""
+        a = self._now
+        if a is None:
+            a = self._now = _Agreement(1, self.device)
+        cs, main = self._cap_stream, torch.cuda.current_stream()
         cs.wait_event(slot.ev)
-        with torch.cuda.stream(cs):
-            if self.world_size > 1:
-                dist.all_reduce(slot.cap, op=dist.ReduceOp.MAX, group=self._count_group)
-            self._cap_host.copy_(slot.cap, non_blocking=True)
-            self._cap_ev.record(cs)
-        self._cap_ev.synchronize()
+        torch.cuda.set_stream(cs)
+        try:
+            a.dev.copy_(slot.cap)
+            if self._coll:
+                dist.all_reduce(a.dev, op=dist.ReduceOp.MAX, group=self._count_group)
+            a.host.copy_(a.dev, non_blocking=True)
+            a.ev.record(cs)
+        finally:
+            torch.cuda.set_stream(main)
+        a.ev.synchronize()
         self.cap_reads += 1
-        return int(self._cap_host[0])
+        self.cap_blocking += 1
+        return int(a.host[0])
+
+    def _issue_agreement(self, t: int, ahead) -> None:
+        """Call t's agreement for steps t+1 .. t+LOOKAHEAD (not waited for here)."""
+        a = self._agree[t % 4]
+        a.call = t
+        cs = self._cap_stream
+        known = []
+        for j in range(self.LOOKAHEAD):
+            e = ahead[j] if j < len(ahead) else None
+            s = self._staged.get(e[1]) if e is not None else None
+            a.keys[j] = e[1] if s is not None else None
+            if s is not None:
+                cs.wait_event(s.ev)
+                known.append((j, s))
+        main = torch.cuda.current_stream()
+        torch.cuda.set_stream(cs)
+        try:
+            if len(known) < self.LOOKAHEAD:
+                a.dev.fill_(UNKNOWN_RUN)
+            for j, s in known:
+                a.dev[j:j + 1].copy_(s.cap)
+            if self._coll:
+                dist.all_reduce(a.dev, op=dist.ReduceOp.MAX, group=self._count_group)
+            a.host.copy_(a.dev, non_blocking=True)
+            a.ev.record(cs)
+        finally:
+            torch.cuda.set_stream(main)
+        self._agree_last_ev = a.ev
+
+    def _stage_slot(self, s: InputSlot, ids: torch.Tensor, ev_start, main) -> None:
+        """On the plan stream, after everything enqueued before this step and after the last
+        agreement (which reads staged slots' run maxima): ids into slot s, its plan."""
+        ps = self._plan_stream
+        ps.wait_event(ev_start)
+        if self._agree_last_ev is not None:
+            ps.wait_event(self._agree_last_ev)
+        torch.cuda.set_stream(ps)
+        try:
+            s.ids.copy_(ids, non_blocking=True)
+            if ids.is_cuda:
+                ids.record_stream(ps)
+            self._plan_slot(s)
+        finally:
+            torch.cuda.set_stream(main)
 
     def _slot_stream(self, stream_i: int):
         return self._plan_stream  # every slot is copied and planned on the one plan stream
 
     def _plan_slot(self, slot: InputSlot) -> None:
         """On the current (plan) stream: the slot's plan, its largest per-owner run
-        (slot.cap, int64 scalar) and an event."""
+        (slot.cap, int64 scalar) and an event. Replayed from the slot's own captured graph
+        once it exists (graphs on, no timing)."""
         if slot.cap is None:
             slot.cap = torch.zeros(1, dtype=torch.int64, device=self.device)
             slot.counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+        if slot.plan_graph is not None and self.timing is None:
+            slot.plan_graph.replay()
+        else:
+            self._plan_launch(slot)
+            if self.use_graphs and self.timing is None:
+                g = torch.cuda.CUDAGraph()
+                with graph_capture(g, pool=live_pool(self), stream=torch.cuda.current_stream()):
+                    self._plan_launch(slot)  # captured, not executed
+                slot.plan_graph = g
+        slot.ev = self._slot_event(slot)
+        slot.ev.record()
+
+    def _plan_launch(self, slot: InputSlot) -> None:
         slot.plan.build(slot.ids, self.V, err_flag=self.err)
         slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts)
         torch.amax(slot.counts, dim=0, keepdim=True, out=slot.cap)
-        slot.ev = torch.cuda.Event()
-        slot.ev.record()
 
     def _xb(self, B: int, F: int, C: int) -> _XBufs:
         key = (B, F, C)
@@ -398,6 +560,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         x, y = slot.ids, slot.y
         B, F = x.shape
         n = self.world_size
+        f = self._coll  # the collectives (N > 1, or forced on a one-rank group)
         b = self._buffers(B, F)
         b.plan = plan = slot.plan
         xb = self._xb(B, F, C)
@@ -409,7 +572,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         t = self._mark("exchange")
         hip_ops.shard_pack_ids(plan, self.shard_rows, self.V, n, C, xb.send_ids, xb.counts,
                                xb.offsets, err_flag=self.err)
-        alltoall_equal(xb.recv_ids, xb.send_ids, self.group)
+        alltoall_equal(xb.recv_ids, xb.send_ids, self.group, force=f)
         self._span("exchange", t)
         # 2. owners: catch the rows up, gather them, send them back
         t = self._mark("catchup")
@@ -420,13 +583,13 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("catchup", t)
         t = self._mark("exchange")
         hip_ops.embedding_gather(self.E_tab, xb.recv_ids, out=xb.rows_out)
-        alltoall_equal(xb.rows_in, xb.rows_out, self.group)
+        alltoall_equal(xb.rows_in, xb.rows_out, self.group, force=f)
         hip_ops.shard_runs_copy(xb.rows_in, xb.table, C, xb.counts, xb.offsets, pack=False)
         T_lin = None
         if has_lin:
             hip_ops.embedding_gather(self.w_tab.view(Vo, 1), xb.recv_ids,
                                      out=xb.lin_out.view(-1, 1))
-            alltoall_equal(xb.lin_in, xb.lin_out, self.group)
+            alltoall_equal(xb.lin_in, xb.lin_out, self.group, force=f)
             hip_ops.shard_runs_copy(xb.lin_in, xb.lin_table, C, xb.counts, xb.offsets, pack=False)
             T_lin = xb.lin_table.view(-1, 1)
         self._span("exchange", t)
@@ -437,14 +600,14 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 4. gradients to the owners, summed per row in (source rank, position) order
         t = self._mark("exchange")
         hip_ops.shard_runs_copy(b.grad_rows, xb.g_out, C, xb.counts, xb.offsets, pack=True)
-        alltoall_equal(xb.g_in, xb.g_out, self.group)
+        alltoall_equal(xb.g_in, xb.g_out, self.group, force=f)
         if has_lin:
             hip_ops.shard_runs_copy(b.grad_lin, xb.glin_out, C, xb.counts, xb.offsets, pack=True)
-            alltoall_equal(xb.glin_in, xb.glin_out, self.group)
+            alltoall_equal(xb.glin_in, xb.glin_out, self.group, force=f)
         self._join_wgrad()
-        allreduce_sum_(self.flat_grad, self.group)
-        if n > 1:
-            allreduce_sum_(b.loss, self.group)
+        allreduce_sum_(self.flat_grad, self.group, force=f)
+        if f:
+            allreduce_sum_(b.loss, self.group, force=f)
             b.loss.div_(n)
         self._span("exchange", t)
         t = self._mark("scatter")

@@ -511,7 +511,10 @@ class FusedCTRTrainer:
         step with other ids builds its plan as usual. next_y (optional, aligned with next_x):
         those batches' labels, copied into their slots on the plan stream as well, so the
         step that trains on them skips its label copy (the same tensor must then be passed
-        as that step's y; any other y is copied as usual).
+        as that step's y; any other y is copied as usual). A staged batch is recognised by
+        its tensor (address, shape, strides), not its contents: the ids and labels are those
+        the tensors held when they were staged, so a tensor refilled in place between its
+        staging and its step trains on the staged contents — refill a different buffer.
 
         Every step also adds its loss (fp64) to the device accumulator ``loss_sum`` inside
         the step's last launch — the driver's epoch loss without a host sync per step

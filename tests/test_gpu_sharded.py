@@ -124,11 +124,22 @@ def _rank_main(rank, world, port, kind, V, F, K, B, steps, q, drop=0.0, exchange
         assert torch.equal(sd["feature_embedding.weight"], E)
         # model.state_dict() is local (no collective): rank 0 alone may save it, and every
         # rank resumes from its own dict or from the full one (cut to its rows)
-        local = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        import io
+        buf = io.BytesIO()
+        torch.save(m.state_dict(), buf)  # the shard, its row range in the metadata
+        buf.seek(0)
+        local = torch.load(buf, weights_only=True)
         assert local["feature_embedding.weight"].shape[0] == rows
-        if rank == 0:
-            import io
-            torch.save(m.state_dict(), io.BytesIO())
+        assert list(local._metadata[""]["ctr_rows"]) == [tr.row_lo, tr.row_hi, V]
+        # another rank's shard (equal shard sizes here) or a shard without its row range is
+        # refused, not loaded as this rank's rows
+        other = [None, None]
+        dist.all_gather_object(other, buf.getvalue())
+        theirs = torch.load(io.BytesIO(other[1 - rank]), weights_only=True)
+        with pytest.raises(RuntimeError, match="row range"):
+            m.load_state_dict(theirs)
+        with pytest.raises(RuntimeError, match="row range"):
+            m.load_state_dict(dict(local))  # a plain dict: no metadata
         dist.barrier()
         m.load_state_dict(local)
         m.load_state_dict(sd)
@@ -361,48 +372,131 @@ def test_padded_exchange_equals_varsplit_world2_rccl(cuda, graphs):
             assert np.array_equal(a[3][k], b[3][k]), (rank, k)
 
 
-def _capacity_read_main(q):
-    """The capacity-read check in a process of its own (see the test)."""
-    import torch.distributed as dist
+@pytest.mark.parametrize("depth", [1, 2])
+def test_capacity_read_never_waits_for_main(cuda, depth):
+    """The row-sharded step's one host read (the agreed exchange capacity) never waits for
+    work enqueued on the main stream after the previous step() call: with a long sleep
+    kernel queued on the main stream between two calls, step() returns while the sleep still
+    runs. Run in the suite's own process, after every other test here has created its
+    streams: the agreement a step reads is enqueued by an earlier call (at its end), so in
+    FIFO order it precedes the sleep on whichever hardware queue its stream shares
+    (the stream-to-queue mapping)."""
     import rl_ctr_prediction_amd as P
     from rl_ctr_prediction_amd.synthetic import CriteoSynth
-    cuda = torch.device("cuda:0")
     V, F, K, B = 50_000, 26, 16, 512
     data = [tuple(torch.tensor(a, device=cuda) for a in xy)
-            for xy in CriteoSynth(V, F, seed=12).batches(3, B)]
+            for xy in CriteoSynth(V, F, seed=12).batches(4, B)]
     tr = P.ShardedCTRTrainer(_model("FM", V, F, K), lr=1e-3, weight_decay=1e-5, seed=3)
-    for i in range(9):  # every (slot, capacity) graph captured
-        tr.step(*data[i % 3], next_x=[data[(i + 1) % 3][0]], return_loss=False)
+
+    def nxt(i):
+        return [data[(i + j) % 4][0] for j in range(1, depth + 1)]
+
+    for i in range(12):  # every (slot, capacity) graph captured
+        tr.step(*data[i % 4], next_x=nxt(i), return_loss=False)
     torch.cuda.synchronize()
-    reads = tr.cap_reads
+    reads, blocking = tr.cap_reads, tr.cap_blocking
+    assert blocking == 1  # the first step only: nothing was agreed before it
     main = torch.cuda.current_stream()
     torch.cuda._sleep(600_000_000)  # 0.25-6 s of one wave spinning on the main stream
     after_sleep = torch.cuda.Event()
     after_sleep.record(main)
     t0 = time.perf_counter()
-    tr.step(*data[0], next_x=[data[1][0]], return_loss=False)
+    tr.step(*data[0], next_x=nxt(12), return_loss=False)
     host_s = time.perf_counter() - t0
     pending = not after_sleep.query()
     torch.cuda.synchronize()
     sleep_s = time.perf_counter() - t0
-    q.put(dict(reads=tr.cap_reads - reads, pending=pending, host_s=host_s, sleep_s=sleep_s,
-               dist=dist.is_initialized(), ws=tr.world_size, captures=tr.captures))
+    r = dict(reads=tr.cap_reads - reads, blocking=tr.cap_blocking - blocking,
+             pending=pending, host_s=host_s, sleep_s=sleep_s)
+    assert r["reads"] == 1 and r["blocking"] == 0, r
+    assert r["pending"], f"step() waited for the main stream: {r}"
 
 
-def test_capacity_read_never_waits_for_main(cuda):
-    """The row-sharded step's one host read (the agreed exchange capacity) waits for the
-    batch's plan only, never for the main stream: with a long sleep kernel queued on the
-    main stream ahead of the step, step() returns while the sleep still runs (graphs
-    captured in the warm-up; the batch planned ahead by the previous step's next_x). Run in
-    a fresh process: in the suite's process, after the multi-process tests above had used
-    the GPU, the host's wait was seen to take the whole sleep on some runs and not on
-    others (the same check alone or in a fresh process: 0.2-0.5 ms, the sleep pending)."""
+def test_capacity_agreement_mismatch(cuda):
+    """A step whose batch is not the one announced for it (next_x) is agreed in the step
+    (one process; with collectives the ranks sized the step by the announced batch and the
+    step raises instead); steps without lookahead agree in the step, and every result is
+    bitwise the fused trainer's."""
+    import rl_ctr_prediction_amd as P
+    from rl_ctr_prediction_amd.synthetic import CriteoSynth
+    V, F, K, B = 50_000, 26, 16, 512
+    data = [tuple(torch.tensor(a, device=cuda) for a in xy)
+            for xy in CriteoSynth(V, F, seed=13).batches(6, B)]
+    out = {}
+    for name in ("fused", "sharded"):
+        m = _model("FM", V, F, K)
+        tr = (P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3) if name == "fused" else
+              P.ShardedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3))
+        # announced 1, 2; then 5 trains instead of 2 (a decoy), no lookahead, then 3, 4:
+        # agreed in the step at calls 0 (first), 2 (decoy), 3 and 5 (nothing announced)
+        order = [(0, [1, 2]), (1, [2]), (5, None), (3, [4]), (4, None), (2, [0])]
+        losses = [tr.step(*data[i], next_x=None if n is None else [data[j][0] for j in n]
+                          ).item() for i, n in order]
+        tr.flush()
+        out[name] = (losses, m.feature_embedding.weight.detach().clone())
+        if name == "sharded":
+            assert tr.cap_reads == len(order) and tr.cap_blocking == 4, (
+                tr.cap_reads, tr.cap_blocking)
+    assert out["fused"][0] == out["sharded"][0]
+    assert torch.equal(out["fused"][1], out["sharded"][1])
+
+
+def _rccl_world1_main(q, port, kind, V, F, K, B, steps):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        import rl_ctr_prediction_amd as P
+        from rl_ctr_prediction_amd.synthetic import CriteoSynth
+        data = [tuple(torch.tensor(a, device=dev) for a in xy)
+                for xy in CriteoSynth(V, F, seed=31).batches(steps, B)]
+        res = {}
+        for name, force, graphs in (("local", False, True), ("rccl_eager", True, False),
+                                    ("rccl_graphs", True, True)):
+            m = _model(kind, V, F, K, drop=0.2, device=dev)
+            tr = P.ShardedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3,
+                                     force_collectives=force)
+            tr.use_graphs = graphs
+            losses = [tr.step(*data[i], next_x=[d[0] for d in data[i + 1:i + 3]]).item()
+                      for i in range(steps)]
+            tr.check_errors()
+            E, w = tr.gather_tables()
+            res[name] = dict(losses=losses, E=E.cpu().numpy(),
+                             w=None if w is None else w.cpu().numpy(),
+                             dense={k: v.detach().cpu().numpy() for k, v in tr.views.items()},
+                             m=tr.m_E[:tr.V_tab].cpu().numpy(), v=tr.v_E[:tr.V_tab].cpu().numpy(),
+                             captures=tr.captures, blocking=tr.cap_blocking,
+                             backend=dist.get_backend(tr.group))
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,K", [("DeepFM", 16), ("FM", 32)])
+def test_rccl_world1_collectives_bitwise(cuda, kind, K):
+    """RCCL on the hardware: the row-sharded step with every exchange sent through the
+    collectives of a one-rank nccl (RCCL) process group — equal-split all_to_all_single for
+    ids / rows / gradients, all_reduce for the dense gradient, the loss and the capacity
+    agreements — eager and captured into the step's HIP graphs, is bitwise the local-copy
+    step over 5 steps with two batches of lookahead (dropout on)."""
+    V, F, B, steps = 40_000, 26, 512, 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_capacity_read_main, args=(q,))
+    p = ctx.Process(target=_rccl_world1_main, args=(q, _free_port(), kind, V, F, K, B, steps))
     p.start()
-    r = q.get(timeout=180)
+    res = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
-    assert r["reads"] == 1, r
-    assert r["pending"], f"step() waited for the main stream: {r}"
+    a = res["local"]
+    assert res["rccl_graphs"]["captures"] >= 1 and res["rccl_eager"]["captures"] == 0
+    assert res["rccl_graphs"]["backend"] == "nccl"
+    for name in ("rccl_eager", "rccl_graphs"):
+        b = res[name]
+        assert a["losses"] == b["losses"], name
+        for k in ("E", "w", "m", "v"):
+            if a[k] is not None:
+                assert np.array_equal(a[k], b[k]), (name, k)
+        for k in a["dense"]:
+            assert np.array_equal(a["dense"][k], b["dense"][k]), (name, k)

@@ -4,8 +4,9 @@
 
 At N = 1 the sharded step is the N > 1 launch sequence with every collective a local copy.
 Prints one JSON line: host ms per step of eager steps (use_graphs off: every launch issued
-from Python, as at N > 1 by default) and of graph-replayed steps, and the wall ms per step of
-each. The launch count per step comes from a kernel trace of the same run
+from Python) and of graph-replayed steps, the wall ms per step of each, the host time per
+section of step() (ShardedCTRTrainer.host_sections: prologue, capacity_read, step_launch,
+stage_ahead, agreement_issue) and the agreements made inside a step (0 with lookahead). The launch count per step comes from a kernel trace of the same run
 (rocprofv3 --kernel-trace, then tools/timeline.py --marker step_end_kernel: the kernels
 between two step ends; the N > 1 step adds its collectives: 4 equal-split all-to-alls of
 ids / rows / gradients (+2 for the linear table), one all-reduce of the dense gradient, and
@@ -53,6 +54,8 @@ def main():
             tr.step(xs[i], ys[i], next_x=xs[i + 1:i + 3], return_loss=False)
             i += 1
         torch.cuda.synchronize()
+        blocking0 = tr.cap_blocking
+        tr.host_sections = {}
         t_host, t0 = 0.0, time.perf_counter()
         for _ in range(args.steps):
             h = time.perf_counter()
@@ -63,6 +66,10 @@ def main():
         key = "graphs" if graphs else "eager"
         res[f"{key}_host_ms_per_step"] = t_host / args.steps * 1e3
         res[f"{key}_ms_per_step"] = (time.perf_counter() - t0) / args.steps * 1e3
+        res[f"{key}_sections_ms_per_step"] = {k: v / args.steps * 1e3
+                                              for k, v in tr.host_sections.items()}
+        res[f"{key}_blocking_agreements"] = tr.cap_blocking - blocking0
+        tr.host_sections = None
         del tr, m
     print(json.dumps(res), flush=True)
 
