@@ -102,7 +102,7 @@ class _Agreement:
         self.host = torch.empty(n, dtype=torch.int64, pin_memory=True)
         self.ev = torch.cuda.Event()
         self.keys = [None] * n  # this rank's batch (ids key) behind each entry
-        self.call = -1          # the step() call that issued it
+        self.call = None        # the step() call that issued it
 
 
 class ShardedCTRTrainer(FusedCTRTrainer):
@@ -153,6 +153,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if not self._vec_ok:
             raise ValueError("row sharding needs K % 4 == 0 and (K/4) dividing 64")
         self._side = None  # the exchange needs the plan before anything else
+        self._pipe = False  # the dense gradient is all-reduced within its step
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
         # the plans (and per-owner counts / run maxima) are built on the plan stream, ahead

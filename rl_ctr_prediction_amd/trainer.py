@@ -76,8 +76,14 @@ def flush_hooks(model: nn.Module, trainer) -> None:
         t = ref()
         if t is not None:
             t.flush()
+
+    def drain(*_):  # a pending weight-gradient tail is applied before the loaded values land
+        t = ref()
+        if t is not None:
+            t._drain_tail()
     model.register_forward_pre_hook(flush)
     model.register_state_dict_pre_hook(flush)
+    model._register_load_state_dict_pre_hook(drain)
 
 
 class _nullctx:
@@ -144,6 +150,7 @@ class _Bufs:
     dslot: torch.Tensor | None = None  # IPNN: per-slot embedding gradients [S, K]
     zero: torch.Tensor | None = None   # IPNN: the (absent) FM logit, zeros [B]
     plan_own: hip_ops.SparsePlanBuffers | None = None  # the shape's plan without lookahead
+    xps: tuple = ()  # the X plane buffers (two when the weight-gradient tail is pipelined)
 
 
 class FusedCTRTrainer:
@@ -299,6 +306,19 @@ class FusedCTRTrainer:
         # in one step and none in the next)
         self._stage_seq = 0
         self._extra_plan_streams: list = []
+        # cross-step pipelining of the MLP kinds' weight-gradient tail (one process, deferred
+        # mode): the largest weight gradient dW0 = dH1^T X and the MLP weights' Adam of step t
+        # run at the START of step t+1's graph, on the side stream beside its catch-up and
+        # gather (which read no MLP weight), joined before its first GEMM — instead of beside
+        # step t's scatter chain, where the two shared the CUs and HBM. The
+        # MLP input planes X alternate between two buffers (step t+1's gather writes one
+        # while dW0 of step t reads the other). A pending tail is applied by flush() (model
+        # forward / state_dict / load_state_dict hooks, the epoch end) and by _drain_tail().
+        env = os.environ.get("CTR_PIPELINE_WGRAD")
+        self._pipe = (self.kind in _MLP_KINDS and self.deferred and self._side is not None
+                      and world()[1] == 1 and env != "0")
+        self._tail = None   # (bufset, X planes) of the step whose dW0 + MLP Adam is pending
+        self._xp_flip = 0   # which of the two X plane buffers this step writes
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -383,8 +403,15 @@ class FusedCTRTrainer:
 
     # ----------------------------------------------------------------- optimiser -----
     def flush(self) -> None:
-        """Bring every embedding row up to the last completed step (deferred mode). The
-        plan streams only read staged ids and write plans: nothing to wait for."""
+        """Apply the pending weight-gradient tail (pipelined MLP kinds) and bring every
+        embedding row up to the last completed step (deferred mode): every parameter and
+        moment is then the reference's after the last step. The plan streams only read
+        staged ids and write plans: nothing to wait for."""
+        self._drain_tail()
+        self._flush_table()
+
+    def _flush_table(self) -> None:
+        """The embedding rows up to the last completed step (deferred mode)."""
         self._flushed_at = self.step_count
         if self.deferred and self._dirty and self.step_count > 0:
             t = self._mark("flush")
@@ -417,7 +444,7 @@ class FusedCTRTrainer:
         more than that many steps behind when a batch reads it."""
         if (self.deferred and self.flush_every > 0
                 and self.step_count - self._flushed_at >= self.flush_every):
-            self.flush()
+            self._flush_table()  # the tables only: the pipelined tail stays pending
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.Adam-compatible state_dict (parameter order = model.parameters())."""
@@ -471,6 +498,8 @@ class FusedCTRTrainer:
             # db1 = colsum dH2 as one more output column
             # ... and so does the MLP input X (db0 = colsum dH1 from dW0, CTR_WGRAD_ORDER)
             b.xp = P(B, W, dev, ones_col=True)
+            # pipelined tail: two X plane buffers, alternating by step (_launch)
+            b.xps = (b.xp, P(B, W, dev, ones_col=True)) if self._pipe else (b.xp,)
             b.h1p = P(B, H1, dev, ones_col=True)
             b.dh2p, b.dh1p = P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
@@ -731,6 +760,33 @@ class FusedCTRTrainer:
         self.step_count += 1
         if self.deferred:
             self._dirty = True
+        if self._pipe and self._bufs is not None and self._bufs.xps:
+            # this step's dW0 + MLP Adam are pending; the next step writes the other X planes
+            self._tail = (self._bufs, self._bufs.xp)
+            self._xp_flip ^= 1
+
+    def _pipe_state(self):
+        """(X plane buffer index of the next step, its pending tail or None)."""
+        return (self._xp_flip, self._tail) if self._pipe else (0, None)
+
+    def _drain_tail(self) -> None:
+        """Apply the pending weight-gradient tail now, on the current stream (eager)."""
+        if self._tail is None:
+            return
+        tail, self._tail = self._tail, None
+        with self._scratch.scope():
+            self._tail_launch(tail)
+
+    def _tail_launch(self, tail) -> None:
+        """dW0 = dH1^T X (+ db0 from X's ones column) of the pending step and the Adam step of
+        the MLP parameters with it, on the current stream. The step is the last completed one
+        (the device counter step_done: read at run time, so a captured tail replays right)."""
+        b, xp = tail
+        gv = self.grad_views
+        H1, W = b.h1.shape[1], b.dx.shape[1]
+        self._gemm_planes(b.dh1p, xp, True, True, H1, W, b.B,
+                          out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
+        self._adam_dense(self.step_count, part="mlp", step_dev=self.step_done)
 
     def _graph_step(self, slot: InputSlot, mean_div: float, have: bool):
         if self.step_table.capacity < self.step_count + 2:
@@ -741,36 +797,47 @@ class FusedCTRTrainer:
             self._graph_tab_version = self.step_table.version
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
-        key = (slot.shape, slot.index, mean_div, self.model.training, drops, have)
+        pipe = self._pipe_state()
+        key = (slot.shape, slot.index, mean_div, self.model.training, drops, have,
+               pipe[0], None if pipe[1] is None else pipe[1][0].B)
         hit = self._graphs.get(key)
         if hit is None:
             # the real step (sizes every buffer), then the same launches captured
-            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
+            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan, pipe=pipe)
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
                 with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
-                    self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
+                    self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan, pipe=pipe)
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1
             return loss
         g, self._bufs = hit  # the buffer set the graph was captured with
         self._bufs.plan = slot.plan
+        if pipe[0] < len(self._bufs.xps):
+            self._bufs.xp = self._bufs.xps[pipe[0]]
         g.replay()
         self._after_step()
         return self._bufs.loss
 
     def _launch(self, x: torch.Tensor, y: torch.Tensor, mean_div: float,
-                have_plan: bool = False, plan: hip_ops.SparsePlanBuffers | None = None
-                ) -> torch.Tensor:
+                have_plan: bool = False, plan: hip_ops.SparsePlanBuffers | None = None,
+                pipe=None) -> torch.Tensor:
         """Enqueue one step. Changes no host state: step-dependent values come from
         self.step_ctr (advanced on the device), so the launch sequence can be captured.
         plan: the batch's plan buffers (its input slot's; built here unless have_plan —
-        built ahead on the plan stream by the previous steps' lookahead)."""
+        built ahead on the plan stream by the previous steps' lookahead). pipe: the
+        pipelined tail state (_pipe_state(), taken before the step)."""
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
         b.plan = plan if plan is not None else b.plan_own
+        if pipe is None:
+            pipe = self._pipe_state()
+        piped = self._pipe and bool(b.xps)
+        if piped:
+            b.xp = b.xps[pipe[0]]
+        b.ev_tail = None
         y = y.reshape(-1)
         if y.dtype != torch.float32:
             y = y.float()
@@ -822,6 +889,15 @@ class FusedCTRTrainer:
                                                   step_hint, self.betas, self.eps,
                                                   self.weight_decay)
             self._span("catchup", t)
+            if piped and pipe[1] is not None:
+                # the previous step's dW0 + MLP Adam beside this step's catch-up and gather
+                # (one side list: the plan, when built in-step, follows it there)
+                side = self._wgrad_stream
+                side.wait_event(ev0)
+                with torch.cuda.stream(side):
+                    self._tail_launch(pipe[1])
+                    b.ev_tail = torch.cuda.Event()
+                    b.ev_tail.record()
             if not self.plan_first:
                 plan()
         else:
@@ -910,25 +986,39 @@ class FusedCTRTrainer:
         if wg is None:
             self._join_wgrad()
         with torch.cuda.stream(wg) if wg is not None else _nullctx():
-            self._adam_dense(step_hint)
+            # pipelined: the FM bias now (the next step's gather reads it), the MLP at the
+            # start of the next step (_tail_launch)
+            self._adam_dense(step_hint, part="bias" if piped else "all")
         self._join_wgrad()
         hip_ops.step_end(self.step_ctr, b.loss, self.loss_sum)
         return b.loss
 
-    def _adam_dense(self, step_hint: int) -> None:
+    def _adam_dense(self, step_hint: int, part: str = "all", step_dev=None) -> None:
         """The flat dense parameters' Adam step; the MLP weights' planes are rewritten with
         the updated values (the next step's GEMM operands) — by the Adam kernel itself when
-        a weight's row length is a multiple of 4, by a split pass after it otherwise."""
+        a weight's row length is a multiple of 4, by a split pass after it otherwise.
+        part: "all", "bias" (the FM bias alone: the flat buffer ahead of mlp.0.weight) or
+        "mlp" (from mlp.0.weight on) — elementwise, so the two parts are bitwise the one
+        launch. step_dev: the device step counter to read (default: the step in flight)."""
+        lo = 0
+        hi = self.flat.numel()
+        if part != "all" and "mlp.0.weight" in self.offsets:
+            cut = self.offsets["mlp.0.weight"]
+            lo, hi = (0, cut) if part == "bias" else (cut, hi)
+        if lo == hi:
+            return
         planes, resplit = [], []
-        if self._wplanes is not None:
+        if self._wplanes is not None and part != "bias":
             for name, pl in zip(("mlp.0.weight", "mlp.3.weight"), self._wplanes):
-                if pl.cols % 4 == 0 and self.offsets[name] % 4 == 0:
-                    planes.append((self.offsets[name], pl))
+                if pl.cols % 4 == 0 and (self.offsets[name] - lo) % 4 == 0:
+                    planes.append((self.offsets[name] - lo, pl))
                 else:
                     resplit.append((name, pl))
-        hip_ops.adam_dense(self.flat, self.flat_grad, self.m_flat, self.v_flat, step_hint,
-                           self.lr, self.betas, self.eps, self.weight_decay,
-                           step_dev=self.step_cur, table=self.step_table, planes=planes or None)
+        hip_ops.adam_dense(self.flat[lo:hi], self.flat_grad[lo:hi], self.m_flat[lo:hi],
+                           self.v_flat[lo:hi], step_hint, self.lr, self.betas, self.eps,
+                           self.weight_decay,
+                           step_dev=self.step_cur if step_dev is None else step_dev,
+                           table=self.step_table, planes=planes or None)
         for name, pl in resplit:
             hip_ops.split_planes(self.views[name], out=pl)
 
@@ -966,6 +1056,8 @@ class FusedCTRTrainer:
         if X is not None:
             hip_ops.split_planes(X, out=b.xp)
         self._span("gather", t)
+        if getattr(b, "ev_tail", None) is not None:  # the previous step's MLP Adam
+            torch.cuda.current_stream().wait_event(b.ev_tail)
         # Linear(F*K,300)+ReLU+Dropout: H1 (fp32 for the mask, planes for the next GEMMs)
         self._gemm_planes(b.xp, w0p, False, False, B, H1, W, out=b.h1, out_planes=b.h1p,
                           epi=hip_ops.EPI_BIAS_RELU_DROP if p0 > 0 else hip_ops.EPI_BIAS_RELU,
@@ -1032,8 +1124,9 @@ class FusedCTRTrainer:
             # Linear(F*K,300)'s db0 = colsum dH1 comes out of dW0 = dH1^T X as the ones
             # column of X
             hip_ops.colsum_multi(jobs)
-            self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
-                              out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
+            if not (self._pipe and len(b.xps) > 1):  # pipelined: at the next step's start
+                self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
+                                  out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
 
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""

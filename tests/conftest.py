@@ -167,6 +167,7 @@ def fused_grads(tr):
     (E grad [V,K], w grad [V,1] or None, {dense name: grad})."""
     import torch
     assert getattr(tr, "keep_grads", True), "set tr.keep_grads = True before stepping"
+    tr._drain_tail()  # a pipelined trainer's last dW0 (and its MLP Adam) is still pending
     b = tr._bufs
     U = b.plan.num_unique_host()
     rows = b.plan.unique_rows[:U].long()

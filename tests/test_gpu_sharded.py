@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import gc
 import os
 import socket
 import time
@@ -469,8 +470,13 @@ def _rccl_world1_main(q, port, kind, V, F, K, B, steps):
                              m=tr.m_E[:tr.V_tab].cpu().numpy(), v=tr.v_E[:tr.V_tab].cpu().numpy(),
                              captures=tr.captures, blocking=tr.cap_blocking,
                              backend=dist.get_backend(tr.group))
+            # the captured graphs (RCCL kernels inside) go before the communicators do
+            torch.cuda.synchronize()
+            del tr, m, E, w
+            gc.collect()
         q.put(res)
     finally:
+        torch.cuda.synchronize()
         dist.destroy_process_group()
 
 
@@ -486,8 +492,13 @@ def test_rccl_world1_collectives_bitwise(cuda, kind, K):
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_world1_main, args=(q, _free_port(), kind, V, F, K, B, steps))
     p.start()
-    res = q.get(timeout=300)
-    p.join(timeout=60)
+    try:
+        res = q.get(timeout=300)
+        p.join(timeout=60)
+    finally:
+        if p.is_alive():  # never leave a rank behind on the device
+            p.kill()
+            p.join(timeout=30)
     assert p.exitcode == 0
     a = res["local"]
     assert res["rccl_graphs"]["captures"] >= 1 and res["rccl_eager"]["captures"] == 0
