@@ -150,7 +150,8 @@ class _Bufs:
     dslot: torch.Tensor | None = None  # IPNN: per-slot embedding gradients [S, K]
     zero: torch.Tensor | None = None   # IPNN: the (absent) FM logit, zeros [B]
     plan_own: hip_ops.SparsePlanBuffers | None = None  # the shape's plan without lookahead
-    xps: tuple = ()  # the X plane buffers (two when the weight-gradient tail is pipelined)
+    xps: dict | None = None  # pipelined tail: X plane buffers by index (_xp_for)
+    xp_idx: int = 0
 
 
 class FusedCTRTrainer:
@@ -311,14 +312,18 @@ class FusedCTRTrainer:
         # run at the START of step t+1's graph, on the side stream beside its catch-up and
         # gather (which read no MLP weight), joined before its first GEMM — instead of beside
         # step t's scatter chain, where the two shared the CUs and HBM. The
-        # MLP input planes X alternate between two buffers (step t+1's gather writes one
-        # while dW0 of step t reads the other). A pending tail is applied by flush() (model
+        # MLP input planes X are per input slot (step t+1's gather writes its slot's
+        # while dW0 of step t reads step t's slot's; _pipe_state). A pending tail is applied by flush() (model
         # forward / state_dict / load_state_dict hooks, the epoch end) and by _drain_tail().
+        # Opt-in (CTR_PIPELINE_WGRAD=1): bitwise the in-step tail, but measured slower at C3
+        # (11.77 / 11.89 vs 12.77 / 12.62 M ex/s, alternating): the scatter chain loses dW0's
+        # contention (105 -> 76 us) but the gather beside dW0 takes 85 us instead of 28
+        # (profiles/r05_pipelined_tail.txt)
         env = os.environ.get("CTR_PIPELINE_WGRAD")
         self._pipe = (self.kind in _MLP_KINDS and self.deferred and self._side is not None
-                      and world()[1] == 1 and env != "0")
-        self._tail = None   # (bufset, X planes) of the step whose dW0 + MLP Adam is pending
-        self._xp_flip = 0   # which of the two X plane buffers this step writes
+                      and world()[1] == 1 and env == "1")
+        # (bufset, X planes, their index) of the step whose dW0 + MLP Adam is pending
+        self._tail = None
         self.step_table = hip_ops.AdamStepTable(self.lr, self.betas, self.device)
         self._dirty = False
         if self.deferred:  # nothing may read a table with rows still owed steps
@@ -498,8 +503,8 @@ class FusedCTRTrainer:
             # db1 = colsum dH2 as one more output column
             # ... and so does the MLP input X (db0 = colsum dH1 from dW0, CTR_WGRAD_ORDER)
             b.xp = P(B, W, dev, ones_col=True)
-            # pipelined tail: two X plane buffers, alternating by step (_launch)
-            b.xps = (b.xp, P(B, W, dev, ones_col=True)) if self._pipe else (b.xp,)
+            # pipelined tail: one X plane buffer per input slot (+ a spare), _xp_for
+            b.xps = {0: b.xp} if self._pipe else None
             b.h1p = P(B, H1, dev, ones_col=True)
             b.dh2p, b.dh1p = P(B, H2, dev), P(B, H1, dev)
             if self.kind == "IPNN":
@@ -618,7 +623,8 @@ class FusedCTRTrainer:
             loss = self._graph_step(slot, mean_div, have)
         else:
             self.step_table.ensure(self.step_count + 1)
-            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan)
+            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan,
+                                pipe=self._pipe_state(slot))
             self._after_step()
         for n, k in todo:
             self._stage_ahead(n, k, shape, slot, ev_start, main, ny.get(k))
@@ -760,14 +766,30 @@ class FusedCTRTrainer:
         self.step_count += 1
         if self.deferred:
             self._dirty = True
-        if self._pipe and self._bufs is not None and self._bufs.xps:
-            # this step's dW0 + MLP Adam are pending; the next step writes the other X planes
-            self._tail = (self._bufs, self._bufs.xp)
-            self._xp_flip ^= 1
+        if self._pipe and self._bufs is not None and self._bufs.xps is not None:
+            # this step's dW0 + MLP Adam are pending (they read its X planes)
+            self._tail = (self._bufs, self._bufs.xp, self._bufs.xp_idx)
 
-    def _pipe_state(self):
-        """(X plane buffer index of the next step, its pending tail or None)."""
-        return (self._xp_flip, self._tail) if self._pipe else (0, None)
+    def _pipe_state(self, slot: InputSlot):
+        """(X plane buffer index of a step on `slot`, the pending tail or None). Each input
+        slot writes X planes of its own, so in a slot ring the pending tail (the previous
+        step, another slot) never holds the buffer the next gather writes: the steady state
+        replays one graph per slot. A step on the slot of the pending tail (a repeated slot:
+        no lookahead) writes the spare buffer (-1)."""
+        if not self._pipe:
+            return (0, None)
+        idx, tail = slot.index, self._tail
+        if tail is not None and tail[0].B == slot.shape[0] and tail[2] == idx:
+            idx = -1
+        return (idx, tail)
+
+    def _xp_for(self, b: _Bufs, idx: int):
+        """The bufset's X plane buffer number idx (allocated on first use, never inside a
+        capture: the eager step that precedes each capture allocates it)."""
+        xp = b.xps.get(idx)
+        if xp is None:
+            xp = b.xps[idx] = hip_ops.Planes(b.B, b.xp.cols, self.device, ones_col=True)
+        return xp
 
     def _drain_tail(self) -> None:
         """Apply the pending weight-gradient tail now, on the current stream (eager)."""
@@ -781,7 +803,7 @@ class FusedCTRTrainer:
         """dW0 = dH1^T X (+ db0 from X's ones column) of the pending step and the Adam step of
         the MLP parameters with it, on the current stream. The step is the last completed one
         (the device counter step_done: read at run time, so a captured tail replays right)."""
-        b, xp = tail
+        b, xp = tail[0], tail[1]
         gv = self.grad_views
         H1, W = b.h1.shape[1], b.dx.shape[1]
         self._gemm_planes(b.dh1p, xp, True, True, H1, W, b.B,
@@ -797,9 +819,9 @@ class FusedCTRTrainer:
             self._graph_tab_version = self.step_table.version
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
-        pipe = self._pipe_state()
+        pipe = self._pipe_state(slot)
         key = (slot.shape, slot.index, mean_div, self.model.training, drops, have,
-               pipe[0], None if pipe[1] is None else pipe[1][0].B)
+               pipe[0], None if pipe[1] is None else (pipe[1][0].B, pipe[1][2]))
         hit = self._graphs.get(key)
         if hit is None:
             # the real step (sizes every buffer), then the same launches captured
@@ -814,8 +836,9 @@ class FusedCTRTrainer:
             return loss
         g, self._bufs = hit  # the buffer set the graph was captured with
         self._bufs.plan = slot.plan
-        if pipe[0] < len(self._bufs.xps):
+        if self._bufs.xps is not None:  # the buffer the graph's gather writes
             self._bufs.xp = self._bufs.xps[pipe[0]]
+            self._bufs.xp_idx = pipe[0]
         g.replay()
         self._after_step()
         return self._bufs.loss
@@ -827,16 +850,16 @@ class FusedCTRTrainer:
         self.step_ctr (advanced on the device), so the launch sequence can be captured.
         plan: the batch's plan buffers (its input slot's; built here unless have_plan —
         built ahead on the plan stream by the previous steps' lookahead). pipe: the
-        pipelined tail state (_pipe_state(), taken before the step)."""
+        pipelined tail state (_pipe_state(slot), taken before the step; None: not
+        pipelined — the replicated N > 1 path)."""
         B, F = x.shape
         rank, ws = world()
         b = self._buffers(B, F)
         b.plan = plan if plan is not None else b.plan_own
-        if pipe is None:
-            pipe = self._pipe_state()
-        piped = self._pipe and bool(b.xps)
+        piped = self._pipe and b.xps is not None and pipe is not None
         if piped:
-            b.xp = b.xps[pipe[0]]
+            b.xp = self._xp_for(b, pipe[0])
+            b.xp_idx = pipe[0]
         b.ev_tail = None
         y = y.reshape(-1)
         if y.dtype != torch.float32:
@@ -1124,7 +1147,7 @@ class FusedCTRTrainer:
             # Linear(F*K,300)'s db0 = colsum dH1 comes out of dW0 = dH1^T X as the ones
             # column of X
             hip_ops.colsum_multi(jobs)
-            if not (self._pipe and len(b.xps) > 1):  # pipelined: at the next step's start
+            if not (self._pipe and b.xps is not None):  # pipelined: at the next step's start
                 self._gemm_planes(b.dh1p, b.xp, True, True, H1, W, B,
                                   out=gv["mlp.0.weight"], last_col=gv["mlp.0.bias"])
 

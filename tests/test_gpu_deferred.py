@@ -91,8 +91,8 @@ def test_graph_replay_equals_eager_bitwise(cuda, kind, mode):
         tr.use_graphs = graphs
         losses = [tr.step(*data[i % 3]).item() for i in range(8)]  # 1 eager+capture, 7 replays
         if graphs:  # every batch goes through the shape's one input slot: one graph (the
-            # pipelined MLP kinds: X plane buffer x pending tail — the first step's, then the
-            # two alternating ones)
+            # pipelined MLP kinds: the first step's, then the slot's and the spare X plane
+            # buffers alternating with the pending tail)
             n = 3 if tr._pipe else 1
             assert tr.captures == n and len(tr._graphs) == n
         sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
@@ -251,7 +251,7 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         out.append((losses, sd, st))
         if graphs:  # (slot, planned ahead) pairs of a ring of ahead + 1 slots (x the
             # pipelined kinds' X plane buffer and pending-tail variants)
-            assert tr.captures <= 2 * (ahead + 1) * (4 if tr._pipe else 1)
+            assert tr.captures <= 2 * (ahead + 1) * (3 if tr._pipe else 1)
     for losses, sd, st in out[1:]:
         assert losses == out[0][0]
         for k in sd:
@@ -325,8 +325,7 @@ def test_pipelined_wgrad_tail_bitwise(cuda, kind, graphs):
         with torch.device("cuda:0"):
             m = P.DeepFM(V, F, K) if kind == "DeepFM" else P.InnerPNN(V, F, K)
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7)
-        assert tr._pipe
-        tr._pipe = piped
+        tr._pipe = piped  # (opt-in: CTR_PIPELINE_WGRAD=1)
         tr.use_graphs = graphs
         tr.flush_every = 3
         losses, mid = [], None
