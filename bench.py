@@ -471,7 +471,7 @@ def main():
                          "batches after the timed region)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch every step eagerly (no HIP-graph replay): the host-paced "
-                         "launch path that N > 1 row sharding takes without CTR_SHARDED_GRAPHS")
+                         "launch path (N > 1 row sharding over gloo, or CTR_SHARDED_GRAPHS=0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

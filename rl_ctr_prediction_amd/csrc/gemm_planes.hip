@@ -250,12 +250,20 @@ __device__ __forceinline__ void planes_store(const PlanesArgs& a, pf32x4 (&acc)[
 // of the N tiles of a quarter of the M rows (dX: each XCD's share of W0 is 1.6 of 3.2 MB,
 // so it stays in the 4 MiB L2 beside the streamed dH1 rows). Falls back to g = 1, then to
 // the identity, where the grid does not divide.
+// g = 3: whole M rows per XCD as g = 1, but each XCD walks its rows N-tile-major (one B
+// column strip for all of its M rows, then the next): its A rows (dX: 16 x 123 KB of dH1
+// planes) stay L2-resident while each B strip streams through once per XCD, instead of all
+// of B once per M row (round-4 counters: dX 160 MB of HBM traffic against 72 algorithmic).
 __device__ __forceinline__ int64_t planes_tile_index(int64_t gn, int g) {
   const int64_t T = gridDim.x;
   const int64_t b = blockIdx.x;
   if (T % 8 != 0) return b;
   const int64_t x = b % 8, i = b / 8;
   const int64_t gm = T / gn;
+  if (g == 3 && gm % 8 == 0) {
+    const int64_t gmx = gm / 8;
+    return (x * gmx + i % gmx) * gn + i / gmx;
+  }
   if (g > 1 && 8 % g == 0 && gn % g == 0 && gm % (8 / g) == 0) {
     const int64_t gnn = gn / g, gmm = gm / (8 / g);
     const int64_t mt = (x / g) * gmm + i / gnn, nt = (x % g) * gnn + i % gnn;
@@ -589,6 +597,10 @@ static const PlDef kPl[] = {
     {256, 64, 4, 2, 2, 1, 0.60},   // 26: 120 KB (dW1: M = 200)
     {192, 64, 4, 2, 2, 1, 0.60},   // 27: 96 KB
     {320, 64, 2, 2, 2, 1, 0.60},   // 28: 144 KB, 4 waves (TM 10)
+    // taller forward tiles (fwd0: N = 300 in two 160 strips; with split-K 2 still 256
+    // blocks): W0's strip is re-read by half as many blocks, 27 KB of fill per
+    // 64 x 160 x 32 of work instead of 43
+    {128, 160, 4, 2, 2, 1, 0.62},  // 29: 110 KB
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -641,7 +653,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
                  &used) >= 8 && m == M && n == N && k == Kp && ar == (int)a_rc &&
           br == (int)b_rc && ti >= 0 && ti < kNumPl && sp >= 1 && pl_valid(ti, a_rc, b_rc)) {
         PlCfg c = mk(ti, sp);
-        c.xg = xg == 2 || xg == 4 || xg == 8 ? xg : 1;
+        c.xg = xg == 2 || xg == 3 || xg == 4 || xg == 8 ? xg : 1;
         if (pl_ks_ok(kPl[ti], Kp, c.kps)) return c;
       }
       q = strchr(q, ';');
@@ -653,7 +665,7 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     if (sscanf(env, "%d,%d,%d", &ti, &sp, &xg) >= 1 && ti >= 0 && ti < kNumPl && sp >= 1 &&
         pl_valid(ti, a_rc, b_rc)) {
       PlCfg c = mk(ti, sp);
-      c.xg = xg == 2 || xg == 4 || xg == 8 ? xg : 1;
+      c.xg = xg == 2 || xg == 3 || xg == 4 || xg == 8 ? xg : 1;
       if (pl_ks_ok(kPl[ti], Kp, c.kps)) return c;
     }
   }
@@ -707,8 +719,8 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   PlCfg best = mk(0, 1);
   double best_t = 1e30;
   for (int ti = 0; ti < kNumPl; ++ti) {
-    // the model: KS = 1 only
-    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1) continue;
+    // the model: KS = 1 only, the round-2 tilings (later ones by measured rules only)
+    if (!pl_valid(ti, a_rc, b_rc) || kPl[ti].ks != 1 || ti >= 29) continue;
     const PlDef& d = kPl[ti];
     const int64_t tiles = ceil_div(M, d.bm) * ceil_div(N, d.bn);
     for (int s = 1; s <= 32; ++s) {
@@ -778,6 +790,7 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 26: CTR_PL_ALL4(256, 64, 4, 2, 2) break;
     case 27: CTR_PL_ALL4(192, 64, 4, 2, 2) break;
     case 28: CTR_PL_ALL4(320, 64, 2, 2, 2) break;
+    case 29: CTR_PL_AONLY(128, 160, 4, 2, 2) break;
   }
 }
 #undef CTR_PL_AONLY

@@ -19,8 +19,7 @@ per step:
      (ctr_shard_pack_ids: each owner's run, padded with the owner's spare row), rows back,
      gradients out (ctr_shard_runs_copy packs / unpacks the runs): their sizes depend on C
      alone, so the step has no variable-split collective and, for a given C, is one fixed
-     launch sequence (captured as a HIP graph at N = 1; at N > 1 with RCCL when
-     CTR_SHARDED_GRAPHS=1);
+     launch sequence (captured as a HIP graph, RCCL collectives included; gloo: eager);
   4. owners bring the requested rows up to date (plan-free deferred catch-up: duplicates
      across requesters resolved by the owner scratch), gather E[row] and w[row] and send
      them back: every rank then holds its batch's rows compacted in unique order;
@@ -43,6 +42,7 @@ both give bitwise the same results.
 from __future__ import annotations
 
 import os
+import warnings
 import weakref
 from time import perf_counter
 
@@ -187,11 +187,14 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self.host_sections: dict | None = None
         self._xbufs: dict = {}
         self._cap = 0  # the exchange capacity in use (rows per (requester, owner) pair)
-        # graph replay of the fixed-capacity step: at one process always (no collective), at
-        # N > 1 only where the collectives can be captured (RCCL) and it is asked for
+        # graph replay of the fixed-capacity step: at one process always, at N > 1 where the
+        # collectives can be captured — RCCL (nccl backend; round 5: the one-rank RCCL step
+        # captured with its all_to_all_single / all_reduce kernels is bitwise the eager and
+        # the local-copy step on the MI355X, test_rccl_world1_collectives_bitwise) — unless
+        # CTR_SHARDED_GRAPHS=0; gloo stages through the host and cannot be captured
         backend = dist.get_backend(self.group) if self.world_size > 1 else None
         self._graph_ok = self.world_size == 1 or (
-            backend == "nccl" and os.environ.get("CTR_SHARDED_GRAPHS", "0") == "1")
+            backend == "nccl" and os.environ.get("CTR_SHARDED_GRAPHS", "1") != "0")
         # varsplit: lookahead plans per ids tensor (LRU): ids key -> plan buffers / event
         self._plans: dict = {}
         self._pending: dict = {}
@@ -544,8 +547,17 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._after_step()
             if len(self._graphs) < self.max_graphs:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
-                    self._launch_sharded(slot, mean_div, C)  # captured, not executed
+                try:
+                    with graph_capture(g, pool=live_pool(self), stream=self._capture_stream):
+                        self._launch_sharded(slot, mean_div, C)  # captured, not executed
+                except RuntimeError as e:  # a backend that refuses capture: eager from here
+                    if self.world_size == 1 and not self._coll:
+                        raise
+                    warnings.warn(f"ShardedCTRTrainer: step graph capture failed ({e}); "
+                                  "launching the steps eagerly")
+                    torch.cuda.synchronize(self.device)
+                    self._graph_ok = False
+                    return loss
                 self._graphs[key] = (g, self._bufs)
                 self.captures += 1
             return loss
