@@ -569,12 +569,15 @@ def main():
     dominant = max(("adam", "catchup", "gather", "plan", "scatter", "gemm", "flush"),
                    key=lambda k: per_step[k])
 
-    # re-warm (untimed): the breakdown's eager steps and its flush left the trainer with no
-    # pipelined weight-gradient tail pending; a few graph-replayed steps restore the steady
-    # state the timed region runs in (every graph it replays captured before it starts)
+    # re-warm (untimed), only with the pipelined weight-gradient tail (CTR_PIPELINE_WGRAD=1):
+    # the breakdown's flush left no tail pending; a few graph-replayed steps restore the
+    # steady state the timed region runs in (every graph it replays captured before it
+    # starts), and a flush after them keeps the region's own flush at K replayed steps
     trainer.timing = None
-    for i in range(3):
-        step(i)
+    if getattr(trainer, "_pipe", False):
+        for i in range(3):
+            step(i)
+        trainer._flush_table()  # the tables only: the tail stays pending
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
