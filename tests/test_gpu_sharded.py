@@ -442,7 +442,8 @@ def test_capacity_agreement_mismatch(cuda):
     assert torch.equal(out["fused"][1], out["sharded"][1])
 
 
-def _rccl_world1_main(q, port, kind, V, F, K, B, steps):
+def _rccl_world1_main(q, port, kind, V, F, K, B, steps, name, force, graphs):
+    import sys
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
@@ -453,27 +454,24 @@ def _rccl_world1_main(q, port, kind, V, F, K, B, steps):
         from rl_ctr_prediction_amd.synthetic import CriteoSynth
         data = [tuple(torch.tensor(a, device=dev) for a in xy)
                 for xy in CriteoSynth(V, F, seed=31).batches(steps, B)]
-        res = {}
-        for name, force, graphs in (("local", False, True), ("rccl_eager", True, False),
-                                    ("rccl_graphs", True, True)):
-            m = _model(kind, V, F, K, drop=0.2, device=dev)
-            tr = P.ShardedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3,
-                                     force_collectives=force)
-            tr.use_graphs = graphs
-            losses = [tr.step(*data[i], next_x=[d[0] for d in data[i + 1:i + 3]]).item()
-                      for i in range(steps)]
-            tr.check_errors()
-            E, w = tr.gather_tables()
-            res[name] = dict(losses=losses, E=E.cpu().numpy(),
-                             w=None if w is None else w.cpu().numpy(),
-                             dense={k: v.detach().cpu().numpy() for k, v in tr.views.items()},
-                             m=tr.m_E[:tr.V_tab].cpu().numpy(), v=tr.v_E[:tr.V_tab].cpu().numpy(),
-                             captures=tr.captures, blocking=tr.cap_blocking,
-                             backend=dist.get_backend(tr.group))
-            # the captured graphs (RCCL kernels inside) go before the communicators do
-            torch.cuda.synchronize()
-            del tr, m, E, w
-            gc.collect()
+        m = _model(kind, V, F, K, drop=0.2, device=dev)
+        tr = P.ShardedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=3, force_collectives=force)
+        tr.use_graphs = graphs
+        losses = []
+        for i in range(steps):
+            losses.append(tr.step(*data[i], next_x=[d[0] for d in data[i + 1:i + 3]]).item())
+            print(f"[rccl {name}] step {i} done", file=sys.stderr, flush=True)
+        tr.check_errors()
+        E, w = tr.gather_tables()
+        res = dict(losses=losses, E=E.cpu().numpy(), w=None if w is None else w.cpu().numpy(),
+                   dense={k: v.detach().cpu().numpy() for k, v in tr.views.items()},
+                   m=tr.m_E[:tr.V_tab].cpu().numpy(), v=tr.v_E[:tr.V_tab].cpu().numpy(),
+                   captures=tr.captures, blocking=tr.cap_blocking,
+                   backend=dist.get_backend(tr.group))
+        # the captured graphs (RCCL kernels inside) go before the communicators do
+        torch.cuda.synchronize()
+        del tr, m, E, w
+        gc.collect()
         q.put(res)
     finally:
         torch.cuda.synchronize()
@@ -486,20 +484,25 @@ def test_rccl_world1_collectives_bitwise(cuda, kind, K):
     collectives of a one-rank nccl (RCCL) process group — equal-split all_to_all_single for
     ids / rows / gradients, all_reduce for the dense gradient, the loss and the capacity
     agreements — eager and captured into the step's HIP graphs, is bitwise the local-copy
-    step over 5 steps with two batches of lookahead (dropout on)."""
+    step over 5 steps with two batches of lookahead (dropout on). Each variant in a process
+    of its own (one communicator set per process), bounded well inside the suite's limits."""
     V, F, B, steps = 40_000, 26, 512, 5
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_rccl_world1_main, args=(q, _free_port(), kind, V, F, K, B, steps))
-    p.start()
-    try:
-        res = q.get(timeout=300)
-        p.join(timeout=60)
-    finally:
-        if p.is_alive():  # never leave a rank behind on the device
-            p.kill()
+    res = {}
+    for name, force, graphs in (("local", False, True), ("rccl_eager", True, False),
+                                ("rccl_graphs", True, True)):
+        q = ctx.Queue()
+        p = ctx.Process(target=_rccl_world1_main,
+                        args=(q, _free_port(), kind, V, F, K, B, steps, name, force, graphs))
+        p.start()
+        try:
+            res[name] = q.get(timeout=90)
             p.join(timeout=30)
-    assert p.exitcode == 0
+        finally:
+            if p.is_alive():  # never leave a rank behind on the device
+                p.kill()
+                p.join(timeout=30)
+        assert p.exitcode == 0, (name, p.exitcode)
     a = res["local"]
     assert res["rccl_graphs"]["captures"] >= 1 and res["rccl_eager"]["captures"] == 0
     assert res["rccl_graphs"]["backend"] == "nccl"
