@@ -294,7 +294,7 @@ class FusedCTRTrainer:
         # queues (GPU_MAX_HW_QUEUES = 4), and streams beyond that share queues in order
         self._plan_stream = None
         if self._side is not None:
-            self._plan_stream = self._new_stream()
+            self._plan_stream = self._new_plan_stream()
         # lookahead plans may alternate over n_plan_streams streams (each key keeps its own:
         # its captured graph holds that stream's scratch), two plans in flight at once.
         # Default 2: with the host off the step's critical path (step(): 30 us of Python),
@@ -648,10 +648,29 @@ class FusedCTRTrainer:
                 return st
         raise RuntimeError("FusedCTRTrainer: no free stream in torch's stream pool")
 
+    def _new_plan_stream(self):
+        """A plan stream: a torch stream of its own (_new_stream), or with
+        CTR_PLAN_STREAM_PRIORITY=low a HIP stream created at the runtime's LOW priority
+        (hipStreamCreateWithPriority, priority 1: its own hardware queue in the low-priority
+        pool, dispatched after the normal-priority step when both have work), wrapped as a
+        torch ExternalStream that this trainer keeps alive."""
+        if os.environ.get("CTR_PLAN_STREAM_PRIORITY", "") != "low":
+            return self._new_stream()
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            rc = hip.hipStreamCreateWithPriority(ctypes.byref(handle), 1, 1)  # NonBlocking, low
+        if rc != 0:
+            raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
+        st = torch.cuda.ExternalStream(handle.value, device=self.device)
+        self._own_streams.append(st)
+        return st
+
     def _slot_stream(self, stream_i: int):
         """Plan stream number stream_i (created on first use)."""
         while stream_i > len(self._extra_plan_streams):
-            self._extra_plan_streams.append(self._new_stream())
+            self._extra_plan_streams.append(self._new_plan_stream())
         return self._plan_stream if stream_i == 0 else self._extra_plan_streams[stream_i - 1]
 
     def _acquire_slot(self, shape, exclude=None, ahead: bool = False) -> InputSlot:
