@@ -679,6 +679,22 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
   // removed) was faster standalone (59.1 vs 65.2 us, profiles/r03_gemm_direct_a.txt) but not
   // in the step, where it read the X planes 4 times instead of 2
   if (!a_rc && !b_rc && M >= 2048 && N > 256 && N <= 320) return mk(CTR_PL_FWD0_TILE, 1);
+  // round 5 (tools/gemm_planes_bench.py --pg --sweep, gpurun_out/r05_pg_sweep.jsonl; the C4
+  // policy MLP at an episode of 4096): longer-k products on the 64-deep-stage tilings —
+  // N <= 256 with K >= 512 (4096 x 256 x 512: tile 21 11.9 us vs 17.3 on 17), 320 < N <= 768
+  // with K >= 1024 (4096 x 512 x 1024: tile 22 30.7 vs 35.0 on 16) — and a k-strided B with
+  // K >= 512 on 128 x 128 tiles (4096 x 1024 x 512: tile 10 31.2 vs 33.6 on 7). The C3 shapes
+  // (K 300 / 320) keep their in-step-measured tilings. CTR_PL_RULES_R05=0: the round-4 rules.
+  static const bool r05 = [] {
+    const char* e = getenv("CTR_PL_RULES_R05");
+    return !(e && e[0] == '0');
+  }();
+  if (r05 && !a_rc && !b_rc && M >= 2048 && N <= 256 && Kp >= 512 && Kp % 64 == 0)
+    return mk(21, 1);
+  if (r05 && !a_rc && !b_rc && M >= 2048 && N > 320 && N <= 768 && Kp >= 1024 && Kp % 64 == 0)
+    return mk(22, 1);
+  if (r05 && !a_rc && b_rc && M >= 2048 && N >= 1024 && N <= 1024 + 64 && Kp >= 512)
+    return mk(10, 1);
   if (!a_rc && !b_rc && M >= 2048 && N <= 256) return mk(17, 1);
   if (!a_rc && b_rc && M >= 2048 && N >= 1024) {
     PlCfg c = mk(CTR_PL_DX_TILE, 1);
@@ -706,7 +722,9 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     // target block count of the weight-gradient GEMMs: ~1170 (4.5 per CU) with the
     // split-major XCD map — measured dW0 (130 tiles) 9 splits 66 us vs 4 splits 73, dW1
     // (20 tiles) 24-32 splits 22.5-23 us vs 16 24
-    constexpr int64_t wg_blocks = 1170;
+    // round 5: at K <= 4096 (the C4 policy weight gradients) ~600 blocks, 2-3 per CU — dW1
+    // (128 tiles) 4 splits 35.5 us vs 10 41.6, dW0 (192 tiles) 4 splits 47.1 vs 7 53.9
+    const int64_t wg_blocks = (r05 && Kp <= 4096) ? 600 : 1170;
     const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
     const int s = (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(
                       ceil_div(wg_blocks, tiles), Kp / 256), 64));
