@@ -279,6 +279,12 @@ int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t stream);
  * ctr_shard_runs_copy: rows of `width` floats between the compact order (run j at offsets[j])
  *   and the padded layout (run j at j*capacity): pack = 1 writes every padded row (zeros past
  *   a run), pack = 0 writes the runs back to their compact places. */
+/* ctr_batch_stage_copy: one launch copying a batch into its fixed input slot — n0 bytes src0 ->
+ * dst0 (the ids) and n1 bytes src1 -> dst1 (the labels; n1 = 0: none); device pointers, bitwise
+ * copies. The staging of the reference's per-iteration batch (all_main/pretrain_main.py:71-74,
+ * `for x, y in loader: x.to(device)`) ahead of the step that trains on it. */
+int ctr_batch_stage_copy(void* dst0, const void* src0, int64_t n0, void* dst1, const void* src1,
+                         int64_t n1, ctr_stream_t stream);
 int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V, int n_shards,
                        int64_t capacity, int32_t* send, int32_t* counts, int32_t* offsets,
                        int32_t* err_flag, ctr_stream_t stream);

@@ -14,6 +14,30 @@
 
 namespace ctr {
 
+// ctr_batch_stage_copy: a batch's ids and labels into its input slot in ONE launch (the
+// runtime's D2D copies are one copy kernel each, ~2.5-5 us apiece on the plan stream at
+// C2 / C3). Both segments walk one grid-stride index space of 16-B units (or bytes where a
+// segment is not 16-B aligned and sized): pure copies, bit-exact.
+__global__ __launch_bounds__(256) void batch_stage_copy_kernel(char* __restrict__ d0,
+                                                               const char* __restrict__ s0,
+                                                               int64_t u0, bool v0,
+                                                               char* __restrict__ d1,
+                                                               const char* __restrict__ s1,
+                                                               int64_t u1, bool v1) {
+  const int64_t total = u0 + u1;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const bool first = t < u0;
+    const int64_t i = first ? t : t - u0;
+    char* d = first ? d0 : d1;
+    const char* s = first ? s0 : s1;
+    if (first ? v0 : v1)
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+    else
+      d[i] = s[i];
+  }
+}
+
 constexpr int kTT = 64;
 
 __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ src,
@@ -108,5 +132,23 @@ extern "C" int ctr_transpose_f32(const float* src, int64_t rows, int64_t cols, i
     hipLaunchKernelGGL(transpose_f32_kernel, grid, 256, 0, as_stream(stream), src, rows, cols,
                        ld_src, dst, ld_dst, row_tiles);
   CTR_LAUNCH_CHECK("ctr_transpose_f32");
+  return CTR_OK;
+}
+
+extern "C" int ctr_batch_stage_copy(void* dst0, const void* src0, int64_t n0, void* dst1,
+                                    const void* src1, int64_t n1, ctr_stream_t stream) {
+  CTR_REQUIRE(n0 >= 0 && n1 >= 0 && (n0 == 0 || (dst0 && src0)) && (n1 == 0 || (dst1 && src1)),
+              "ctr_batch_stage_copy: bad arguments");
+  if (n0 + n1 == 0) return CTR_OK;
+  auto vec = [](const void* d, const void* s, int64_t n) {
+    return n % 16 == 0 && ((uintptr_t)d | (uintptr_t)s) % 16 == 0;
+  };
+  const bool v0 = vec(dst0, src0, n0), v1 = vec(dst1, src1, n1);
+  const int64_t u0 = v0 ? n0 / 16 : n0, u1 = v1 ? n1 / 16 : n1;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(u0 + u1, 256), 4096));
+  hipLaunchKernelGGL(batch_stage_copy_kernel, grid, 256, 0, as_stream(stream),
+                     static_cast<char*>(dst0), static_cast<const char*>(src0), u0, v0,
+                     static_cast<char*>(dst1), static_cast<const char*>(src1), u1, v1);
+  CTR_LAUNCH_CHECK("batch_stage_copy_kernel");
   return CTR_OK;
 }

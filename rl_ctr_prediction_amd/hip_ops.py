@@ -551,6 +551,28 @@ def shard_pack_ids(plan: SparsePlanBuffers, shard_rows: int, V: int, n_shards: i
                            _p(send), _p(counts), _p(offsets), _p(err_flag), _stream())
 
 
+_STAGE_COPY = os.environ.get("CTR_STAGE_COPY", "1") != "0"  # A/B: the runtime's copies
+
+
+def batch_stage_copy(ids_dst: torch.Tensor, ids_src: torch.Tensor,
+                     y_dst: torch.Tensor | None = None, y_src: torch.Tensor | None = None) -> bool:
+    """Copy a batch's ids (and labels) into its input slot in one launch
+    (ctr_batch_stage_copy). Only for same-dtype, same-size, contiguous device tensors: returns
+    False (nothing launched) otherwise, and the caller copies with torch."""
+    if not _STAGE_COPY:
+        return False
+    pairs = [(ids_dst, ids_src)] + ([(y_dst, y_src)] if y_dst is not None else [])
+    for d, s_ in pairs:
+        if not (d.is_cuda and s_.is_cuda and d.dtype == s_.dtype and d.numel() == s_.numel()
+                and d.is_contiguous() and s_.is_contiguous() and d.device == s_.device):
+            return False
+    n0 = ids_dst.numel() * ids_dst.element_size()
+    n1 = y_dst.numel() * y_dst.element_size() if y_dst is not None else 0
+    lib.ctr_batch_stage_copy(_p(ids_dst), _p(ids_src), n0, _p(y_dst) if n1 else None,
+                             _p(y_src) if n1 else None, n1, _stream())
+    return True
+
+
 def shard_runs_copy(src: torch.Tensor, dst: torch.Tensor, capacity: int, counts: torch.Tensor,
                     offsets: torch.Tensor, pack: bool) -> torch.Tensor:
     """Rows between the compact order and the padded exchange layout (ctr_shard_runs_copy):

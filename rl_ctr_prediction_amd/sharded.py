@@ -489,7 +489,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             ps.wait_event(self._agree_last_ev)
         torch.cuda.set_stream(ps)
         try:
-            s.ids.copy_(ids, non_blocking=True)
+            if not hip_ops.batch_stage_copy(s.ids, ids):
+                s.ids.copy_(ids, non_blocking=True)
             if ids.is_cuda:
                 ids.record_stream(ps)
             self._plan_slot(s)

@@ -701,12 +701,16 @@ class FusedCTRTrainer:
         # context manager (~9 us per use: it looks the current stream up again)
         torch.cuda.set_stream(ps)
         try:
-            s.ids.copy_(nx, non_blocking=True)
+            # the ids and (ny) the labels in one launch where both are plain device copies
+            yflat = ny.reshape(-1) if ny is not None else None
+            if not hip_ops.batch_stage_copy(s.ids, nx, s.y if ny is not None else None, yflat):
+                s.ids.copy_(nx, non_blocking=True)
+                if ny is not None:
+                    s.y.copy_(yflat, non_blocking=True)
             if nx.is_cuda:
                 nx.record_stream(ps)
             s.y_key = None
             if ny is not None:  # the labels too: the step on this batch skips its copy
-                s.y.copy_(ny.reshape(-1), non_blocking=True)
                 if ny.is_cuda:
                     ny.record_stream(ps)
                 s.y_key = self._xkey(ny)

@@ -650,3 +650,27 @@ def test_fm_step_tail_bitwise_separate_launches(cuda):
             out[mode] = [t.cpu() for t in (loss, g, p, m, v, ctr)]
         for a, b in zip(out["tail"], out["separate"]):
             assert torch.equal(a, b), (B, n, a, b)
+
+
+@pytest.mark.parametrize("B,F,dt", [(4096, 26, torch.int64), (513, 26, torch.int32),
+                                    (7, 3, torch.int32), (1, 1, torch.int64)])
+def test_batch_stage_copy_bitwise(cuda, B, F, dt):
+    """ctr_batch_stage_copy: ids and labels into a slot in one launch, bitwise (16-B units
+    where aligned, bytes otherwise: odd sizes and offset views); labels optional; anything
+    but same-dtype contiguous device tensors is refused (the caller copies with torch)."""
+    from rl_ctr_prediction_amd import hip_ops
+    g = torch.Generator(device=cuda).manual_seed(B)
+    src = torch.randint(0, 2**31 - 1, (B + 1, F), device=cuda, generator=g).to(dt)[1:]  # offset
+    ys = torch.rand(B + 3, device=cuda, generator=g)[3:]
+    ids, y = torch.full((B, F), -1, dtype=dt, device=cuda), torch.full((B,), -1.0, device=cuda)
+    assert hip_ops.batch_stage_copy(ids, src, y, ys)
+    torch.cuda.synchronize()
+    assert torch.equal(ids, src) and torch.equal(y, ys)
+    ids2 = torch.zeros_like(ids)
+    assert hip_ops.batch_stage_copy(ids2, src)  # ids only
+    torch.cuda.synchronize()
+    assert torch.equal(ids2, src)
+    if B > 1 and F > 1:
+        assert not hip_ops.batch_stage_copy(ids2, src.t().contiguous().t())  # not contiguous
+    assert not hip_ops.batch_stage_copy(ids2, src.to(torch.float32))     # other dtype
+    assert not hip_ops.batch_stage_copy(ids2, src.cpu())                 # host tensor
