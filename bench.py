@@ -723,17 +723,19 @@ def main():
         roofline = {"kernel": kname, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": nbytes}
-        if dominant == "plan":  # the column plan's three launches
-            parts = [("colplan_sort_kernel", 1), ("colplan_merge_kernel", 1),
-                     ("seg_write_kernel", 1)]
-            got = [(load_traffic(args.config, k), n) for k, n in parts]
-            traffic = (sum(t * n for (t, _), n in got) if all(t for (t, _), _ in got)
-                       else None)
-            src = got[0][0][1] if traffic else None
-        else:
-            traffic, src = load_traffic(args.config, {"adam": "adam_embedding_vec",
-                                                      "flush": "deferred_flush_tile"}.get(dominant,
-                                                                                          dominant))
+        # the kernels of the dominant group, one launch of each (their PMC traffic summed)
+        parts = {"plan": ["colplan_sort_kernel", "colplan_merge_kernel", "seg_write_kernel"],
+                 "scatter": ["seg_chunk_kernel", "seg_combine_apply_kernel" if fused_apply
+                             else "seg_combine_kernel"],
+                 "catchup": ["deferred_rows_vec"],
+                 "gather": ["ipnn_forward_kernel" if cfg["kind"] == "IPNN" else "fm_forward_vec"],
+                 "adam": ["adam_embedding_vec"],
+                 "flush": ["deferred_flush_tile"]}[dominant]
+        got = [load_traffic(args.config, k) for k in parts]
+        traffic = sum(t for t, _ in got) if all(t for t, _ in got) else None
+        src = got[0][1] if traffic else None
+        if traffic is not None and len(parts) > 1:
+            roofline["traffic_kernels"] = parts
     roofline.update({"traffic": traffic, "traffic_source": src, "avg_launch_ms": launch_ms,
                      "launches_timed": len(spans),
                      "timing": "HIP events on the launch stream around each launch of this "

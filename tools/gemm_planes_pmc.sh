@@ -3,7 +3,7 @@
 # rocprofv3 --pmc pass per counter set, then a per-shape summary.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/gemm_pmc
+OUT=${OUT:-gpurun_out/gemm_pmc}
 rm -rf $OUT; mkdir -p $OUT
 i=0
 for P in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VALU" \
