@@ -627,8 +627,13 @@ static bool pl_ks_ok(const PlDef& d, int64_t Kp, int64_t kps) {
 #ifndef CTR_PL_DX_TILE
 #define CTR_PL_DX_TILE 7  // (A/B builds: 19, the 8-wave 64 x 64 tiling)
 #endif
+// dX's XCD walk: whole M rows per XCD, N-tile-major inside the XCD (3, round 5): HBM traffic
+// 160 -> 100 MB per launch at C3 (profiles/r05_gemm_mfma_busy.json vs
+// r05_gemm_counters_dx_xg3.json), in-step C3 13.26 / 13.39 / 13.22 / 13.20 / 13.22 vs M-row-
+// major (1) 13.21 / 13.21 / 13.26 / 13.24 / 13.42 M ex/s, alternating: the same time for 60 MB
+// less traffic beside the scatter chain
 #ifndef CTR_PL_DX_XG
-#define CTR_PL_DX_XG 1
+#define CTR_PL_DX_XG 3
 #endif
 #ifndef CTR_PL_FWD0_TILE
 #define CTR_PL_FWD0_TILE 8
@@ -700,7 +705,8 @@ static PlCfg pl_choose(bool a_rc, bool b_rc, int64_t M, int64_t N, int64_t Kp) {
     PlCfg c = mk(CTR_PL_DX_TILE, 1);
     // XCD tile groups (planes_tile_index): with the 4-wave tiling, whole M rows per XCD (1)
     // measured C3 13.05 / 13.02 / 13.04 vs 12.93 / 12.70 / 12.93 M ex/s with halves of the
-    // N tiles per XCD (2), 4 no better (alternating, per-shape override)
+    // N tiles per XCD (2), 4 no better (alternating, per-shape override); walked N-major
+    // inside the XCD (3) the same time with 60 MB less HBM traffic (round 5, above)
     c.xg = CTR_PL_DX_XG;
     return c;
   }
