@@ -264,6 +264,16 @@ int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique
                             ctr_stream_t stream);
 int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows, int n_shards,
                           int64_t* counts, ctr_stream_t stream);
+/* ctr_sparse_plan_build_runs: the plan (bit-identical to ctr_sparse_plan_build's) of the ids an
+ * owner shard receives in a row-sharded step: n_runs <= 8 runs of run_len int32 ids
+ * (ids[j*run_len + i]), each run ascending with every row at most once, padded at its end with
+ * the spare row n_rows - 1 (repeated); rows in [0, n_rows). mask: uint32[ceil(n_rows/4)], zero
+ * on entry and left zero (a per-row bitmask of the requesting runs); ws: caller scratch of
+ * ctr_sparse_plan_runs_workspace_bytes bytes. plan->S must be n_runs * run_len. */
+int64_t ctr_sparse_plan_runs_workspace_bytes(int n_runs, int64_t run_len, int64_t n_rows);
+int ctr_sparse_plan_build_runs(const int32_t* ids, int n_runs, int64_t run_len, int64_t n_rows,
+                               const ctr_sparse_plan* plan, uint32_t* mask, void* ws,
+                               int64_t ws_bytes, ctr_stream_t stream);
 /* ids[i] += delta (global row ids <-> shard-local row ids). */
 int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t stream);
 /* Fixed-capacity exchange of a row-sharded step (no reference counterpart: the reference

@@ -167,6 +167,8 @@ SIGNATURES = {
     "ctr_shard_pack_ids": (_i32, [_plan_p, _i64, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp]),
     "ctr_shard_runs_copy": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _vp]),
     "ctr_batch_stage_copy": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp]),
+    "ctr_sparse_plan_runs_workspace_bytes": (_i64, [_i32, _i64, _i64]),
+    "ctr_sparse_plan_build_runs": (_i32, [_vp, _i32, _i64, _i64, _plan_p, _vp, _vp, _i64, _vp]),
     "ctr_segment_workspace_bytes": (_i64, [_i64, _i32]),
     "ctr_fm_embedding_grad": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _i64, _vp]),

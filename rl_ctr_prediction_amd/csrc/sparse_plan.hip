@@ -1021,6 +1021,168 @@ extern "C" int ctr_sparse_plan_build_cols(const void* idx, int idx_type, int64_t
   }
 }
 
+// ------------------------------------------- owner plan over sorted runs (row sharding) -----
+// The owner of a row shard receives, per step, one run of C ids from each of the N <= 8
+// requesters (send[j*C + i]): run j holds requester j's rows of this shard in ascending order,
+// each once, then padding up to C with the shard's spare row (its largest id). The plan of
+// that vector — the stable (row, position) grouping ctr_sparse_plan_build computes by a full
+// LSD sort — follows from a per-row bitmask of the requesting runs: a row's entries come from
+// distinct runs, in run order, so its position in the sorted vector is (entries of smaller
+// rows) + (its runs below this one), and its segment is (distinct smaller rows); the padding
+// forms the last segment in position order. 5 launches over N*C entries and the shard's
+// n_rows/4 mask words (mark, two scan launches, scatter, clear) instead of 8 over 3 radix
+// passes; bit-identical to the LSD plan (tests/test_gpu_kernels.py).
+constexpr int kRunWordsPerBlock = 1024;  // 256 threads x 4 mask words
+
+__global__ __launch_bounds__(256) void runs_mark_kernel(const int32_t* __restrict__ ids,
+                                                        int64_t C, int64_t S, int32_t spare,
+                                                        uint32_t* __restrict__ mask,
+                                                        int32_t* __restrict__ run_len) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < S;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / C);
+    const int64_t i = e - (int64_t)j * C;
+    const int32_t r = ids[e];
+    if (r != spare) {
+      atomicOr(&mask[r >> 2], 1u << (((r & 3) << 3) + j));
+      if (i == C - 1 || ids[e + 1] == spare) run_len[j] = (int32_t)(i + 1);
+    } else if (i == 0) {
+      run_len[j] = 0;
+    }
+  }
+}
+
+__device__ __forceinline__ int32_t nz_bytes(uint32_t w) {
+  return ((w & 0xffu) != 0) + ((w & 0xff00u) != 0) + ((w & 0xff0000u) != 0) + ((w >> 24) != 0);
+}
+
+// per mask word: (entries, distinct rows) exclusive within its block; per block the totals
+__global__ __launch_bounds__(256) void runs_scan_words_kernel(const uint32_t* __restrict__ mask,
+                                                              int64_t n_words,
+                                                              int2* __restrict__ word_pre,
+                                                              int2* __restrict__ block_tot) {
+  __shared__ int2 s_w[4];
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const int64_t w0 = (int64_t)blockIdx.x * kRunWordsPerBlock + (int64_t)t * 4;
+  uint32_t m[4];
+  int2 tot = make_int2(0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    m[q] = w0 + q < n_words ? mask[w0 + q] : 0u;
+    tot.x += __popc(m[q]);
+    tot.y += nz_bytes(m[q]);
+  }
+  int2 x = tot;  // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int yx = __shfl_up(x.x, o, kWave), yy = __shfl_up(x.y, o, kWave);
+    if (lane >= o) { x.x += yx; x.y += yy; }
+  }
+  if (lane == kWave - 1) s_w[w] = x;
+  __syncthreads();
+  int2 off = make_int2(0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < w) { off.x += s_w[j].x; off.y += s_w[j].y; }
+  int2 run = make_int2(off.x + x.x - tot.x, off.y + x.y - tot.y);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (w0 + q < n_words) word_pre[w0 + q] = run;
+    run.x += __popc(m[q]);
+    run.y += nz_bytes(m[q]);
+  }
+  if (t == 255) block_tot[blockIdx.x] = make_int2(off.x + x.x, off.y + x.y);
+}
+
+// one block: exclusive scan of the block totals in place; hdr = {entries, distinct rows}
+__global__ __launch_bounds__(1024) void runs_scan_blocks_kernel(int2* __restrict__ block_tot,
+                                                                int64_t n_blocks,
+                                                                int32_t* __restrict__ hdr) {
+  __shared__ int2 s_w[16];
+  __shared__ int2 s_carry;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  if (t == 0) s_carry = make_int2(0, 0);
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < n_blocks; b0 += 1024) {
+    const int64_t b = b0 + t;
+    const int2 v = b < n_blocks ? block_tot[b] : make_int2(0, 0);
+    int2 x = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int yx = __shfl_up(x.x, o, kWave), yy = __shfl_up(x.y, o, kWave);
+      if (lane >= o) { x.x += yx; x.y += yy; }
+    }
+    if (lane == kWave - 1) s_w[w] = x;
+    __syncthreads();
+    int2 off = s_carry;
+    for (int j = 0; j < w; ++j) { off.x += s_w[j].x; off.y += s_w[j].y; }
+    if (b < n_blocks) block_tot[b] = make_int2(off.x + x.x - v.x, off.y + x.y - v.y);
+    __syncthreads();
+    if (t == 1023) s_carry = make_int2(off.x + x.x, off.y + x.y);
+    __syncthreads();
+  }
+  if (t == 0) { hdr[0] = s_carry.x; hdr[1] = s_carry.y; }
+}
+
+__global__ __launch_bounds__(256) void runs_scatter_kernel(
+    const int32_t* __restrict__ ids, int64_t C, int64_t S, int32_t spare,
+    const uint32_t* __restrict__ mask, const int2* __restrict__ word_pre,
+    const int2* __restrict__ block_pre, const int32_t* __restrict__ hdr,
+    const int32_t* __restrict__ run_len, ctr_sparse_plan plan) {
+  const int32_t T = hdr[0], UR = hdr[1];
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < S;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(e / C);
+    const int64_t i = e - (int64_t)j * C;
+    const int32_t r = ids[e];
+    if (r != spare) {
+      const int64_t wi = r >> 2;
+      const uint32_t m = mask[wi];
+      const int sh = (r & 3) << 3;
+      const uint32_t below = sh ? (m & ((1u << sh) - 1u)) : 0u;  // the word's smaller rows
+      const uint32_t mine = (m >> sh) & 0xffu;
+      const int2 wp = word_pre[wi], bp = block_pre[wi / kRunWordsPerBlock];
+      const int32_t base = bp.x + wp.x + __popc(below);
+      const int32_t seg = bp.y + wp.y + nz_bytes(below);
+      const uint32_t before = mine & ((1u << j) - 1u);  // runs below this one holding r
+      const int32_t pos = base + __popc(before);
+      plan.sorted_rows[pos] = r;
+      plan.sorted_slots[pos] = (int32_t)e;
+      plan.pos_seg[pos] = seg;
+      if (before == 0) {
+        plan.unique_rows[seg] = r;
+        plan.seg_offsets[seg] = base;
+      }
+    } else {
+      int32_t pad_before = 0;  // padding entries of the runs below
+      for (int q = 0; q < j; ++q) pad_before += (int32_t)C - run_len[q];
+      const int32_t pos = T + pad_before + (int32_t)(i - run_len[j]);
+      plan.sorted_rows[pos] = spare;
+      plan.sorted_slots[pos] = (int32_t)e;
+      plan.pos_seg[pos] = UR;
+      if (pos == T) {
+        plan.unique_rows[UR] = spare;
+        plan.seg_offsets[UR] = T;
+      }
+    }
+    if (e == 0) {
+      const int32_t U = UR + (T < (int32_t)S ? 1 : 0);
+      *plan.num_unique = U;
+      plan.seg_offsets[U] = (int32_t)S;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void runs_clear_kernel(const int32_t* __restrict__ ids,
+                                                         int64_t S, int32_t spare,
+                                                         uint32_t* __restrict__ mask) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < S;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t r = ids[e];
+    if (r != spare) mask[r >> 2] = 0u;  // every writer of a word stores 0
+  }
+}
+
 extern "C" int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique,
                                        ctr_stream_t stream) {
   CTR_REQUIRE(plan_ok(plan) && slot_to_unique, "ctr_plan_slot_to_unique: bad arguments");
@@ -1085,5 +1247,63 @@ extern "C" int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, 
     else hipLaunchKernelGGL((shard_runs_copy_kernel<float, false>), grid, 256, 0, st, src, dst, W, capacity, counts, offsets);
   }
   CTR_LAUNCH_CHECK("shard_runs_copy_kernel");
+  return CTR_OK;
+}
+
+static int64_t runs_ws_layout(int64_t n_rows, int64_t n_runs, int64_t* off_word, int64_t* off_block,
+                              int64_t* off_hdr) {
+  const int64_t n_words = ceil_div(std::max<int64_t>(n_rows, 1), 4);
+  const int64_t n_blocks = ceil_div(n_words, kRunWordsPerBlock);
+  *off_word = 0;
+  *off_block = align_up(n_words * 8, 256);
+  *off_hdr = *off_block + align_up(n_blocks * 8, 256);
+  return *off_hdr + align_up((2 + n_runs) * 4, 256);
+}
+
+extern "C" int64_t ctr_sparse_plan_runs_workspace_bytes(int n_runs, int64_t run_len,
+                                                        int64_t n_rows) {
+  if (n_runs < 1 || n_runs > 8 || run_len < 1 || n_rows < 1) {
+    set_error("ctr_sparse_plan_runs_workspace_bytes: need 1 <= n_runs <= 8, run_len >= 1, "
+              "n_rows >= 1");
+    return -1;
+  }
+  int64_t a, b, c;
+  return runs_ws_layout(n_rows, n_runs, &a, &b, &c);
+}
+
+extern "C" int ctr_sparse_plan_build_runs(const int32_t* ids, int n_runs, int64_t run_len,
+                                          int64_t n_rows, const ctr_sparse_plan* plan,
+                                          uint32_t* mask, void* ws, int64_t ws_bytes,
+                                          ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan) && ids && mask, "ctr_sparse_plan_build_runs: bad arguments");
+  CTR_REQUIRE(n_runs >= 1 && n_runs <= 8 && run_len >= 1 && n_rows >= 1 &&
+                  n_rows < (int64_t(1) << 31) && plan->S == n_runs * run_len &&
+                  plan->S < (int64_t(1) << 31),
+              "ctr_sparse_plan_build_runs: need 1 <= n_runs <= 8, S = n_runs * run_len");
+  int64_t ow, ob, oh;
+  const int64_t need = runs_ws_layout(n_rows, n_runs, &ow, &ob, &oh);
+  CTR_REQUIRE(ws && ws_bytes >= need, "ctr_sparse_plan_build_runs: workspace too small");
+  char* base = static_cast<char*>(ws);
+  int2* word_pre = reinterpret_cast<int2*>(base + ow);
+  int2* block_tot = reinterpret_cast<int2*>(base + ob);
+  int32_t* hdr = reinterpret_cast<int32_t*>(base + oh);
+  int32_t* run_len_d = hdr + 2;
+  const int64_t S = plan->S, n_words = ceil_div(n_rows, 4);
+  const int64_t n_blocks = ceil_div(n_words, kRunWordsPerBlock);
+  const int32_t spare = (int32_t)(n_rows - 1);
+  hipStream_t st = as_stream(stream);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(S, 256), 4096));
+  hipLaunchKernelGGL(runs_mark_kernel, g, 256, 0, st, ids, run_len, S, spare, mask, run_len_d);
+  CTR_LAUNCH_CHECK("runs_mark_kernel");
+  hipLaunchKernelGGL(runs_scan_words_kernel, (unsigned)n_blocks, 256, 0, st, mask, n_words,
+                     word_pre, block_tot);
+  CTR_LAUNCH_CHECK("runs_scan_words_kernel");
+  hipLaunchKernelGGL(runs_scan_blocks_kernel, 1, 1024, 0, st, block_tot, n_blocks, hdr);
+  CTR_LAUNCH_CHECK("runs_scan_blocks_kernel");
+  hipLaunchKernelGGL(runs_scatter_kernel, g, 256, 0, st, ids, run_len, S, spare, mask,
+                     word_pre, block_tot, hdr, run_len_d, *plan);
+  CTR_LAUNCH_CHECK("runs_scatter_kernel");
+  hipLaunchKernelGGL(runs_clear_kernel, g, 256, 0, st, ids, S, spare, mask);
+  CTR_LAUNCH_CHECK("runs_clear_kernel");
   return CTR_OK;
 }

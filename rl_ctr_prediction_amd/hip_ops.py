@@ -517,6 +517,33 @@ class SparsePlanBuffers:
                                       self._ws.numel(), _p(err_flag), _stream())
         return self
 
+    def build_runs(self, ids: torch.Tensor, n_runs: int, n_rows: int,
+                   mask: torch.Tensor) -> "SparsePlanBuffers":
+        """The plan of an owner shard's received ids (ctr_sparse_plan_build_runs): n_runs <= 8
+        ascending runs of equal length, each row at most once per run, padded with the spare
+        row n_rows - 1; bit-identical to build(). mask: int32[ceil(n_rows / 4)] zeros (left
+        zero)."""
+        _dev(ids, "ids")
+        S = ids.numel()
+        if ids.dtype != torch.int32 or not ids.is_contiguous() or S % n_runs:
+            raise ValueError("build_runs: ids must be contiguous int32, n_runs equal runs")
+        if S > self.capacity:
+            raise ValueError(f"sparse plan: {S} slots > capacity {self.capacity}")
+        if mask.dtype != torch.int32 or mask.numel() < (n_rows + 3) // 4:
+            raise ValueError("build_runs: mask must be int32[ceil(n_rows / 4)]")
+        self.S = S
+        need = lib.ctr_sparse_plan_runs_workspace_bytes(int(n_runs), S // n_runs, int(n_rows))
+        if need < 0:
+            raise RuntimeError(lib.load().ctr_last_error().decode())
+        if self._ws is None or self._ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("sparse plan: scratch grown inside a graph capture")
+            self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        lib.ctr_sparse_plan_build_runs(_p(ids), int(n_runs), S // n_runs, int(n_rows),
+                                       self.struct(), _p(mask), _p(self._ws), self._ws.numel(),
+                                       _stream())
+        return self
+
     def num_unique_host(self) -> int:
         return int(self.num_unique.item())
 

@@ -674,3 +674,39 @@ def test_batch_stage_copy_bitwise(cuda, B, F, dt):
         assert not hip_ops.batch_stage_copy(ids2, src.t().contiguous().t())  # not contiguous
     assert not hip_ops.batch_stage_copy(ids2, src.to(torch.float32))     # other dtype
     assert not hip_ops.batch_stage_copy(ids2, src.cpu())                 # host tensor
+
+
+@pytest.mark.parametrize("N,C,n_rows,seed", [(1, 1000, 5000, 0), (2, 777, 3000, 1),
+                                             (8, 1024, 1_250_001, 2), (8, 300, 301, 3),
+                                             (5, 64, 9, 4), (3, 1, 4, 5), (8, 4096, 40_000, 6)])
+def test_sparse_plan_runs_bit_exact(cuda, N, C, n_rows, seed):
+    """ctr_sparse_plan_build_runs (an owner shard's received ids: N ascending runs of unique
+    rows, each padded with the spare row n_rows - 1) == the LSD plan of the same vector, bit
+    for bit — including empty runs (all padding), full runs (no padding), rows every run
+    holds — and leaves its mask zero."""
+    from rl_ctr_prediction_amd import hip_ops
+    rng = np.random.default_rng(seed)
+    spare = n_rows - 1
+    hot = rng.choice(spare, size=min(spare, max(1, C // 4)), replace=False) if spare else []
+    runs = []
+    for j in range(N):
+        n = [0, C, int(rng.integers(0, C + 1))][j % 3] if N > 2 else int(rng.integers(1, C + 1))
+        n = min(n, spare)
+        # half of the run from the rows every run draws from (shared), the rest at random
+        r = np.unique(np.concatenate([np.asarray(hot[: n // 2], dtype=np.int64),
+                                      rng.choice(spare, size=n, replace=False)]))[:n]
+        runs.append(np.concatenate([r, np.full(C - len(r), spare)]).astype(np.int32))
+    ids = torch.tensor(np.concatenate(runs), device=cuda)
+    a = hip_ops.SparsePlanBuffers(N * C, cuda).build(ids, n_rows)
+    mask = torch.zeros((n_rows + 3) // 4, dtype=torch.int32, device=cuda)
+    b = hip_ops.SparsePlanBuffers(N * C, cuda).build_runs(ids, N, n_rows, mask)
+    b.build_runs(ids, N, n_rows, mask)  # twice: the mask came back zero
+    torch.cuda.synchronize()
+    U = a.num_unique_host()
+    assert b.num_unique_host() == U
+    S = N * C
+    for name in ("sorted_slots", "sorted_rows", "pos_seg"):
+        assert torch.equal(getattr(a, name)[:S], getattr(b, name)[:S]), name
+    assert torch.equal(a.unique_rows[:U], b.unique_rows[:U])
+    assert torch.equal(a.seg_offsets[:U + 1], b.seg_offsets[:U + 1])
+    assert int(mask.abs().sum()) == 0
