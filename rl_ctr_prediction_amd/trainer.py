@@ -1111,8 +1111,6 @@ class FusedCTRTrainer:
         # Linear(300,200): dH1 = (dH2 @ W1) masked by Dropout+ReLU of layer 1
         self._gemm_planes(b.dh2p, w1p, False, True, B, H1, H2, out=b.dh1, out_planes=b.dh1p,
                           epi=hip_ops.EPI_GRAD_MASK, aux=b.h1, scale=1.0 / (1.0 - p0))
-        b.ev_dh1 = torch.cuda.Event()
-        b.ev_dh1.record()
         # Linear(F*K,300): dX = dH1 @ W0, the MLP-input gradient the scatter needs
         self._gemm_planes(b.dh1p, w0p, False, True, B, W, H1, out=b.dx)
         if self.kind == "IPNN":  # per-slot embedding gradients through the pair products
