@@ -264,6 +264,11 @@ int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slot_to_unique
                             ctr_stream_t stream);
 int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows, int n_shards,
                           int64_t* counts, ctr_stream_t stream);
+/* ctr_plan_shard_counts_max: the same counts and, in max_out[0] (int64, may be NULL), their
+ * maximum — the step's largest per-owner run, which sizes the row-sharded exchange (one
+ * launch; max_out needs n_shards <= 15). */
+int ctr_plan_shard_counts_max(const ctr_sparse_plan* plan, int64_t shard_rows, int n_shards,
+                              int64_t* counts, int64_t* max_out, ctr_stream_t stream);
 /* ctr_sparse_plan_build_runs: the plan (bit-identical to ctr_sparse_plan_build's) of the ids an
  * owner shard receives in a row-sharded step: n_runs <= 8 runs of run_len int32 ids
  * (ids[j*run_len + i]), each run ascending with every row at most once, padded at its end with

@@ -738,6 +738,53 @@ __global__ void shard_counts_kernel(const int32_t* __restrict__ unique_rows,
   counts[j] = lower((int64_t)(j + 1) * shard_rows) - lower((int64_t)j * shard_rows);
 }
 
+// The same counts for up to kCountsMaxShards shards in ONE block, and their maximum (the
+// step's largest run, what the capacity agreement reads): wave w finds the run boundary
+// lower_bound(w * shard_rows) by a 64-ary search — 64 probes per round, a ballot picks the
+// sub-range — so the chain is ~3 dependent loads at U = 61k instead of a binary search's 16
+// (the thread-per-shard kernel above ran 24 us at C3, plus a separate max launch).
+constexpr int kCountsMaxShards = 15;
+
+__device__ __forceinline__ int wave_lower_bound(const int32_t* __restrict__ rows, int U, int64_t v,
+                                                int lane) {
+  int lo = 0, hi = U;  // the answer lies in [lo, hi]
+  while (hi - lo > kWave) {
+    const int step = (hi - lo + kWave - 1) / kWave;
+    const int q = lo + lane * step;
+    const bool below = q < hi && (int64_t)rows[q] < v;
+    const int c = __popcll(__ballot(below));  // probes below v (a prefix of the lanes)
+    if (c == 0) return lo;                    // rows[lo] >= v
+    const int nlo = lo + (c - 1) * step + 1;
+    hi = min(hi, lo + c * step);
+    lo = nlo;
+  }
+  const int q = lo + lane;
+  const bool below = q < hi && (int64_t)rows[q] < v;
+  return lo + __popcll(__ballot(below));
+}
+
+__global__ __launch_bounds__(1024) void shard_counts_max_kernel(
+    const int32_t* __restrict__ unique_rows, const int32_t* __restrict__ num_unique,
+    int64_t shard_rows, int n_shards, int64_t* __restrict__ counts, int64_t* __restrict__ max_out) {
+  __shared__ int bound[kCountsMaxShards + 1];
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int U = *num_unique;
+  if (w <= n_shards) {
+    const int b = w == 0 ? 0 : wave_lower_bound(unique_rows, U, (int64_t)w * shard_rows, lane);
+    if (lane == 0) bound[w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t mx = 0;
+    for (int j = 0; j < n_shards; ++j) {
+      const int64_t c = bound[j + 1] - bound[j];
+      counts[j] = c;
+      mx = c > mx ? c : mx;
+    }
+    if (max_out) max_out[0] = mx;
+  }
+}
+
 // Fixed-capacity exchange of a row-sharded step: every (requester, owner) pair moves C rows
 // (equal-split all-to-alls whose sizes depend on C alone, so a step is graph-capturable).
 // The plan's unique rows owned by shard j are the run [lo_j, hi_j) of unique_rows (ascending);
@@ -745,16 +792,6 @@ __global__ void shard_counts_kernel(const int32_t* __restrict__ unique_rows,
 // the owner's dummy row id (its row count: owners keep one spare row that padding entries
 // read and update, never a real one). counts[j] / offsets[j] (int32) describe the runs; a
 // run longer than C raises CTR_EFLAG_CAPACITY.
-__device__ __forceinline__ int plan_lower_bound(const int32_t* __restrict__ rows, int U, int64_t v) {
-  int lo = 0, hi = U;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if ((int64_t)rows[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 __global__ __launch_bounds__(256) void shard_pack_ids_kernel(
     const int32_t* __restrict__ unique_rows, const int32_t* __restrict__ num_unique,
     int64_t shard_rows, int64_t V, int64_t C, int32_t* __restrict__ send,
@@ -762,8 +799,16 @@ __global__ __launch_bounds__(256) void shard_pack_ids_kernel(
   const int j = blockIdx.y;
   const int U = *num_unique;
   const int64_t base = (int64_t)j * shard_rows;
-  const int lo = plan_lower_bound(unique_rows, U, base);
-  const int hi = plan_lower_bound(unique_rows, U, base + shard_rows);
+  // the run's bounds by two waves' 64-ary searches (~3 dependent loads each, not a binary
+  // search's 16 in every thread), shared through LDS
+  __shared__ int bounds[2];
+  const int wave = threadIdx.x / kWave;
+  if (wave < 2) {
+    const int b = wave_lower_bound(unique_rows, U, base + (wave ? shard_rows : 0), threadIdx.x % kWave);
+    if (threadIdx.x % kWave == 0) bounds[wave] = b;
+  }
+  __syncthreads();
+  const int lo = bounds[0], hi = bounds[1];
   const int32_t dummy = (int32_t)max<int64_t>(0, min<int64_t>(shard_rows, V - base));
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < C;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -1196,8 +1241,23 @@ extern "C" int ctr_plan_slot_to_unique(const ctr_sparse_plan* plan, int32_t* slo
 
 extern "C" int ctr_plan_shard_counts(const ctr_sparse_plan* plan, int64_t shard_rows,
                                      int n_shards, int64_t* counts, ctr_stream_t stream) {
+  return ctr_plan_shard_counts_max(plan, shard_rows, n_shards, counts, nullptr, stream);
+}
+
+extern "C" int ctr_plan_shard_counts_max(const ctr_sparse_plan* plan, int64_t shard_rows,
+                                         int n_shards, int64_t* counts, int64_t* max_out,
+                                         ctr_stream_t stream) {
   CTR_REQUIRE(plan_ok(plan) && counts && shard_rows > 0 && n_shards > 0,
               "ctr_plan_shard_counts: bad arguments");
+  // the last boundary is lower_bound(n_shards * shard_rows): int32 ids stay below it
+  if (n_shards <= kCountsMaxShards) {
+    hipLaunchKernelGGL(shard_counts_max_kernel, 1, kWave * (n_shards + 1), 0, as_stream(stream),
+                       plan->unique_rows, plan->num_unique, shard_rows, n_shards, counts, max_out);
+    CTR_LAUNCH_CHECK("shard_counts_max_kernel");
+    return CTR_OK;
+  }
+  CTR_REQUIRE(max_out == nullptr, "ctr_plan_shard_counts_max: the maximum needs <= %d shards",
+              kCountsMaxShards);
   hipLaunchKernelGGL(shard_counts_kernel, (unsigned)ceil_div(n_shards, 64), 64, 0,
                      as_stream(stream), plan->unique_rows, plan->num_unique, shard_rows, n_shards,
                      counts);

@@ -554,12 +554,16 @@ class SparsePlanBuffers:
         lib.ctr_plan_slot_to_unique(self.struct(), _p(out), _stream())
         return out
 
-    def shard_counts(self, shard_rows: int, n_shards: int,
-                     out: torch.Tensor | None = None) -> torch.Tensor:
-        """int64[n_shards]: unique rows owned by each shard (ids // shard_rows)."""
+    def shard_counts(self, shard_rows: int, n_shards: int, out: torch.Tensor | None = None,
+                     max_out: torch.Tensor | None = None) -> torch.Tensor:
+        """int64[n_shards]: unique rows owned by each shard (ids // shard_rows); max_out
+        (int64[1], n_shards <= 15): their maximum, from the same launch."""
         if out is None:
             out = torch.empty(n_shards, dtype=torch.int64, device=self.device)
-        lib.ctr_plan_shard_counts(self.struct(), int(shard_rows), int(n_shards), _p(out), _stream())
+        if max_out is not None and (max_out.dtype != torch.int64 or max_out.numel() < 1):
+            raise ValueError("shard_counts: max_out must be an int64 tensor")
+        lib.ctr_plan_shard_counts_max(self.struct(), int(shard_rows), int(n_shards), _p(out),
+                                      _p(max_out), _stream())
         return out
 
 

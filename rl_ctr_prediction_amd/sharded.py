@@ -521,8 +521,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
 
     def _plan_launch(self, slot: InputSlot) -> None:
         slot.plan.build(slot.ids, self.V, err_flag=self.err)
-        slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts)
-        torch.amax(slot.counts, dim=0, keepdim=True, out=slot.cap)
+        if self.world_size <= 15:  # the counts and their maximum in one launch
+            slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts,
+                                   max_out=slot.cap)
+        else:
+            slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts)
+            torch.amax(slot.counts, dim=0, keepdim=True, out=slot.cap)
 
     def _runs_mask(self, n_rows: int) -> torch.Tensor:
         """The owner plan's per-row run mask (zero between uses; ctr_sparse_plan_build_runs)."""

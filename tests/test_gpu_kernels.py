@@ -710,3 +710,58 @@ def test_sparse_plan_runs_bit_exact(cuda, N, C, n_rows, seed):
     assert torch.equal(a.unique_rows[:U], b.unique_rows[:U])
     assert torch.equal(a.seg_offsets[:U + 1], b.seg_offsets[:U + 1])
     assert int(mask.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("n_shards", [1, 2, 3, 8, 15, 16])
+@pytest.mark.parametrize("case", ["zipf", "empty", "one", "one_shard", "boundaries"])
+def test_plan_shard_counts_and_max(cuda, n_shards, case):
+    """ctr_plan_shard_counts(_max): per-shard unique-row counts (the wave-parallel 64-ary
+    search for <= 15 shards, the per-shard binary search above) == numpy, and max_out == their
+    maximum — the run length that sizes the row-sharded exchange; ctr_shard_pack_ids' padded
+    exchange layout (its own per-block run search) with the same counts and offsets."""
+    from rl_ctr_prediction_amd import hip_ops
+    V = 1_000_003
+    shard_rows = -(-V // n_shards)
+    rng = np.random.default_rng(n_shards * 7 + len(case))
+    if case == "zipf":
+        ids = np.minimum(rng.zipf(1.2, size=8192 * 26) - 1, V - 1)
+    elif case == "empty":
+        ids = np.zeros(0, dtype=np.int64)
+    elif case == "one":
+        ids = np.array([V - 1])
+    elif case == "one_shard":
+        ids = rng.integers(0, min(shard_rows, V), size=50_000)
+    else:  # every shard's first and last row, and their neighbours
+        b = np.arange(n_shards + 1) * shard_rows
+        ids = np.concatenate([b - 1, b, b + 1])
+        ids = ids[(ids >= 0) & (ids < V)]
+    plan = hip_ops.SparsePlanBuffers(max(ids.size, 1), cuda).build(
+        torch.tensor(ids.astype(np.int64), device=cuda).reshape(1, -1) if ids.size else
+        torch.zeros(0, 1, dtype=torch.int64, device=cuda), V)
+    uniq = np.unique(ids)
+    want = np.bincount(uniq // shard_rows, minlength=n_shards)[:n_shards].astype(np.int64)
+    got = plan.shard_counts(shard_rows, n_shards).cpu().numpy()
+    assert np.array_equal(got, want), (got, want)
+    # the padded exchange layout (ctr_shard_pack_ids: the same run bounds, searched per block)
+    C = max(int(want.max()) + 3, 1)
+    send = torch.full((n_shards * C,), -7, dtype=torch.int32, device=cuda)
+    cnt = torch.zeros(n_shards, dtype=torch.int32, device=cuda)
+    off = torch.zeros(n_shards, dtype=torch.int32, device=cuda)
+    hip_ops.shard_pack_ids(plan, shard_rows, V, n_shards, C, send, cnt, off)
+    send = send.cpu().numpy().reshape(n_shards, C)
+    assert np.array_equal(cnt.cpu().numpy(), want)
+    assert np.array_equal(off.cpu().numpy(), np.concatenate([[0], np.cumsum(want)[:-1]]))
+    for j in range(n_shards):
+        run = uniq[uniq // shard_rows == j] - j * shard_rows
+        spare = max(0, min(shard_rows, V - j * shard_rows))
+        assert np.array_equal(send[j, :run.size], run)
+        assert (send[j, run.size:] == spare).all()
+    if n_shards <= 15:
+        mx = torch.full((1,), -1, dtype=torch.int64, device=cuda)
+        got2 = plan.shard_counts(shard_rows, n_shards, max_out=mx).cpu().numpy()
+        assert np.array_equal(got2, want)
+        assert int(mx.item()) == int(want.max()), (int(mx.item()), want)
+    else:
+        with pytest.raises(Exception, match="15 shards"):
+            plan.shard_counts(shard_rows, n_shards,
+                              max_out=torch.zeros(1, dtype=torch.int64, device=cuda))
