@@ -306,6 +306,23 @@ int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t 
 int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, int64_t capacity,
                         int n_shards, const int32_t* counts, const int32_t* offsets, int pack,
                         ctr_stream_t stream);
+/* The same exchange with each row's linear weight in the same message: the padded buffer is
+ * n_shards chunks of `chunk` floats (chunk >= capacity*K + capacity, a multiple of 4), chunk j
+ * = [capacity rows of K floats][capacity linear weights][padding]; lin == NULL: rows only.
+ * One equal-split all-to-all then moves rows and weights (and their gradients) together.
+ * ctr_shard_gather_rows (owner): chunk j row i = (emb[ids[j*capacity+i]], lin[...]).
+ * ctr_shard_rows_pack: chunk j row i = (rows[offsets[j]+i], lin[...]) for i < counts[j],
+ *   zeros past it.  ctr_shard_rows_unpack: the reverse, for i < counts[j].
+ * K % 4 == 0, 16-B aligned buffers. */
+int ctr_shard_gather_rows(const float* emb, const float* lin, int K, const int32_t* ids,
+                          int n_shards, int64_t capacity, int64_t chunk, float* out,
+                          ctr_stream_t stream);
+int ctr_shard_rows_pack(const float* rows, const float* lin, int K, int64_t capacity,
+                        int64_t chunk, int n_shards, const int32_t* counts,
+                        const int32_t* offsets, float* out, ctr_stream_t stream);
+int ctr_shard_rows_unpack(const float* in, int K, int64_t capacity, int64_t chunk, int n_shards,
+                          const int32_t* counts, const int32_t* offsets, float* rows, float* lin,
+                          ctr_stream_t stream);
 int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
                           void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
 /* The same plan (bit-identical) for ids laid out as a [S/F][F] matrix (slot s = b*F + f: the

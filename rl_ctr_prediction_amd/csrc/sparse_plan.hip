@@ -847,6 +847,48 @@ __global__ __launch_bounds__(256) void shard_runs_copy_kernel(
   }
 }
 
+// The row-sharded exchange's rows WITH their linear weight in one message per (requester,
+// owner) pair: chunk j of the padded buffer = [C rows of K floats][C linear weights][pad to a
+// multiple of 4] (`chunk` floats), so a step moves the embedding rows and the linear weights
+// (and their gradients) in one equal-split all-to-all each instead of two. One thread per
+// float4 of a row; the thread of the row's first float4 also moves its linear weight.
+//   GATHER: chunked[j][i] = (E[ids[jC+i]], lin[ids[jC+i]])           (owner, rows out)
+//   PACK:   chunked[j][i] = (rows[off_j+i], lin[off_j+i]), zeros past counts[j]
+//   UNPACK: (rows[off_j+i], lin[off_j+i]) = chunked[j][i] for i < counts[j]
+enum { kRowsGather = 0, kRowsPack = 1, kRowsUnpack = 2 };
+template <int MODE>
+__global__ __launch_bounds__(256) void shard_rows_lin_kernel(
+    const float4* __restrict__ src, const float* __restrict__ src_lin, float4* __restrict__ dst,
+    float* __restrict__ dst_lin, const int32_t* __restrict__ ids, int64_t K4, int64_t C,
+    int64_t chunk, const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets) {
+  const int j = blockIdx.y;
+  const int64_t cnt = MODE == kRowsGather ? C : min<int64_t>(counts[j], C);
+  const int64_t off = MODE == kRowsGather ? 0 : offsets[j];
+  const int64_t n = (MODE == kRowsUnpack ? cnt : C) * K4;
+  const int64_t cbase = (int64_t)j * chunk;  // floats
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / K4, k = t - i * K4;
+    if (MODE == kRowsUnpack) {
+      const float* cs = reinterpret_cast<const float*>(src) + cbase;  // chunk j
+      dst[(off + i) * K4 + k] = reinterpret_cast<const float4*>(cs + i * 4 * K4)[k];
+      if (k == 0 && dst_lin) dst_lin[off + i] = cs[C * 4 * K4 + i];
+    } else {
+      float* const cf = reinterpret_cast<float*>(dst) + cbase;  // chunk j
+      float4* const crow = reinterpret_cast<float4*>(cf + i * 4 * K4);
+      if (MODE == kRowsGather) {
+        const int64_t r = ids[(int64_t)j * C + i];
+        crow[k] = src[r * K4 + k];
+        if (k == 0 && src_lin) cf[C * 4 * K4 + i] = src_lin[r];
+      } else {
+        const bool live = i < cnt;
+        crow[k] = live ? src[(off + i) * K4 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k == 0 && src_lin) cf[C * 4 * K4 + i] = live ? src_lin[off + i] : 0.f;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host side --------
 static int key_bits(int64_t V) {
   int bits = 1;
@@ -1308,6 +1350,55 @@ extern "C" int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, 
   }
   CTR_LAUNCH_CHECK("shard_runs_copy_kernel");
   return CTR_OK;
+}
+
+// chunked E + linear rows (shard_rows_lin_kernel): chunk >= C*K (+ C with a linear table),
+// a multiple of 4; K % 4 == 0; 16-B aligned buffers
+static bool rows_lin_ok(const void* a, const void* b, int K, int64_t C, int64_t chunk, bool lin) {
+  return a && b && K > 0 && K % 4 == 0 && C > 0 && chunk % 4 == 0 &&
+         chunk >= C * K + (lin ? C : 0) && ((uintptr_t)a | (uintptr_t)b) % 16 == 0;
+}
+
+template <int MODE>
+static int rows_lin_launch(const float* src, const float* src_lin, float* dst, float* dst_lin,
+                           const int32_t* ids, int K, int64_t C, int64_t chunk, int n_shards,
+                           const int32_t* counts, const int32_t* offsets, ctr_stream_t stream) {
+  const int64_t K4 = K / 4;
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(C * K4, 256), 2048), (unsigned)n_shards);
+  hipLaunchKernelGGL(shard_rows_lin_kernel<MODE>, grid, 256, 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(src), src_lin, reinterpret_cast<float4*>(dst),
+                     dst_lin, ids, K4, C, chunk, counts, offsets);
+  CTR_LAUNCH_CHECK("shard_rows_lin_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_shard_gather_rows(const float* emb, const float* lin, int K, const int32_t* ids,
+                                     int n_shards, int64_t capacity, int64_t chunk, float* out,
+                                     ctr_stream_t stream) {
+  CTR_REQUIRE(ids && n_shards > 0 && rows_lin_ok(emb, out, K, capacity, chunk, lin != nullptr),
+              "ctr_shard_gather_rows: bad arguments");
+  return rows_lin_launch<kRowsGather>(emb, lin, out, nullptr, ids, K, capacity, chunk, n_shards,
+                                      nullptr, nullptr, stream);
+}
+
+extern "C" int ctr_shard_rows_pack(const float* rows, const float* lin, int K, int64_t capacity,
+                                   int64_t chunk, int n_shards, const int32_t* counts,
+                                   const int32_t* offsets, float* out, ctr_stream_t stream) {
+  CTR_REQUIRE(counts && offsets && n_shards > 0 &&
+                  rows_lin_ok(rows, out, K, capacity, chunk, lin != nullptr),
+              "ctr_shard_rows_pack: bad arguments");
+  return rows_lin_launch<kRowsPack>(rows, lin, out, nullptr, nullptr, K, capacity, chunk, n_shards,
+                                    counts, offsets, stream);
+}
+
+extern "C" int ctr_shard_rows_unpack(const float* in, int K, int64_t capacity, int64_t chunk,
+                                     int n_shards, const int32_t* counts, const int32_t* offsets,
+                                     float* rows, float* lin, ctr_stream_t stream) {
+  CTR_REQUIRE(counts && offsets && n_shards > 0 &&
+                  rows_lin_ok(in, rows, K, capacity, chunk, lin != nullptr),
+              "ctr_shard_rows_unpack: bad arguments");
+  return rows_lin_launch<kRowsUnpack>(in, nullptr, rows, lin, nullptr, K, capacity, chunk,
+                                      n_shards, counts, offsets, stream);
 }
 
 static int64_t runs_ws_layout(int64_t n_rows, int64_t n_runs, int64_t* off_word, int64_t* off_block,

@@ -621,6 +621,64 @@ def shard_runs_copy(src: torch.Tensor, dst: torch.Tensor, capacity: int, counts:
     return dst
 
 
+def rows_chunk(capacity: int, K: int, lin: bool) -> int:
+    """Floats per (requester, owner) chunk of the rows + linear-weight exchange layout
+    (ctr_shard_gather_rows / _rows_pack / _rows_unpack): capacity rows of K floats, then the
+    capacity linear weights, padded to a multiple of 4."""
+    return capacity * K + ((capacity + 3) // 4 * 4 if lin else 0)
+
+
+def _rows_lin_check(name, chunked, n_shards, chunk, rows, K, lin):
+    _f32(chunked, name)
+    if chunked.numel() < n_shards * chunk:
+        raise ValueError(f"{name}: needs n_shards * chunk = {n_shards * chunk} floats")
+    _f32(rows, "rows")
+    if rows.dim() != 2 or rows.shape[1] != K:
+        raise ValueError(f"{name}: rows must be [*, {K}]")
+    if lin is not None:
+        _f32(lin, "lin")
+
+
+def shard_gather_rows(emb: torch.Tensor, lin: torch.Tensor | None, ids: torch.Tensor,
+                      n_shards: int, capacity: int, out: torch.Tensor) -> torch.Tensor:
+    """Owner side: the requested rows and their linear weights into the chunked exchange
+    layout (ctr_shard_gather_rows); ids int32[n_shards * capacity]."""
+    K = emb.shape[1]
+    chunk = rows_chunk(capacity, K, lin is not None)
+    _rows_lin_check("shard_gather_rows", out, n_shards, chunk, emb, K, lin)
+    _dev(ids, "ids")
+    if ids.dtype != torch.int32 or ids.numel() < n_shards * capacity:
+        raise ValueError("shard_gather_rows: ids must be int32 of n_shards * capacity")
+    lib.ctr_shard_gather_rows(_p(emb), _p(lin), K, _p(ids), int(n_shards), int(capacity), chunk,
+                              _p(out), _stream())
+    return out
+
+
+def shard_rows_pack(rows: torch.Tensor, lin: torch.Tensor | None, capacity: int,
+                    counts: torch.Tensor, offsets: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """Compact rows (+ linear values) -> the chunked exchange layout, zeros past each run
+    (ctr_shard_rows_pack)."""
+    n, K = counts.numel(), rows.shape[1]
+    chunk = rows_chunk(capacity, K, lin is not None)
+    _rows_lin_check("shard_rows_pack", out, n, chunk, rows, K, lin)
+    lib.ctr_shard_rows_pack(_p(rows), _p(lin), K, int(capacity), chunk, n, _p(counts),
+                            _p(offsets), _p(out), _stream())
+    return out
+
+
+def shard_rows_unpack(chunked: torch.Tensor, capacity: int, counts: torch.Tensor,
+                      offsets: torch.Tensor, rows: torch.Tensor,
+                      lin: torch.Tensor | None = None) -> torch.Tensor:
+    """The chunked exchange layout -> compact rows (+ linear values), the runs only
+    (ctr_shard_rows_unpack)."""
+    n, K = counts.numel(), rows.shape[1]
+    chunk = rows_chunk(capacity, K, lin is not None)
+    _rows_lin_check("shard_rows_unpack", chunked, n, chunk, rows, K, lin)
+    lib.ctr_shard_rows_unpack(_p(chunked), K, int(capacity), chunk, n, _p(counts), _p(offsets),
+                              _p(rows), _p(lin), _stream())
+    return rows
+
+
 def ids_add_(ids: torch.Tensor, delta: int) -> torch.Tensor:
     """In place: ids += delta (int32 device ids)."""
     _dev(ids, "ids")

@@ -57,26 +57,31 @@ CAP_QUANTUM = 1024  # exchange capacities are multiples of this many rows
 
 
 class _XBufs:
-    """The fixed-capacity exchange buffers of one (batch shape, capacity)."""
+    """The fixed-capacity exchange buffers of one (batch shape, capacity). Rows travel with
+    their linear weight in one chunk per (requester, owner) pair (hip_ops.rows_chunk floats:
+    C rows of K, then the C weights), so each direction is one all-to-all."""
 
     def __init__(self, n: int, C: int, S: int, K: int, lin: bool, dev):
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         NC = n * C
+        self.chunk = hip_ops.rows_chunk(C, K, lin)
         self.send_ids, self.recv_ids = torch.empty(NC, **i32), torch.empty(NC, **i32)
         self.counts, self.offsets = torch.empty(n, **i32), torch.empty(n, **i32)
-        self.rows_out, self.rows_in = torch.empty(NC, K, **f32), torch.empty(NC, K, **f32)
+        # every chunk's C rows in source order: the owner's view of the received gradients
+        self.all_counts = torch.full((n,), C, **i32)
+        self.all_offsets = torch.arange(n, **i32) * C
+        self.rows_out, self.rows_in = (torch.empty(n * self.chunk, **f32) for _ in range(2))
+        self.g_out, self.g_recv = (torch.empty(n * self.chunk, **f32) for _ in range(2))
         self.table = torch.empty(max(S, 1), K, **f32)  # the batch's rows, compact
-        self.g_out, self.g_in = torch.empty(NC, K, **f32), torch.empty(NC, K, **f32)
+        self.g_in = torch.empty(NC, K, **f32)          # owner: received gradients, by source
         self.g_rows = torch.empty(NC, K, **f32)
         if lin:
-            self.lin_out, self.lin_in = torch.empty(NC, **f32), torch.empty(NC, **f32)
             self.lin_table = torch.empty(max(S, 1), **f32)
-            self.glin_out, self.glin_in = torch.empty(NC, **f32), torch.empty(NC, **f32)
+            self.glin_in = torch.empty(NC, **f32)
             self.g_lin = torch.empty(NC, **f32)
         else:
-            self.lin_out = self.lin_in = self.lin_table = None
-            self.glin_out = self.glin_in = self.g_lin = None
+            self.lin_table = self.glin_in = self.g_lin = None
         self.gplan = hip_ops.SparsePlanBuffers(NC, dev)
         self.slot2u = torch.empty(max(S, 1), **i32)
 
@@ -277,7 +282,12 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         return t
 
     def _buffers(self, B: int, F: int):
+        fresh = (B, F) not in self._bufsets
         b = super()._buffers(B, F)
+        if fresh and self._coll and self.exchange == "padded":
+            # the batch loss lives in the dense gradient's tail: one all-reduce carries both
+            n = self.flat_grad.numel()
+            b.loss = self._grad_ext[n:n + 1]
         if b.gplan is None:  # world size 1: the owner-side plan is still needed
             S = B * F * self.world_size
             e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
@@ -623,28 +633,26 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                                    step_dev=self.step_done)
         self._span("catchup", t)
         t = self._mark("exchange")
-        hip_ops.embedding_gather(self.E_tab, xb.recv_ids, out=xb.rows_out)
+        # the rows and their linear weights: one gather, one all-to-all, one unpack
+        hip_ops.shard_gather_rows(self.E_tab, self.w_tab if has_lin else None, xb.recv_ids, n,
+                                  C, out=xb.rows_out)
         alltoall_equal(xb.rows_in, xb.rows_out, self.group, force=f)
-        hip_ops.shard_runs_copy(xb.rows_in, xb.table, C, xb.counts, xb.offsets, pack=False)
-        T_lin = None
-        if has_lin:
-            hip_ops.embedding_gather(self.w_tab.view(Vo, 1), xb.recv_ids,
-                                     out=xb.lin_out.view(-1, 1))
-            alltoall_equal(xb.lin_in, xb.lin_out, self.group, force=f)
-            hip_ops.shard_runs_copy(xb.lin_in, xb.lin_table, C, xb.counts, xb.offsets, pack=False)
-            T_lin = xb.lin_table.view(-1, 1)
+        hip_ops.shard_rows_unpack(xb.rows_in, C, xb.counts, xb.offsets, xb.table,
+                                  xb.lin_table if has_lin else None)
+        T_lin = xb.lin_table.view(-1, 1) if has_lin else None
         self._span("exchange", t)
         # 3. forward + backward over the compact table
         ids = plan.slot_to_unique(out=xb.slot2u)[:B * F].view(B, F)
         T = xb.table
         gz = self._sharded_fwd_bwd(ids, y, b, T, T_lin, bias, mean_div, F)
-        # 4. gradients to the owners, summed per row in (source rank, position) order
+        # 4. gradients (with the linear ones) to the owners in one all-to-all, then every
+        # source's chunk into the (source, position) order the owner plan indexes
         t = self._mark("exchange")
-        hip_ops.shard_runs_copy(b.grad_rows, xb.g_out, C, xb.counts, xb.offsets, pack=True)
-        alltoall_equal(xb.g_in, xb.g_out, self.group, force=f)
-        if has_lin:
-            hip_ops.shard_runs_copy(b.grad_lin, xb.glin_out, C, xb.counts, xb.offsets, pack=True)
-            alltoall_equal(xb.glin_in, xb.glin_out, self.group, force=f)
+        hip_ops.shard_rows_pack(b.grad_rows, b.grad_lin if has_lin else None, C, xb.counts,
+                                xb.offsets, out=xb.g_out)
+        alltoall_equal(xb.g_recv, xb.g_out, self.group, force=f)
+        hip_ops.shard_rows_unpack(xb.g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
+                                  xb.glin_in if has_lin else None)
         self._span("exchange", t)
         # 5. the owners' sums and Adam here, beside the weight-gradient stream (dW0 ...);
         # only the dense all-reduce and the dense Adam wait for it (6.)
@@ -679,9 +687,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 6. the dense gradient (and the loss) over the ranks, then the dense Adam
         t = self._mark("exchange")
         self._join_wgrad()
-        allreduce_sum_(self.flat_grad, self.group, force=f)
-        if f:
-            allreduce_sum_(b.loss, self.group, force=f)
+        if f:  # the dense gradient and, in its tail, the batch loss: one collective
+            allreduce_sum_(self._grad_ext, self.group, force=f)
             b.loss.div_(n)
         self._span("exchange", t)
         self._adam_dense(step_hint)

@@ -187,7 +187,10 @@ class FusedCTRTrainer:
             self.offsets[n] = total
             total += (named[n].numel() + 3) // 4 * 4
         flat = torch.zeros(total, dtype=torch.float32, device=self.device)
-        self.flat_grad = torch.zeros_like(flat)
+        # the dense gradient with 4 floats of tail room: the row-sharded step all-reduces the
+        # batch loss there, in the gradient's own collective (sharded.py)
+        self._grad_ext = torch.zeros(total + 4, dtype=torch.float32, device=self.device)
+        self.flat_grad = self._grad_ext[:total]
         self.views, self.grad_views = {}, {}
         for n in self.dense_names:
             p, off = named[n], self.offsets[n]

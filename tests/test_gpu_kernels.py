@@ -765,3 +765,52 @@ def test_plan_shard_counts_and_max(cuda, n_shards, case):
         with pytest.raises(Exception, match="15 shards"):
             plan.shard_counts(shard_rows, n_shards,
                               max_out=torch.zeros(1, dtype=torch.int64, device=cuda))
+
+
+@pytest.mark.parametrize("n,C,K,lin", [(1, 1024, 64, True), (3, 1000, 16, True), (8, 37, 4, False),
+                                       (2, 5, 8, True)])
+def test_shard_rows_lin_exchange_layout(cuda, n, C, K, lin):
+    """The chunked rows + linear-weight exchange (ctr_shard_gather_rows / _rows_pack /
+    _rows_unpack) == the layout written out with numpy: chunk j = [C rows][C weights][pad];
+    pack zero-fills past each run, unpack restores exactly the runs, gather reads the ids."""
+    from rl_ctr_prediction_amd import hip_ops
+    rng = np.random.default_rng(n * C + K)
+    Vo = 500
+    E = rng.standard_normal((Vo, K)).astype(np.float32)
+    w = rng.standard_normal(Vo).astype(np.float32)
+    counts = rng.integers(0, C + 1, size=n).astype(np.int32)
+    offsets = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+    U = int(counts.sum())
+    chunk = hip_ops.rows_chunk(C, K, lin)
+    assert chunk % 4 == 0 and chunk >= C * K + (C if lin else 0)
+    d = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    # gather (owner side): chunk j row i = E[ids[j*C+i]], w[ids[j*C+i]]
+    ids = rng.integers(0, Vo, size=n * C).astype(np.int32)
+    out = torch.full((n * chunk,), float("nan"), device=cuda)
+    hip_ops.shard_gather_rows(d(E), d(w) if lin else None, d(ids), n, C, out=out)
+    o = out.cpu().numpy().reshape(n, chunk)
+    for j in range(n):
+        assert np.array_equal(o[j, :C * K].reshape(C, K), E[ids[j * C:(j + 1) * C]])
+        if lin:
+            assert np.array_equal(o[j, C * K:C * K + C], w[ids[j * C:(j + 1) * C]])
+    # pack: compact rows -> chunks, zeros past each run
+    rows = rng.standard_normal((max(U, 1), K)).astype(np.float32)
+    lv = rng.standard_normal(max(U, 1)).astype(np.float32)
+    out = torch.full((n * chunk,), float("nan"), device=cuda)
+    hip_ops.shard_rows_pack(d(rows), d(lv) if lin else None, C, d(counts), d(offsets), out=out)
+    o = out.cpu().numpy().reshape(n, chunk)
+    for j in range(n):
+        c, f = counts[j], offsets[j]
+        blk = o[j, :C * K].reshape(C, K)
+        assert np.array_equal(blk[:c], rows[f:f + c]) and (blk[c:] == 0).all()
+        if lin:
+            assert np.array_equal(o[j, C * K:C * K + c], lv[f:f + c])
+            assert (o[j, C * K + c:C * K + C] == 0).all()
+    # unpack: the chunks back to the runs (rows past U untouched)
+    back = torch.full((max(U, 1) + 3, K), -5.0, device=cuda)
+    backl = torch.full((max(U, 1) + 3,), -5.0, device=cuda)
+    hip_ops.shard_rows_unpack(out, C, d(counts), d(offsets), back, backl if lin else None)
+    assert np.array_equal(back.cpu().numpy()[:U], rows[:U])
+    assert (back.cpu().numpy()[max(U, 1):] == -5.0).all()
+    if lin:
+        assert np.array_equal(backl.cpu().numpy()[:U], lv[:U])
