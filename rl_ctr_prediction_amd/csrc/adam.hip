@@ -701,6 +701,81 @@ extern "C" int ctr_adam_embedding(float* emb, float* m_emb, float* v_emb, float*
   return CTR_OK;
 }
 
+// The owner side of a row-sharded step: each unique row's gradient is the sum of its few
+// received entries (at most one per requester: a requester sends each row once), summed in
+// plan order — source rank, then position — straight in the lane group that then replays
+// the row's missed steps and applies this one (deferred_rows_vec<APPLY>'s update, the same
+// adam_vec chain). One launch instead of the chunked segmented sums + fused apply, whose
+// chunk machinery pays off for long segments (a batch's hot rows), not for runs of <= N.
+// skip_row (the owner's spare row, the target of every padding entry: a long segment whose
+// value is never used) is left alone. out / out_lin (optional): the sums.
+template <int K4>
+__global__ __launch_bounds__(256) void deferred_entries_vec(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw,
+    int32_t* __restrict__ last, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ num_unique, const int32_t* __restrict__ seg_offsets,
+    const int32_t* __restrict__ sorted_entries, const float4* __restrict__ vals,
+    const float* __restrict__ vals_lin, int64_t skip_row, int step_val,
+    const int32_t* __restrict__ step_ptr, const float* __restrict__ tab, AdamHP h,
+    float4* __restrict__ out, float* __restrict__ out_lin) {
+  constexpr int kTabWin = CTR_ROWS_TAB_WIN > 0 ? CTR_ROWS_TAB_WIN : 1;
+  __shared__ float2 s_tab[kTabWin];
+  const int c = threadIdx.x % K4;
+  const int64_t groups = (int64_t)gridDim.x * (blockDim.x / K4);
+  const int U = *num_unique;
+  const int step = step_ptr ? *step_ptr : step_val;
+  const int target = step - 1;
+  const int win0 = CTR_ROWS_TAB_WIN > 0 ? max(0, target - kTabWin + 1) : target + 1;
+  if (threadIdx.x < kTabWin && win0 + (int)threadIdx.x <= target)
+    s_tab[threadIdx.x] = reinterpret_cast<const float2*>(tab)[win0 + threadIdx.x];
+  __syncthreads();
+  for (int64_t u = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / K4; u < U; u += groups) {
+    const int64_t r = rows[u];
+    if (r == skip_row) continue;
+    const int64_t e = r * K4 + c;
+    const int from = last[r];
+    float4 pp = E[e], mm = mE[e], vv = vE[e];
+    float pw = 0.f, mws = 0.f, vws = 0.f;
+    const bool own_lin = w && c == 0;
+    if (own_lin) {
+      pw = w[r]; mws = mw[r]; vws = vw[r];
+    }
+    const int p0 = seg_offsets[u], p1 = seg_offsets[u + 1];
+    int64_t s = sorted_entries[p0];
+    float4 g = vals[s * K4 + c];
+    float gl = own_lin ? vals_lin[s] : 0.f;
+    for (int p = p0 + 1; p < p1; ++p) {
+      s = sorted_entries[p];
+      const float4 x = vals[s * K4 + c];
+      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+      if (own_lin) gl += vals_lin[s];
+    }
+    if (out) out[u * K4 + c] = g;
+    if (out_lin && c == 0) out_lin[u] = gl;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = from + 1; t <= target; ++t) {
+      if (t >= win0) {
+        const float2 v = s_tab[t - win0];
+        h.neg_step_size = v.x;
+        h.inv_bc2_sqrt = v.y;
+      } else {
+        load_step(h, tab, t);
+      }
+      adam_vec(pp, z4, mm, vv, h);
+      if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
+    }
+    load_step(h, tab, step);
+    adam_vec(pp, g, mm, vv, h);
+    if (own_lin) adam_elem(pw, gl, mws, vws, h);
+    E[e] = pp; mE[e] = mm; vE[e] = vv;
+    if (own_lin) {
+      w[r] = pw; mw[r] = mws; vw[r] = vws;
+    }
+    if (c == 0) last[r] = step;
+  }
+}
+
 static bool deferred_vec_ok(int K, const void* a, const void* b, const void* c, const void* g) {
   return K % 4 == 0 && K / 4 <= 64 && (kWave % (K / 4)) == 0 &&
          ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)g) % 16 == 0;
@@ -764,6 +839,51 @@ extern "C" int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, fl
                        v_lin, n, K, last, plan->unique_rows, plan->num_unique, nullptr, nullptr,
                        (int)step, step_ptr, step_table, h);
   CTR_LAUNCH_CHECK("deferred_scalar");
+  return CTR_OK;
+}
+
+extern "C" int ctr_adam_deferred_entries(float* emb, float* m_emb, float* v_emb, float* lin,
+                                         float* m_lin, float* v_lin, int64_t V, int K,
+                                         int32_t* last, const ctr_sparse_plan* plan,
+                                         const float* vals, const float* vals_lin,
+                                         int64_t skip_row, int64_t step, const int32_t* step_ptr,
+                                         const float* step_table, double beta1, double beta2,
+                                         double eps, double weight_decay, float* out,
+                                         float* out_lin, ctr_stream_t stream) {
+  CTR_REQUIRE(emb && m_emb && v_emb && last && step_table && vals,
+              "ctr_adam_deferred_entries: null pointer");
+  CTR_REQUIRE(plan && plan->unique_rows && plan->num_unique && plan->seg_offsets &&
+                  plan->sorted_slots,
+              "ctr_adam_deferred_entries: bad plan");
+  CTR_REQUIRE(V > 0 && K > 0 && (step_ptr || (step >= 1 && step < (int64_t(1) << 31))),
+              "ctr_adam_deferred_entries: bad sizes");
+  CTR_REQUIRE((lin && m_lin && v_lin && vals_lin) || (!lin && !m_lin && !v_lin),
+              "ctr_adam_deferred_entries: linear table pointers (and vals_lin) all set or all NULL");
+  CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, vals) && (!out || (uintptr_t)out % 16 == 0),
+              "ctr_adam_deferred_entries: needs K %% 4 == 0, (K/4) | 64 and 16-B aligned rows");
+  if (plan->S == 0) return CTR_OK;
+  const AdamHP h = make_hp(1.0, 1.0, beta1, beta2, eps, weight_decay);
+  const int K4 = K / 4;
+  const int64_t n = plan->S;  // upper bound on unique rows
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n * K4, 256), 8192));
+#define CTR_DEF_ENTRIES(K4_)                                                                    \
+  hipLaunchKernelGGL((deferred_entries_vec<K4_>), grid, 256, 0, as_stream(stream),              \
+                     reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
+                     reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                 \
+                     plan->unique_rows, plan->num_unique, plan->seg_offsets, plan->sorted_slots, \
+                     reinterpret_cast<const float4*>(vals), vals_lin, skip_row, (int)step,       \
+                     step_ptr, step_table, h, reinterpret_cast<float4*>(out), out_lin)
+  switch (K4) {
+    case 1: CTR_DEF_ENTRIES(1); break;
+    case 2: CTR_DEF_ENTRIES(2); break;
+    case 4: CTR_DEF_ENTRIES(4); break;
+    case 8: CTR_DEF_ENTRIES(8); break;
+    case 16: CTR_DEF_ENTRIES(16); break;
+    case 32: CTR_DEF_ENTRIES(32); break;
+    case 64: CTR_DEF_ENTRIES(64); break;
+  }
+#undef CTR_DEF_ENTRIES
+  CTR_LAUNCH_CHECK("deferred_entries_vec");
   return CTR_OK;
 }
 

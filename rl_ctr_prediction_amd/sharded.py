@@ -159,6 +159,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             raise ValueError("row sharding needs K % 4 == 0 and (K/4) dividing 64")
         self._side = None  # the exchange needs the plan before anything else
         self._pipe = False  # the dense gradient is all-reduced within its step
+        # owners sum their received entries (<= N per row) straight and apply in one launch;
+        # CTR_OWNER_DIRECT=0: the chunked segmented sums with the fused apply (A/B)
+        self._owner_direct = os.environ.get("CTR_OWNER_DIRECT", "1") != "0"
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
         # the plans (and per-owner counts / run maxima) are built on the plan stream, ahead
@@ -656,7 +659,22 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("exchange", t)
         # 5. the owners' sums and Adam here, beside the weight-gradient stream (dW0 ...);
         # only the dense all-reduce and the dense Adam wait for it (6.)
-        if self.fuse_apply and self.K >= self.fuse_apply_min_k:
+        if self._owner_direct:
+            # each row's <= N received entries summed straight in its lane group, then its
+            # deferred Adam step, one launch (ctr_adam_deferred_entries); the spare row (the
+            # padding target) is skipped
+            t = self._mark("scatter")
+            hip_ops.adam_deferred_entries(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
+                                          self.v_w, self.last, xb.gplan, xb.g_in,
+                                          xb.glin_in if has_lin else None, step_hint,
+                                          self.step_table, self.betas, self.eps,
+                                          self.weight_decay, skip_row=Vo - 1,
+                                          step_dev=self.step_cur,
+                                          out=xb.g_rows if self.keep_grads else None,
+                                          out_lin=xb.g_lin if self.keep_grads and has_lin
+                                          else None)
+            self._span("scatter", t)
+        elif self.fuse_apply and self.K >= self.fuse_apply_min_k:
             # the owners' row sums with each row's deferred Adam step applied where its sum
             # completes (ctr_segment_sum_rows_adam; bitwise the two passes below: one pass
             # over the rows instead of a sums write + read, N = 1 C3 29 us less)

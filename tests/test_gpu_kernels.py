@@ -814,3 +814,75 @@ def test_shard_rows_lin_exchange_layout(cuda, n, C, K, lin):
     assert (back.cpu().numpy()[max(U, 1):] == -5.0).all()
     if lin:
         assert np.array_equal(backl.cpu().numpy()[:U], lv[:U])
+
+
+@pytest.mark.parametrize("K,lin", [(64, True), (16, True), (32, False)])
+def test_adam_deferred_entries_equals_sums_then_rows(cuda, K, lin):
+    """ctr_adam_deferred_entries (the row-sharded owner: each row's entries summed straight,
+    then replayed + stepped) == numpy's sequential fp32 sums in plan order, and the table after
+    it == ctr_adam_deferred_rows with grad_rows = those sums, bitwise; skip_row untouched."""
+    from rl_ctr_prediction_amd import hip_ops as H
+    rng = np.random.default_rng(K)
+    Vo, n, C = 3000, 4, 700
+    spare = Vo - 1
+    # n runs of ascending unique rows padded with the spare row: each row <= n entries
+    ids = np.full((n, C), spare, dtype=np.int32)
+    for j in range(n):
+        cnt = rng.integers(C // 2, C)
+        ids[j, :cnt] = np.sort(rng.choice(spare, size=cnt, replace=False))
+    ids = ids.reshape(-1)
+    vals = rng.standard_normal((n * C, K)).astype(np.float32) * 1e-2
+    vlin = rng.standard_normal(n * C).astype(np.float32) * 1e-2
+    d = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    plan = H.SparsePlanBuffers(n * C, cuda).build(d(ids), Vo)
+    tab = H.AdamStepTable(1e-3, (0.9, 0.999), cuda)
+    E0 = rng.standard_normal((Vo, K)).astype(np.float32) * 0.05
+    w0 = rng.standard_normal(Vo).astype(np.float32) * 0.05
+    last0 = rng.integers(0, 6, size=Vo).astype(np.int32)  # rows 0..5 steps behind
+    step = 7
+
+    def state():
+        z = lambda *s: torch.zeros(*s, device=cuda)  # noqa: E731
+        st = [d(E0), z(Vo, K), z(Vo, K)]
+        st += [d(w0), z(Vo), z(Vo)] if lin else [None, None, None]
+        return st + [d(last0)]
+
+    a = state()
+    U = plan.num_unique_host()
+    sums = torch.zeros(n * C, K, device=cuda)
+    slin = torch.zeros(n * C, device=cuda)
+    H.adam_deferred_entries(*a, plan, d(vals), d(vlin) if lin else None, step, tab,
+                            weight_decay=1e-5, skip_row=spare, out=sums,
+                            out_lin=slin if lin else None)
+    # numpy: sequential sums in plan order
+    srt = plan.sorted_slots[:n * C].cpu().numpy()
+    offs = plan.seg_offsets[:U + 1].cpu().numpy()
+    urows = plan.unique_rows[:U].cpu().numpy()
+    want = np.zeros((U, K), np.float32)
+    want_l = np.zeros(U, np.float32)
+    for u in range(U):
+        if urows[u] == spare:
+            continue
+        e = srt[offs[u]:offs[u + 1]]
+        acc, accl = vals[e[0]].copy(), np.float32(vlin[e[0]])
+        for x in e[1:]:
+            acc = (acc + vals[x]).astype(np.float32)
+            accl = np.float32(accl + vlin[x])
+        want[u], want_l[u] = acc, accl
+    live = urows != spare
+    got = sums[:U].cpu().numpy()
+    assert np.array_equal(got[live], want[live])
+    if lin:
+        assert np.array_equal(slin[:U].cpu().numpy()[live], want_l[live])
+    # the same update from the sums through ctr_adam_deferred_rows
+    b = state()
+    grows = torch.tensor(np.where(live[:, None], want, 0), device=cuda)
+    glin = torch.tensor(np.where(live, want_l, 0), device=cuda) if lin else None
+    H.adam_deferred_rows(*b, plan, step, tab, weight_decay=1e-5, grad_rows=grows,
+                         grad_lin=glin)
+    rows_live = torch.tensor(urows[live].astype(np.int64), device=cuda)
+    for x, y in zip(a, b):
+        if x is None:
+            continue
+        assert torch.equal(x[rows_live], y[rows_live])
+    assert torch.equal(a[0][spare], d(E0)[spare]) and int(a[-1][spare]) == last0[spare]
