@@ -428,11 +428,15 @@ int ctr_adam_deferred_rows(float* emb, float* m_emb, float* v_emb, float* lin, f
  * its entries e in plan order (source rank, then position: sequential fp32 adds), then the
  * row replayed to step-1 and stepped with g_u (ctr_adam_deferred_rows with grad_rows = the
  * sums, in one launch). skip_row (e.g. the shard's spare row, the padding target) is left
- * untouched (-1: none). out [U][K] / out_lin [U] (optional): the sums. K % 4 == 0, (K/4) | 64. */
+ * untouched (-1: none). out [U][K] / out_lin [U] (optional): the sums. K % 4 == 0, (K/4) | 64.
+ * run_len = 0: vals [entries][K], vals_lin [entries]; run_len > 0: vals is the chunked
+ * exchange layout of ctr_shard_rows_pack (entry e = row e % run_len of chunk e / run_len,
+ * chunk floats per chunk, the linear values after the rows; vals_lin unused). */
 int ctr_adam_deferred_entries(float* emb, float* m_emb, float* v_emb, float* lin, float* m_lin,
                               float* v_lin, int64_t V, int K, int32_t* last,
                               const ctr_sparse_plan* plan, const float* vals,
-                              const float* vals_lin, int64_t skip_row, int64_t step,
+                              const float* vals_lin, int64_t run_len, int64_t chunk,
+                              int64_t skip_row, int64_t step,
                               const int32_t* step_ptr, const float* step_table, double beta1,
                               double beta2, double eps, double weight_decay, float* out,
                               float* out_lin, ctr_stream_t stream);

@@ -716,7 +716,8 @@ __global__ __launch_bounds__(256) void deferred_entries_vec(
     int32_t* __restrict__ last, const int32_t* __restrict__ rows,
     const int32_t* __restrict__ num_unique, const int32_t* __restrict__ seg_offsets,
     const int32_t* __restrict__ sorted_entries, const float4* __restrict__ vals,
-    const float* __restrict__ vals_lin, int64_t skip_row, int step_val,
+    const float* __restrict__ vals_lin, int64_t run_len, int64_t chunk, int64_t skip_row,
+    int step_val,
     const int32_t* __restrict__ step_ptr, const float* __restrict__ tab, AdamHP h,
     float4* __restrict__ out, float* __restrict__ out_lin) {
   constexpr int kTabWin = CTR_ROWS_TAB_WIN > 0 ? CTR_ROWS_TAB_WIN : 1;
@@ -741,15 +742,29 @@ __global__ __launch_bounds__(256) void deferred_entries_vec(
     if (own_lin) {
       pw = w[r]; mws = mw[r]; vws = vw[r];
     }
+    // entry s: row s of vals [entries][K] and vals_lin[s]; chunked (run_len > 0): row
+    // s % run_len of chunk s / run_len (chunk floats each: run_len rows, then their linear
+    // values — the exchange's receive buffer as it arrived)
+    auto row_of = [&](int64_t s) -> const float4* {
+      if (run_len == 0) return vals + s * K4;
+      const int64_t j = s / run_len;
+      return reinterpret_cast<const float4*>(reinterpret_cast<const float*>(vals) + j * chunk) +
+             (s - j * run_len) * K4;
+    };
+    auto lin_of = [&](int64_t s) -> float {
+      if (run_len == 0) return vals_lin[s];
+      const int64_t j = s / run_len;
+      return reinterpret_cast<const float*>(vals)[j * chunk + run_len * 4 * K4 + (s - j * run_len)];
+    };
     const int p0 = seg_offsets[u], p1 = seg_offsets[u + 1];
     int64_t s = sorted_entries[p0];
-    float4 g = vals[s * K4 + c];
-    float gl = own_lin ? vals_lin[s] : 0.f;
+    float4 g = row_of(s)[c];
+    float gl = own_lin ? lin_of(s) : 0.f;
     for (int p = p0 + 1; p < p1; ++p) {
       s = sorted_entries[p];
-      const float4 x = vals[s * K4 + c];
+      const float4 x = row_of(s)[c];
       g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-      if (own_lin) gl += vals_lin[s];
+      if (own_lin) gl += lin_of(s);
     }
     if (out) out[u * K4 + c] = g;
     if (out_lin && c == 0) out_lin[u] = gl;
@@ -846,7 +861,8 @@ extern "C" int ctr_adam_deferred_entries(float* emb, float* m_emb, float* v_emb,
                                          float* m_lin, float* v_lin, int64_t V, int K,
                                          int32_t* last, const ctr_sparse_plan* plan,
                                          const float* vals, const float* vals_lin,
-                                         int64_t skip_row, int64_t step, const int32_t* step_ptr,
+                                         int64_t run_len, int64_t chunk, int64_t skip_row,
+                                         int64_t step, const int32_t* step_ptr,
                                          const float* step_table, double beta1, double beta2,
                                          double eps, double weight_decay, float* out,
                                          float* out_lin, ctr_stream_t stream) {
@@ -857,8 +873,11 @@ extern "C" int ctr_adam_deferred_entries(float* emb, float* m_emb, float* v_emb,
               "ctr_adam_deferred_entries: bad plan");
   CTR_REQUIRE(V > 0 && K > 0 && (step_ptr || (step >= 1 && step < (int64_t(1) << 31))),
               "ctr_adam_deferred_entries: bad sizes");
-  CTR_REQUIRE((lin && m_lin && v_lin && vals_lin) || (!lin && !m_lin && !v_lin),
+  CTR_REQUIRE((lin && m_lin && v_lin && (vals_lin || run_len > 0)) || (!lin && !m_lin && !v_lin),
               "ctr_adam_deferred_entries: linear table pointers (and vals_lin) all set or all NULL");
+  CTR_REQUIRE(run_len >= 0 && (run_len == 0 || (chunk % 4 == 0 &&
+                                                 chunk >= run_len * K + (lin ? run_len : 0))),
+              "ctr_adam_deferred_entries: chunk must hold run_len rows (+ their linear values)");
   CTR_REQUIRE(deferred_vec_ok(K, emb, m_emb, v_emb, vals) && (!out || (uintptr_t)out % 16 == 0),
               "ctr_adam_deferred_entries: needs K %% 4 == 0, (K/4) | 64 and 16-B aligned rows");
   if (plan->S == 0) return CTR_OK;
@@ -871,7 +890,8 @@ extern "C" int ctr_adam_deferred_entries(float* emb, float* m_emb, float* v_emb,
                      reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),          \
                      reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, last,                 \
                      plan->unique_rows, plan->num_unique, plan->seg_offsets, plan->sorted_slots, \
-                     reinterpret_cast<const float4*>(vals), vals_lin, skip_row, (int)step,       \
+                     reinterpret_cast<const float4*>(vals), vals_lin, run_len, chunk, skip_row, \
+                     (int)step,                                                                  \
                      step_ptr, step_table, h, reinterpret_cast<float4*>(out), out_lin)
   switch (K4) {
     case 1: CTR_DEF_ENTRIES(1); break;

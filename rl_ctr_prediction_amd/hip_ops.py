@@ -867,18 +867,22 @@ def adam_deferred_rows(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "Sparse
 def adam_deferred_entries(emb, m_emb, v_emb, lin, m_lin, v_lin, last, plan: "SparsePlanBuffers",
                           vals: torch.Tensor, vals_lin: torch.Tensor | None, step: int,
                           table: AdamStepTable, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                          skip_row: int = -1, step_dev=None, out=None, out_lin=None) -> None:
+                          skip_row: int = -1, step_dev=None, out=None, out_lin=None,
+                          run_len: int = 0) -> None:
     """The owner side of a row-sharded step in one launch (ctr_adam_deferred_entries): each
     unique row of `plan` (over the received entries) stepped with the sequential sum of its
-    entries' vals / vals_lin; skip_row left alone."""
+    entries' vals / vals_lin; skip_row left alone. run_len > 0: vals is the chunked exchange
+    buffer (shard_rows_pack's layout, rows_chunk(run_len, K, lin) floats per chunk)."""
     V, K = emb.shape
     _f32(vals, "vals")
-    if vals.dim() != 2 or vals.shape[1] != K:
+    chunk = rows_chunk(run_len, K, lin is not None) if run_len else 0
+    if run_len == 0 and (vals.dim() != 2 or vals.shape[1] != K):
         raise ValueError(f"adam_deferred_entries: vals must be [entries, {K}]")
     tab = table.ensure(max(step, 1))
     lib.ctr_adam_deferred_entries(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin),
                                   V, K, _p(last), plan.struct(), _p(vals), _p(vals_lin),
-                                  int(skip_row), max(int(step), 1), _p(step_dev), _p(tab),
+                                  int(run_len), int(chunk), int(skip_row), max(int(step), 1),
+                                  _p(step_dev), _p(tab),
                                   float(betas[0]), float(betas[1]), float(eps),
                                   float(weight_decay), _p(out), _p(out_lin), _stream())
 

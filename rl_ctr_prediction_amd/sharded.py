@@ -654,8 +654,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         hip_ops.shard_rows_pack(b.grad_rows, b.grad_lin if has_lin else None, C, xb.counts,
                                 xb.offsets, out=xb.g_out)
         alltoall_equal(xb.g_recv, xb.g_out, self.group, force=f)
-        hip_ops.shard_rows_unpack(xb.g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
-                                  xb.glin_in if has_lin else None)
+        if not self._owner_direct:  # the owners' chunked sums read (source, position) rows
+            hip_ops.shard_rows_unpack(xb.g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
+                                      xb.glin_in if has_lin else None)
         self._span("exchange", t)
         # 5. the owners' sums and Adam here, beside the weight-gradient stream (dW0 ...);
         # only the dense all-reduce and the dense Adam wait for it (6.)
@@ -665,14 +666,14 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             # padding target) is skipped
             t = self._mark("scatter")
             hip_ops.adam_deferred_entries(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
-                                          self.v_w, self.last, xb.gplan, xb.g_in,
-                                          xb.glin_in if has_lin else None, step_hint,
+                                          self.v_w, self.last, xb.gplan, xb.g_recv, None,
+                                          step_hint,
                                           self.step_table, self.betas, self.eps,
                                           self.weight_decay, skip_row=Vo - 1,
                                           step_dev=self.step_cur,
                                           out=xb.g_rows if self.keep_grads else None,
                                           out_lin=xb.g_lin if self.keep_grads and has_lin
-                                          else None)
+                                          else None, run_len=C)
             self._span("scatter", t)
         elif self.fuse_apply and self.K >= self.fuse_apply_min_k:
             # the owners' row sums with each row's deferred Adam step applied where its sum

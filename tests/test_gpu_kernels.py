@@ -820,7 +820,8 @@ def test_shard_rows_lin_exchange_layout(cuda, n, C, K, lin):
 def test_adam_deferred_entries_equals_sums_then_rows(cuda, K, lin):
     """ctr_adam_deferred_entries (the row-sharded owner: each row's entries summed straight,
     then replayed + stepped) == numpy's sequential fp32 sums in plan order, and the table after
-    it == ctr_adam_deferred_rows with grad_rows = those sums, bitwise; skip_row untouched."""
+    it == ctr_adam_deferred_rows with grad_rows = those sums, bitwise; the same read from the
+    chunked exchange layout (run_len = C); skip_row untouched."""
     from rl_ctr_prediction_amd import hip_ops as H
     rng = np.random.default_rng(K)
     Vo, n, C = 3000, 4, 700
@@ -869,6 +870,19 @@ def test_adam_deferred_entries_equals_sums_then_rows(cuda, K, lin):
             acc = (acc + vals[x]).astype(np.float32)
             accl = np.float32(accl + vlin[x])
         want[u], want_l[u] = acc, accl
+    # the same from the exchange's chunked receive buffer (run_len = C): bitwise
+    chunk = H.rows_chunk(C, K, lin)
+    buf = np.zeros((n, chunk), np.float32)
+    for j in range(n):
+        buf[j, :C * K] = vals[j * C:(j + 1) * C].reshape(-1)
+        if lin:
+            buf[j, C * K:C * K + C] = vlin[j * C:(j + 1) * C]
+    cst = state()
+    H.adam_deferred_entries(*cst, plan, d(buf.reshape(-1)), None, step, tab, weight_decay=1e-5,
+                            skip_row=spare, run_len=C)
+    for x, y in zip(a, cst):
+        if x is not None:
+            assert torch.equal(x, y)
     live = urows != spare
     got = sums[:U].cpu().numpy()
     assert np.array_equal(got[live], want[live])
