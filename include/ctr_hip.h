@@ -323,6 +323,17 @@ int ctr_shard_rows_pack(const float* rows, const float* lin, int K, int64_t capa
 int ctr_shard_rows_unpack(const float* in, int K, int64_t capacity, int64_t chunk, int n_shards,
                           const int32_t* counts, const int32_t* offsets, float* rows, float* lin,
                           ctr_stream_t stream);
+/* ctr_shard_row_grads: a row-sharded requester's per-row gradient sums (ctr_fm_embedding_grad
+ * when gz != NULL, else ctr_segment_sum_rows over vals without linear sums) written straight
+ * into the exchange chunks of ctr_shard_rows_pack's layout: unique row u of run j (the last
+ * run with run_offsets[j] <= u) goes to row u - run_offsets[j] of chunk j, its linear sum
+ * after the chunk's run_len rows (lin != 0). Rows past a run's count are not written (the
+ * owner's spare row takes them). K % 4 == 0, 16-B aligned buffers. */
+int ctr_shard_row_grads(const ctr_sparse_plan* plan, int F, int K, const float* emb,
+                        const float* gz, const float* sum_e, const float* dx, const float* vals,
+                        int lin, int n_runs, const int32_t* run_offsets, int64_t run_len,
+                        int64_t chunk, float* out_chunks, void* ws, int64_t ws_bytes,
+                        ctr_stream_t stream);
 int ctr_sparse_plan_build(const void* idx, int idx_type, int64_t V, const ctr_sparse_plan* plan,
                           void* ws, int64_t ws_bytes, int32_t* err_flag, ctr_stream_t stream);
 /* The same plan (bit-identical) for ids laid out as a [S/F][F] matrix (slot s = b*F + f: the

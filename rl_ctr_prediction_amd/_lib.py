@@ -167,6 +167,8 @@ SIGNATURES = {
     "ctr_adam_deferred_entries": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _plan_p,
                                          _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _f64, _f64,
                                          _f64, _f64, _vp, _vp, _vp]),
+    "ctr_shard_row_grads": (_i32, [_plan_p, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp,
+                                   _i64, _i64, _vp, _vp, _i64, _vp]),
     "ctr_shard_gather_rows": (_i32, [_vp, _vp, _i32, _vp, _i32, _i64, _i64, _vp, _vp]),
     "ctr_shard_rows_pack": (_i32, [_vp, _vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp]),
     "ctr_shard_rows_unpack": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp]),

@@ -85,12 +85,29 @@ struct SegArgs {
   const int32_t* step_ptr;
   const float* tab;
   AdamHP hp;
+  // row-sharded requester (map_n > 0): row u's sum goes straight into its owner's exchange
+  // chunk — run j = the last with map_off[j] <= u, row u - map_off[j] of chunk j (map_chunk
+  // floats from out), its linear sum after the chunk's map_C rows (map_lin)
+  int map_n;
+  bool map_lin;
+  const int32_t* map_off;
+  int64_t map_C, map_chunk;
 };
 
 // a completed row sum: written out (and the rowmap entry of the dense-mode optimizer)
 template <typename VT>
 __device__ __forceinline__ void seg_emit(const SegArgs& a, int64_t u, int c, bool col,
                                          const VT& acc, float accl) {
+  if (a.map_n > 0) {
+    int j = 0;
+    while (j + 1 < a.map_n && u >= a.map_off[j + 1]) ++j;
+    const int64_t i = u - a.map_off[j];
+    float* const base = static_cast<float*>(a.out) + j * a.map_chunk;
+    if (col) reinterpret_cast<VT*>(base)[i * a.KV + c] = acc;
+    if (c == 0 && a.map_lin)
+      base[a.map_C * a.KV * (int64_t)(sizeof(VT) / sizeof(float)) + i] = accl;
+    return;
+  }
   if (col) static_cast<VT*>(a.out)[u * a.KV + c] = acc;
   if (c == 0) {
     if (a.out_lin) a.out_lin[u] = accl;
@@ -562,6 +579,43 @@ extern "C" int ctr_segment_sum_rows(const ctr_sparse_plan* plan, int K, const fl
   a.vals_lin = vals_lin;
   const bool al = ((uintptr_t)vals | (uintptr_t)out | (uintptr_t)ws) % 16 == 0;
   return launch_seg(a, K, MODE_VALS, as_stream(stream), al);
+}
+
+extern "C" int ctr_shard_row_grads(const ctr_sparse_plan* plan, int F, int K, const float* emb,
+                                   const float* gz, const float* sum_e, const float* dx,
+                                   const float* vals, int lin, int n_runs,
+                                   const int32_t* run_offsets, int64_t run_len, int64_t chunk,
+                                   float* out_chunks, void* ws, int64_t ws_bytes,
+                                   ctr_stream_t stream) {
+  CTR_REQUIRE(plan_ok(plan), "ctr_shard_row_grads: incomplete plan");
+  CTR_REQUIRE(K > 0 && K % 4 == 0 && out_chunks && run_offsets && n_runs > 0 && run_len > 0,
+              "ctr_shard_row_grads: bad arguments");
+  CTR_REQUIRE(chunk % 4 == 0 && chunk >= run_len * K + (lin ? run_len : 0),
+              "ctr_shard_row_grads: chunk must hold run_len rows (+ their linear sums)");
+  CTR_REQUIRE(gz ? (F > 0 && emb && sum_e) : (vals && !lin),
+              "ctr_shard_row_grads: FM mode needs emb / gz / sum_e; vals mode has no linear sums");
+  if (plan->S == 0) return CTR_OK;
+  SegArgs a;
+  int rc = seg_prepare(a, plan, K, out_chunks, nullptr, nullptr, ws, ws_bytes);
+  if (rc != CTR_OK) return rc;
+  a.map_n = n_runs;
+  a.map_lin = lin != 0;
+  a.map_off = run_offsets;
+  a.map_C = run_len;
+  a.map_chunk = chunk;
+  const bool al = ((uintptr_t)emb | (uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)vals |
+                   (uintptr_t)out_chunks | (uintptr_t)ws) % 16 == 0;
+  CTR_REQUIRE(al, "ctr_shard_row_grads: 16-B aligned buffers required");
+  if (gz) {
+    a.F = F;
+    a.gz = gz;
+    a.sum_e = sum_e;
+    a.dx = dx;
+    a.emb = emb;
+    return launch_seg(a, K, MODE_FM, as_stream(stream), true);
+  }
+  a.vals = vals;
+  return launch_seg(a, K, MODE_VALS, as_stream(stream), true);
 }
 
 extern "C" int ctr_rows_to_dense(const ctr_sparse_plan* plan, int K, const float* grad_rows,

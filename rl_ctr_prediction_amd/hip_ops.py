@@ -730,6 +730,26 @@ def _deferred_table(emb, m_emb, v_emb, lin, m_lin, v_lin, last):
     return DeferredTable(_p(emb), _p(m_emb), _p(v_emb), _p(lin), _p(m_lin), _p(v_lin), _p(last))
 
 
+def shard_row_grads(plan: SparsePlanBuffers, capacity: int, offsets: torch.Tensor,
+                    out: torch.Tensor, *, K: int, F: int = 0, emb=None, gz=None, sum_e=None,
+                    dx=None, vals=None, lin: bool = False) -> torch.Tensor:
+    """A row-sharded requester's per-row gradient sums written straight into the exchange
+    chunks (ctr_shard_row_grads; the layout of shard_rows_pack): FM mode (gz: the FM / DeepFM
+    slot gradients over the compact table emb) or vals mode (IPNN's per-slot gradients)."""
+    _f32(out, "out")
+    n = offsets.numel()
+    chunk = rows_chunk(capacity, K, lin)
+    if out.numel() < n * chunk:
+        raise ValueError(f"shard_row_grads: out needs {n * chunk} floats")
+    if offsets.dtype != torch.int32:
+        raise TypeError("shard_row_grads: offsets must be int32")
+    ws = _seg_ws(plan, K)
+    lib.ctr_shard_row_grads(plan.struct(gz is not None), int(F), int(K), _p(emb), _p(gz),
+                            _p(sum_e), _p(dx), _p(vals), int(bool(lin)), n, _p(offsets),
+                            int(capacity), chunk, _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
 def fm_embedding_grad_adam(plan: SparsePlanBuffers, F: int, gz, sum_e, dx, table, step_dev,
                            step_table: "AdamStepTable", step: int, betas=(0.9, 0.999), eps=1e-8,
                            weight_decay=0.0, grad_rows=None, grad_lin=None,

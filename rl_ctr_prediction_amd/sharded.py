@@ -65,6 +65,7 @@ class _XBufs:
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         NC = n * C
+        self.C = C
         self.chunk = hip_ops.rows_chunk(C, K, lin)
         self.send_ids, self.recv_ids = torch.empty(NC, **i32), torch.empty(NC, **i32)
         self.counts, self.offsets = torch.empty(n, **i32), torch.empty(n, **i32)
@@ -162,6 +163,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # owners sum their received entries (<= N per row) straight and apply in one launch;
         # CTR_OWNER_DIRECT=0: the chunked segmented sums with the fused apply (A/B)
         self._owner_direct = os.environ.get("CTR_OWNER_DIRECT", "1") != "0"
+        # requesters write their row sums straight into the exchange chunks (the padding rows
+        # past each run are left unwritten: only the direct owner pass, which skips the spare
+        # row they map to, may read them); CTR_GRADS_TO_CHUNKS=0: compact sums + pack (A/B)
+        self._grads_to_chunks = (self._owner_direct and
+                                 os.environ.get("CTR_GRADS_TO_CHUNKS", "1") != "0")
         self._slot2u = None
         self._counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
         # the plans (and per-owner counts / run maxima) are built on the plan stream, ahead
@@ -647,12 +653,17 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 3. forward + backward over the compact table
         ids = plan.slot_to_unique(out=xb.slot2u)[:B * F].view(B, F)
         T = xb.table
-        gz = self._sharded_fwd_bwd(ids, y, b, T, T_lin, bias, mean_div, F)
+        self._xb_cur = xb  # the row sums go straight into xb.g_out's chunks (_sharded_fwd_bwd)
+        try:
+            gz = self._sharded_fwd_bwd(ids, y, b, T, T_lin, bias, mean_div, F)
+        finally:
+            self._xb_cur = None
         # 4. gradients (with the linear ones) to the owners in one all-to-all, then every
         # source's chunk into the (source, position) order the owner plan indexes
         t = self._mark("exchange")
-        hip_ops.shard_rows_pack(b.grad_rows, b.grad_lin if has_lin else None, C, xb.counts,
-                                xb.offsets, out=xb.g_out)
+        if not self._grads_to_chunks or self.keep_grads:  # keep_grads: the compact sums stay
+            hip_ops.shard_rows_pack(b.grad_rows, b.grad_lin if has_lin else None, C, xb.counts,
+                                    xb.offsets, out=xb.g_out)
         alltoall_equal(xb.g_recv, xb.g_out, self.group, force=f)
         if not self._owner_direct:  # the owners' chunked sums read (source, position) rows
             hip_ops.shard_rows_unpack(xb.g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
@@ -729,7 +740,17 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         else:
             gz = self._deepfm_forward_backward(ids, y, b, T, T_lin, bias, mean_div)
         t = self._mark("scatter")
-        if self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
+        xb = getattr(self, "_xb_cur", None)
+        if xb is not None and self._grads_to_chunks and not self.keep_grads:
+            # the row sums straight into the exchange chunks (no compact sums + pack pass)
+            if self.kind == "IPNN":
+                hip_ops.shard_row_grads(b.plan, xb.C, xb.offsets, xb.g_out, K=self.K,
+                                        vals=b.dslot)
+            else:
+                hip_ops.shard_row_grads(b.plan, xb.C, xb.offsets, xb.g_out, K=self.K, F=F, emb=T,
+                                        gz=gz, sum_e=b.fm.sum_e, dx=b.dx,
+                                        lin=T_lin is not None)
+        elif self.kind == "IPNN":  # per-slot gradients (through the pair products) summed per row
             hip_ops.segment_sum_rows(b.plan, b.dslot, out=b.grad_rows)
         else:
             hip_ops.fm_embedding_grad(b.plan, F, T, gz, b.fm.sum_e, b.dx, None,

@@ -900,3 +900,45 @@ def test_adam_deferred_entries_equals_sums_then_rows(cuda, K, lin):
             continue
         assert torch.equal(x[rows_live], y[rows_live])
     assert torch.equal(a[0][spare], d(E0)[spare]) and int(a[-1][spare]) == last0[spare]
+
+
+@pytest.mark.parametrize("mode", ["fm", "vals"])
+def test_shard_row_grads_into_chunks(cuda, mode):
+    """ctr_shard_row_grads == the compact per-row sums (ctr_fm_embedding_grad compact /
+    ctr_segment_sum_rows) then ctr_shard_rows_pack, bitwise on every run row and linear sum."""
+    from rl_ctr_prediction_amd import hip_ops as H
+    rng = np.random.default_rng(3 if mode == "fm" else 4)
+    B, F, K, V = 512, 6, 16, 5000
+    x = torch.tensor(rng.integers(0, V, size=(B, F)), device=cuda)
+    plan = H.SparsePlanBuffers(B * F, cuda).build(x, V)
+    U = plan.num_unique_host()
+    n = 3
+    cuts = np.sort(rng.choice(np.arange(1, U), size=n - 1, replace=False))
+    counts = np.diff(np.concatenate([[0], cuts, [U]])).astype(np.int32)
+    offsets = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+    C = int(counts.max()) + 5
+    d = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    lin = mode == "fm"
+    chunk = H.rows_chunk(C, K, lin)
+    got = torch.zeros(n * chunk, device=cuda)
+    if mode == "fm":
+        T = d(rng.standard_normal((U, K)).astype(np.float32))
+        gz = d(rng.standard_normal(B).astype(np.float32))
+        sum_e = d(rng.standard_normal((B, K)).astype(np.float32))
+        dx = d(rng.standard_normal((B, F * K)).astype(np.float32))
+        gr, gl = H.fm_embedding_grad(plan, F, T, gz, sum_e, dx, compact=True)
+        H.shard_row_grads(plan, C, d(offsets), got, K=K, F=F, emb=T, gz=gz, sum_e=sum_e, dx=dx,
+                          lin=True)
+    else:
+        vals = d(rng.standard_normal((B * F, K)).astype(np.float32))
+        gr, gl = H.segment_sum_rows(plan, vals)
+        H.shard_row_grads(plan, C, d(offsets), got, K=K, vals=vals)
+    want = torch.zeros(n * chunk, device=cuda)
+    H.shard_rows_pack(gr[:max(U, 1)].contiguous(), gl[:max(U, 1)].contiguous() if lin else None,
+                      C, d(counts), d(offsets), out=want)
+    g, w = got.view(n, chunk), want.view(n, chunk)
+    for j in range(n):
+        c = int(counts[j])
+        assert torch.equal(g[j, :c * K], w[j, :c * K]), j
+        if lin:
+            assert torch.equal(g[j, C * K:C * K + c], w[j, C * K:C * K + c]), j
