@@ -84,7 +84,6 @@ class _XBufs:
         else:
             self.lin_table = self.glin_in = self.g_lin = None
         self.gplan = hip_ops.SparsePlanBuffers(NC, dev)
-        self.slot2u = torch.empty(max(S, 1), **i32)
 
 
 def _host_span(acc: dict, key: str, t0: float) -> float:
@@ -526,6 +525,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if slot.cap is None:
             slot.cap = torch.zeros(1, dtype=torch.int64, device=self.device)
             slot.counts = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+            slot.slot2u = torch.empty(max(slot.ids.numel(), 1), dtype=torch.int32,
+                                      device=self.device)
         if slot.plan_graph is not None and self.timing is None:
             slot.plan_graph.replay()
         else:
@@ -540,6 +541,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
 
     def _plan_launch(self, slot: InputSlot) -> None:
         slot.plan.build(slot.ids, self.V, err_flag=self.err)
+        # the forward's ids over the compact table, ahead with the plan (off the step's path)
+        slot.plan.slot_to_unique(out=slot.slot2u)
         if self.world_size <= 15:  # the counts and their maximum in one launch
             slot.plan.shard_counts(self.shard_rows, self.world_size, out=slot.counts,
                                    max_out=slot.cap)
@@ -651,7 +654,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         T_lin = xb.lin_table.view(-1, 1) if has_lin else None
         self._span("exchange", t)
         # 3. forward + backward over the compact table
-        ids = plan.slot_to_unique(out=xb.slot2u)[:B * F].view(B, F)
+        ids = slot.slot2u[:B * F].view(B, F)  # built with the slot's plan (_plan_launch)
         T = xb.table
         self._xb_cur = xb  # the row sums go straight into xb.g_out's chunks (_sharded_fwd_bwd)
         try:

@@ -108,7 +108,7 @@ class InputSlot:
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
     __slots__ = ("shape", "index", "ids", "y", "y_key", "plan", "ev", "plan_graph",
-                 "done_ev", "stream_i", "stage_stream", "cap", "counts")
+                 "done_ev", "stream_i", "stage_stream", "cap", "counts", "slot2u")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -123,6 +123,7 @@ class InputSlot:
         self.stream_i = 0
         self.stage_stream = None  # the plan stream its last staging ran on
         self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
+        self.slot2u = None  # ShardedCTRTrainer: slot -> unique ordinal, built with the plan
 
 
 @dataclass
