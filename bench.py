@@ -818,6 +818,35 @@ def main():
             "unique_rows_per_batch": U, "slots_per_batch": S},
         "cpu_baseline": None,
     }
+    if isinstance(trainer, ShardedCTRTrainer):
+        # the row-sharded exchange as it ran: this rank's shard, the agreed capacity C (rows
+        # per (requester, owner) pair) and the bytes each collective moves per step
+        from rl_ctr_prediction_amd import hip_ops as H
+        C = int(trainer._cap)
+        lin = trainer.w_tab is not None
+        chunk = H.rows_chunk(C, K, lin)
+        dense_n = int(trainer.flat_grad.numel())
+        result["sharding"] = {
+            "shard_rows": int(trainer.V_tab), "row_range": [int(trainer.row_lo),
+                                                           int(trainer.row_hi)],
+            "capacity_rows": C, "chunk_floats": int(chunk),
+            "exchange_bytes_per_step": {
+                "ids_alltoall": world * C * 4, "rows_alltoall": world * chunk * 4,
+                "grads_alltoall": world * chunk * 4,
+                "dense_allreduce": (dense_n + 1) * 4},
+            "unique_rows_this_batch": U,
+            "padding_frac": 1.0 - U / max(1, world * C),
+            "backend": dist.get_backend() if world > 1 else None,
+            "graphs": bool(trainer.use_graphs and trainer._graph_ok),
+            "captures": getattr(trainer, "captures", None),
+            "host_reads_blocking": trainer.cap_blocking, "host_reads": trainer.cap_reads}
+        if world > 1:  # every rank's shard and capacity, gathered to rank 0 for the line
+            mine = [trainer.V_tab, trainer.row_lo, trainer.row_hi, C, U]
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+            result["sharding"]["per_rank"] = [
+                {"rank": r, "shard_rows": a[0], "row_range": [a[1], a[2]], "capacity_rows": a[3],
+                 "unique_rows_last_batch": a[4]} for r, a in enumerate(allr)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(cfg, host_batches)

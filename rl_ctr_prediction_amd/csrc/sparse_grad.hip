@@ -102,6 +102,10 @@ __device__ __forceinline__ void seg_emit(const SegArgs& a, int64_t u, int c, boo
     int j = 0;
     while (j + 1 < a.map_n && u >= a.map_off[j + 1]) ++j;
     const int64_t i = u - a.map_off[j];
+    // a run longer than the capacity (flagged CTR_EFLAG_CAPACITY by shard_pack_ids, raised
+    // by the host's check) must not spill into the next owner's chunk: its rows past C are
+    // dropped here, as the pack / unpack kernels clamp to min(count, C)
+    if (i >= a.map_C) return;
     float* const base = static_cast<float*>(a.out) + j * a.map_chunk;
     if (col) reinterpret_cast<VT*>(base)[i * a.KV + c] = acc;
     if (c == 0 && a.map_lin)

@@ -10,6 +10,7 @@ device-resident and each slice is a view fed to the fused HIP step; everything e
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import pretrain_main as _pm
@@ -25,7 +26,9 @@ def get_dataset(datapath, dataset_name, campaign_id):
     (pretrain_main_2.py:47-62)."""
     train_fm, _, test_fm, field_nums, feature_nums = _pm.get_dataset(datapath, dataset_name,
                                                                      campaign_id)
-    return train_fm, torch.as_tensor(train_fm, dtype=torch.int64), test_fm, field_nums, feature_nums
+    # copied first: train_fm may be a read-only memory map of the binary batch cache
+    return (train_fm, torch.from_numpy(np.array(train_fm, dtype=np.int64)), test_fm, field_nums,
+            feature_nums)
 
 
 def train(model, optimizer, train_data, loss, device, len_train, batch):
@@ -45,7 +48,8 @@ def main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch, l
 
     def epoch_fn(model, trainer, train_fm, loss, dev, bs):
         if "data" not in cache:  # the LongTensor of get_dataset, moved once
-            cache["data"] = torch.as_tensor(train_fm, dtype=torch.int64).to(dev)
+            # copied first: a read-only memory map is not handed to torch as it is
+            cache["data"] = torch.from_numpy(np.array(train_fm, dtype=np.int64)).to(dev)
         return train(model, trainer, cache["data"], loss, dev, len(train_fm), bs)
 
     return _pm.main(data_path, dataset_name, campaign_id, latent_dims, model_name, epoch,

@@ -106,7 +106,9 @@ class _Agreement:
         self.dev = torch.empty(n, dtype=torch.int64, device=dev)
         self.host = torch.empty(n, dtype=torch.int64, pin_memory=True)
         self.ev = torch.cuda.Event()
-        self.keys = [None] * n  # this rank's batch (ids key) behind each entry
+        # this rank's batch behind each entry: (ids key, staging generation of its slot), so
+        # a slot re-staged after the agreement measured it is never sized by that agreement
+        self.keys = [None] * n
         self.call = None        # the step() call that issued it
 
 
@@ -192,6 +194,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._cap_stream = self._new_stream()
         self._agree = [_Agreement(self.LOOKAHEAD, self.device) for _ in range(4)]
         self._calls = 0           # step() calls so far (the index of the next step)
+        self._stage_gen = 0       # slot stagings so far (InputSlot.gen)
+        self._plan_graphs_ok = True
         self._agree_last_ev = None
         self._now = None          # the blocking agreement's record (no lookahead)
         self.cap_reads = 0        # host reads of an agreement (one per step)
@@ -234,6 +238,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             self._spare[id(p)] = buf
         model.to(device)
         self._sharded_params = tabs
+        if E.device.type == "cuda" or device.type == "cuda":
+            # the full table's device block goes back to the device, not to this process's
+            # cache (ranks that share a GPU — the gloo rehearsal of N > 1 on one device —
+            # would otherwise each hold a full table's worth of cached memory)
+            torch.cuda.empty_cache()
         if self.world_size > 1:
             ref = weakref.ref(self)
 
@@ -364,7 +373,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 ahead.append((n, k) if ok else None)
         slot = self._staged.pop(xkey, None)
         if self._staged:
-            keep = {a[1] for a in ahead if a is not None}
+            # batches staged ahead stay staged while next_x names them or an agreement
+            # already issued covers them (call t-1's entry for step t+1): their plans are
+            # what those agreements measured
+            keep = {a[1] for a in ahead if a is not None} | self._agreed_keys(t_call)
             for k in [k for k in self._staged if k not in keep]:
                 main.wait_event(self._staged.pop(k).ev)
         todo = [a for a in ahead if a is not None and a[1] not in self._staged]
@@ -429,6 +441,14 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     # of the GPU. A step whose capacity nobody agreed ahead (no lookahead on some rank: every
     # rank sees the same UNKNOWN_RUN) agrees in the step itself (_agree_now).
 
+    def _agreed_keys(self, t: int) -> set:
+        """The ids keys of the batches an issued agreement covers beyond step t (call t-1's
+        entries past step t)."""
+        a = self._agree[(t - 1) % 4]
+        if a.call != t - 1:
+            return set()
+        return {k[0] for k in a.keys[1:] if k is not None}
+
     def _capacity(self, t: int, xkey, slot: InputSlot) -> int:
         """The agreed capacity need (largest run) of step t."""
         for a, j in ((self._agree[(t - 2) % 4], 1), (self._agree[(t - 1) % 4], 0)):
@@ -438,14 +458,18 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             v = int(a.host[j])
             if v == UNKNOWN_RUN:
                 continue
-            if a.keys[j] == xkey:
+            key = a.keys[j]
+            if key is not None and key == (xkey, slot.gen):
                 self.cap_reads += 1
                 return v
             if self._coll:  # the other ranks sized this step by that agreement
+                what = ("a batch re-staged after its capacity was agreed (the slot the "
+                        "agreement measured was dropped)" if key is not None and key[0] == xkey
+                        else "a batch other than the one passed as next_x for it")
                 raise RuntimeError(
-                    "ShardedCTRTrainer: step trained on a batch other than the one passed as "
-                    "next_x for it; with collectives every rank sized this step's exchange by "
-                    "the agreed capacity of the announced batches (pass next_x=None instead)")
+                    f"ShardedCTRTrainer: step trained on {what}; with collectives every rank "
+                    "sized this step's exchange by the agreed capacity of the announced "
+                    "batches (pass next_x=None instead)")
             break  # one process: agree on this batch now
         return self._agree_now(slot)
 
@@ -479,7 +503,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         for j in range(self.LOOKAHEAD):
             e = ahead[j] if j < len(ahead) else None
             s = self._staged.get(e[1]) if e is not None else None
-            a.keys[j] = e[1] if s is not None else None
+            a.keys[j] = (e[1], s.gen) if s is not None else None
             if s is not None:
                 cs.wait_event(s.ev)
                 known.append((j, s))
@@ -502,6 +526,8 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         """On the plan stream, after everything enqueued before this step and after the last
         agreement (which reads staged slots' run maxima): ids into slot s, its plan."""
         ps = self._plan_stream
+        self._stage_gen += 1
+        s.gen = self._stage_gen
         ps.wait_event(ev_start)
         if self._agree_last_ev is not None:
             ps.wait_event(self._agree_last_ev)
@@ -531,11 +557,24 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             slot.plan_graph.replay()
         else:
             self._plan_launch(slot)
-            if self.use_graphs and self.timing is None:
+            if self.use_graphs and self.timing is None and self._plan_graphs_ok:
                 g = torch.cuda.CUDAGraph()
-                with graph_capture(g, pool=live_pool(self), stream=torch.cuda.current_stream()):
-                    self._plan_launch(slot)  # captured, not executed
-                slot.plan_graph = g
+                # with collectives the process group's watchdog thread queries its events
+                # while this thread captures: a thread-local capture, as the step's
+                mode = "thread_local" if self._coll else "global"
+                try:
+                    with graph_capture(g, pool=live_pool(self), stream=torch.cuda.current_stream(),
+                                       capture_error_mode=mode):
+                        self._plan_launch(slot)  # captured, not executed
+                except RuntimeError as e:
+                    if not self._coll:
+                        raise
+                    warnings.warn(f"ShardedCTRTrainer: plan graph capture failed ({e}); "
+                                  "building the plans eagerly")
+                    torch.cuda.synchronize(self.device)
+                    self._plan_graphs_ok = False
+                else:
+                    slot.plan_graph = g
         slot.ev = self._slot_event(slot)
         slot.ev.record()
 

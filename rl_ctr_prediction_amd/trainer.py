@@ -108,7 +108,7 @@ class InputSlot:
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
     __slots__ = ("shape", "index", "ids", "y", "y_key", "plan", "ev", "plan_graph",
-                 "done_ev", "stream_i", "stage_stream", "cap", "counts", "slot2u")
+                 "done_ev", "stream_i", "stage_stream", "cap", "counts", "slot2u", "gen")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -124,6 +124,7 @@ class InputSlot:
         self.stage_stream = None  # the plan stream its last staging ran on
         self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
         self.slot2u = None  # ShardedCTRTrainer: slot -> unique ordinal, built with the plan
+        self.gen = 0  # ShardedCTRTrainer: staging generation (which contents the plan measured)
 
 
 @dataclass

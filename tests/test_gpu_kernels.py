@@ -942,3 +942,53 @@ def test_shard_row_grads_into_chunks(cuda, mode):
         assert torch.equal(g[j, :c * K], w[j, :c * K]), j
         if lin:
             assert torch.equal(g[j, C * K:C * K + c], w[j, C * K:C * K + c]), j
+
+
+@pytest.mark.parametrize("mode", ["fm", "vals"])
+def test_shard_row_grads_capacity_overflow_stays_in_chunk(cuda, mode):
+    """A run longer than the capacity C (the case shard_pack_ids flags with
+    CTR_EFLAG_CAPACITY) writes its first C rows and nothing past its own chunk: every row and
+    linear slot beyond min(count, C) keeps its sentinel, and the first min(count, C) rows are
+    the pack kernel's (which clamps the same way)."""
+    from rl_ctr_prediction_amd import hip_ops as H
+    rng = np.random.default_rng(11 if mode == "fm" else 12)
+    B, F, K, V = 256, 6, 16, 3000
+    x = torch.tensor(rng.integers(0, V, size=(B, F)), device=cuda)
+    plan = H.SparsePlanBuffers(B * F, cuda).build(x, V)
+    U = plan.num_unique_host()
+    n = 3
+    counts = np.array([U // 2, U // 4, U - U // 2 - U // 4], np.int32)
+    offsets = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+    C = int(counts[1]) + 3  # run 0 (and maybe run 2) overflow
+    assert counts.max() > C
+    d = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    lin = mode == "fm"
+    chunk = H.rows_chunk(C, K, lin)
+    sentinel = 12345.0
+    got = torch.full((n * chunk,), sentinel, device=cuda)
+    if mode == "fm":
+        T = d(rng.standard_normal((U, K)).astype(np.float32))
+        gz = d(rng.standard_normal(B).astype(np.float32))
+        sum_e = d(rng.standard_normal((B, K)).astype(np.float32))
+        dx = d(rng.standard_normal((B, F * K)).astype(np.float32))
+        gr, gl = H.fm_embedding_grad(plan, F, T, gz, sum_e, dx, compact=True)
+        H.shard_row_grads(plan, C, d(offsets), got, K=K, F=F, emb=T, gz=gz, sum_e=sum_e, dx=dx,
+                          lin=True)
+    else:
+        vals = d(rng.standard_normal((B * F, K)).astype(np.float32))
+        gr, gl = H.segment_sum_rows(plan, vals)
+        H.shard_row_grads(plan, C, d(offsets), got, K=K, vals=vals)
+    torch.cuda.synchronize()
+    want = torch.zeros(n * chunk, device=cuda)
+    H.shard_rows_pack(gr[:U].contiguous(), gl[:U].contiguous() if lin else None, C, d(counts),
+                      d(offsets), out=want)
+    g, w = got.view(n, chunk), want.view(n, chunk)
+    for j in range(n):
+        m = min(int(counts[j]), C)
+        assert torch.equal(g[j, :m * K], w[j, :m * K]), j
+        assert bool((g[j, m * K:C * K] == sentinel).all()), j
+        if lin:
+            assert torch.equal(g[j, C * K:C * K + m], w[j, C * K:C * K + m]), j
+            assert bool((g[j, C * K + m:] == sentinel).all()), j
+        else:
+            assert bool((g[j, C * K:] == sentinel).all()), j
