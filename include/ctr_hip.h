@@ -306,6 +306,22 @@ int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t 
 int ctr_shard_runs_copy(const float* src, float* dst, int64_t width, int64_t capacity,
                         int n_shards, const int32_t* counts, const int32_t* offsets, int pack,
                         ctr_stream_t stream);
+/* Cyclic row sharding (ABI v12): global row r belongs to shard r % n_shards as its local row
+ * r / n_shards, so every shard owns rows of every feature field (the field-ordered vocabulary
+ * of the reference's encoders, creat_data.py / data_.py, puts the high-cardinality fields in
+ * the last row blocks: contiguous blocks leave one owner most of every batch's rows).
+ * ctr_shard_permute_ids: in place, ids[i] = (r % n_shards) * shard_rows + r / n_shards — the
+ *   space in which each shard's rows are one contiguous block [j*shard_rows, j*shard_rows+n_j),
+ *   n_j = ceil((V - j) / n_shards); ids outside [0, V) raise CTR_EFLAG_INDEX and map to
+ *   row 0. int64 or int32 ids (ids_is_64); the plan and the exchange then run on these ids.
+ * ctr_shard_pack_ids_layout: ctr_shard_pack_ids over permuted ids; cyclic != 0: each owner's
+ *   spare row is its cyclic row count n_j (blocks: as ctr_shard_pack_ids). */
+int ctr_shard_permute_ids(void* ids, int ids_is_64, int64_t count, int64_t V, int n_shards,
+                          int64_t shard_rows, int32_t* err_flag, ctr_stream_t stream);
+int ctr_shard_pack_ids_layout(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V,
+                              int n_shards, int cyclic, int64_t capacity, int32_t* send,
+                              int32_t* counts, int32_t* offsets, int32_t* err_flag,
+                              ctr_stream_t stream);
 /* The same exchange with each row's linear weight in the same message: the padded buffer is
  * n_shards chunks of `chunk` floats (chunk >= capacity*K + capacity, a multiple of 4), chunk j
  * = [capacity rows of K floats][capacity linear weights][padding]; lin == NULL: rows only.

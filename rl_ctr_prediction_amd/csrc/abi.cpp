@@ -18,7 +18,7 @@ void set_error(const char* fmt, ...) {
 
 }  // namespace ctr
 
-extern "C" int ctr_abi_version(void) { return 11; }
+extern "C" int ctr_abi_version(void) { return 12; }
 
 extern "C" const char* ctr_last_error(void) { return ctr::g_last_error; }
 

@@ -39,6 +39,10 @@ typedef float pf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
 
+#ifndef CTR_PL_PIPE
+#define CTR_PL_PIPE 0
+#endif
+
 struct PlaneSrc {
   const uint16_t* p;  // plane 0 (bf16 bits); planes `ps` elements apart
   int64_t ld;         // elements per storage row
@@ -429,6 +433,78 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   };
 
   constexpr int IPW = IPWA + IPWB;
+#if CTR_PL_PIPE
+  if constexpr (!A_RC && !B_RC && KS == 1) {
+    // Software-pipelined stage (both operands k-contiguous): the B fragments of 16-column
+    // group tn+1 are read while the MFMAs of group tn run, and the stage's LDS-DMA pieces
+    // for stage t+NS-1 are issued between the groups instead of in one burst at the
+    // barrier (the scheduler order is pinned by sched_group_barrier). The DMA is issued
+    // every iteration — past the last stage it re-loads the last stage into the ring slot
+    // nobody reads again — so the wait count is the constant IPW * (NS-2).
+    const int tlast = nt - 1;
+    auto issue_piece = [&](int j, int ts) {
+      char* st_ = smem + (ts % NS) * STAGE;
+      const int tsrc = min(ts, tlast);
+      if (j < IPWA)
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)SA.p + (int64_t)tsrc * stepA + offA[j]),
+                                         (CTR_LDS void*)(st_ + ldsA[j]), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)SB.p + (int64_t)tsrc * stepB + offB[j - IPWA]),
+                                         (CTR_LDS void*)(st_ + ldsB[j - IPWA]), 16, 0, 0);
+    };
+    if (nt > 0) {
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s)
+#pragma unroll
+        for (int j = 0; j < IPW; ++j) issue_piece(j, s);
+    }
+    for (int t = 0; t < nt; ++t) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * (NS - 2)) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* st = smem + (t % NS) * STAGE;
+      pbf16x8 af[TM][3], bf[2][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[i][p] = frag_kc_at(st + p * A_PL + aoff[i][0]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bf[0][p] = frag_kc_at(st + 3 * A_PL + p * B_PL + boff[0][0]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * TM + 3, 0);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int cb = tn & 1;
+        if (tn + 1 < TN) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            bf[cb ^ 1][p] = frag_kc_at(st + 3 * A_PL + p * B_PL + boff[tn + 1][0]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        }
+        // this group's share of the next stage's DMA pieces
+        const int j0 = (IPW * tn) / TN, j1 = (IPW * (tn + 1)) / TN;
+#pragma unroll
+        for (int j = 0; j < IPW; ++j)
+          if (j >= j0 && j < j1) {
+            issue_piece(j, t + NS - 1);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          pf32x4 v = lo[i][tn];
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[cb][1], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][2], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bf[cb][0], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][1], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[cb][0], v, 0, 0, 0);
+          lo[i][tn] = v;
+          acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][0], acc[i][tn], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 6 * TM, 0);
+      }
+    }
+  } else
+#endif
+  {
   // prologue: stages 0 .. NS-2 in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -448,6 +524,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
     asm volatile("" ::: "memory");
     if (t + NS - 1 < nt) CTR_PL_ISSUE(t + NS - 1);
     compute(t % NS);
+  }
   }
 #undef CTR_PL_ISSUE
   __syncthreads();  // every stage read before the epilogue reuses the LDS

@@ -795,7 +795,7 @@ __global__ __launch_bounds__(1024) void shard_counts_max_kernel(
 __global__ __launch_bounds__(256) void shard_pack_ids_kernel(
     const int32_t* __restrict__ unique_rows, const int32_t* __restrict__ num_unique,
     int64_t shard_rows, int64_t V, int64_t C, int32_t* __restrict__ send,
-    int32_t* __restrict__ counts, int32_t* __restrict__ offsets, int32_t* err) {
+    int32_t* __restrict__ counts, int32_t* __restrict__ offsets, int32_t* err, int cyc) {
   const int j = blockIdx.y;
   const int U = *num_unique;
   const int64_t base = (int64_t)j * shard_rows;
@@ -809,7 +809,10 @@ __global__ __launch_bounds__(256) void shard_pack_ids_kernel(
   }
   __syncthreads();
   const int lo = bounds[0], hi = bounds[1];
-  const int32_t dummy = (int32_t)max<int64_t>(0, min<int64_t>(shard_rows, V - base));
+  // the owner's spare row = its row count: blocks min(shard_rows, V - j*shard_rows),
+  // cyclic (n_shards < 0 passed as cyc) ceil((V - j) / n)
+  const int32_t dummy = cyc > 0 ? (int32_t)max<int64_t>(0, (V - j + cyc - 1) / cyc)
+                                : (int32_t)max<int64_t>(0, min<int64_t>(shard_rows, V - base));
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < C;
        i += (int64_t)gridDim.x * blockDim.x)
     send[(int64_t)j * C + i] = lo + i < hi ? (int32_t)(unique_rows[lo + i] - base) : dummy;
@@ -817,6 +820,28 @@ __global__ __launch_bounds__(256) void shard_pack_ids_kernel(
     counts[j] = hi - lo;
     offsets[j] = lo;
     if (hi - lo > C && err) atomicOr(err, (int32_t)CTR_EFLAG_CAPACITY);
+  }
+}
+
+// Cyclic row sharding: global row r is owned by shard r % n, as its local row r / n. The
+// batch's ids are mapped in place to r' = (r % n) * shard_rows + r / n, a space in which every
+// shard's rows are one contiguous block again (shard j: [j*shard_rows, j*shard_rows + n_j),
+// n_j = ceil((V - j) / n)), so the plan's ascending unique rows come out grouped by owner and
+// the exchange below runs unchanged. An id outside [0, V) raises CTR_EFLAG_INDEX and maps
+// to row 0 (nn.Embedding's IndexError, raised by the host's check_errors).
+template <typename T>
+__global__ __launch_bounds__(256) void shard_permute_ids_kernel(T* __restrict__ ids, int64_t count,
+                                                                int64_t V, int64_t n,
+                                                                int64_t shard_rows,
+                                                                int32_t* err) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = (int64_t)ids[i];
+    if (r < 0 || r >= V) {
+      if (err) atomicOr(err, (int32_t)CTR_EFLAG_INDEX);
+      r = 0;
+    }
+    ids[i] = (T)((r % n) * shard_rows + r / n);
   }
 }
 
@@ -1316,17 +1341,54 @@ extern "C" int ctr_ids_add(int32_t* ids, int64_t n, int32_t delta, ctr_stream_t 
   return CTR_OK;
 }
 
-extern "C" int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V,
-                                  int n_shards, int64_t capacity, int32_t* send, int32_t* counts,
-                                  int32_t* offsets, int32_t* err_flag, ctr_stream_t stream) {
+static int shard_pack_ids_impl(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V,
+                               int n_shards, int cyclic, int64_t capacity, int32_t* send,
+                               int32_t* counts, int32_t* offsets, int32_t* err_flag,
+                               ctr_stream_t stream) {
   CTR_REQUIRE(plan_ok(plan) && send && counts && offsets && shard_rows > 0 && n_shards > 0 &&
                   capacity > 0 && V > 0 && shard_rows * n_shards >= V,
               "ctr_shard_pack_ids: bad arguments");
   CTR_REQUIRE(shard_rows < (int64_t(1) << 31), "ctr_shard_pack_ids: shard too large");
   const dim3 grid((unsigned)std::min<int64_t>(ceil_div(capacity, 256), 1024), (unsigned)n_shards);
   hipLaunchKernelGGL(shard_pack_ids_kernel, grid, 256, 0, as_stream(stream), plan->unique_rows,
-                     plan->num_unique, shard_rows, V, capacity, send, counts, offsets, err_flag);
+                     plan->num_unique, shard_rows, V, capacity, send, counts, offsets, err_flag,
+                     cyclic ? n_shards : 0);
   CTR_LAUNCH_CHECK("shard_pack_ids_kernel");
+  return CTR_OK;
+}
+
+extern "C" int ctr_shard_pack_ids(const ctr_sparse_plan* plan, int64_t shard_rows, int64_t V,
+                                  int n_shards, int64_t capacity, int32_t* send, int32_t* counts,
+                                  int32_t* offsets, int32_t* err_flag, ctr_stream_t stream) {
+  return shard_pack_ids_impl(plan, shard_rows, V, n_shards, 0, capacity, send, counts, offsets,
+                             err_flag, stream);
+}
+
+extern "C" int ctr_shard_pack_ids_layout(const ctr_sparse_plan* plan, int64_t shard_rows,
+                                         int64_t V, int n_shards, int cyclic, int64_t capacity,
+                                         int32_t* send, int32_t* counts, int32_t* offsets,
+                                         int32_t* err_flag, ctr_stream_t stream) {
+  return shard_pack_ids_impl(plan, shard_rows, V, n_shards, cyclic, capacity, send, counts,
+                             offsets, err_flag, stream);
+}
+
+extern "C" int ctr_shard_permute_ids(void* ids, int ids_is_64, int64_t count, int64_t V,
+                                     int n_shards, int64_t shard_rows, int32_t* err_flag,
+                                     ctr_stream_t stream) {
+  CTR_REQUIRE(count >= 0 && (ids || count == 0) && V > 0 && n_shards > 0 && shard_rows > 0 &&
+                  shard_rows * n_shards >= V,
+              "ctr_shard_permute_ids: bad arguments");
+  CTR_REQUIRE(ids_is_64 || shard_rows * n_shards < (int64_t(1) << 31),
+              "ctr_shard_permute_ids: int32 ids cannot address the permuted space");
+  if (count == 0) return CTR_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(count, 256), 4096);
+  if (ids_is_64)
+    hipLaunchKernelGGL(shard_permute_ids_kernel<int64_t>, grid, 256, 0, as_stream(stream),
+                       static_cast<int64_t*>(ids), count, V, (int64_t)n_shards, shard_rows, err_flag);
+  else
+    hipLaunchKernelGGL(shard_permute_ids_kernel<int32_t>, grid, 256, 0, as_stream(stream),
+                       static_cast<int32_t*>(ids), count, V, (int64_t)n_shards, shard_rows, err_flag);
+  CTR_LAUNCH_CHECK("shard_permute_ids_kernel");
   return CTR_OK;
 }
 

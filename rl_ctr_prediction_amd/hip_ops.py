@@ -569,17 +569,33 @@ class SparsePlanBuffers:
 
 def shard_pack_ids(plan: SparsePlanBuffers, shard_rows: int, V: int, n_shards: int,
                    capacity: int, send: torch.Tensor, counts: torch.Tensor,
-                   offsets: torch.Tensor, err_flag: torch.Tensor | None = None) -> None:
+                   offsets: torch.Tensor, err_flag: torch.Tensor | None = None,
+                   cyclic: bool = False) -> None:
     """The plan's unique rows, per owner shard, into the padded exchange layout
     send[j*capacity + i] (owner-local ids; the owner's spare row past each run); counts /
-    offsets: int32[n_shards] (ctr_shard_pack_ids)."""
+    offsets: int32[n_shards] (ctr_shard_pack_ids). cyclic: the plan was built over
+    shard_permute_ids_ ids (each owner's spare row is then its cyclic row count)."""
     for t, n, k in ((send, "send", n_shards * capacity), (counts, "counts", n_shards),
                     (offsets, "offsets", n_shards)):
         _dev(t, n)
         if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() < k:
             raise ValueError(f"shard_pack_ids: {n} must be contiguous int32 of >= {k}")
-    lib.ctr_shard_pack_ids(plan.struct(), int(shard_rows), int(V), int(n_shards), int(capacity),
-                           _p(send), _p(counts), _p(offsets), _p(err_flag), _stream())
+    lib.ctr_shard_pack_ids_layout(plan.struct(), int(shard_rows), int(V), int(n_shards),
+                                  int(bool(cyclic)), int(capacity), _p(send), _p(counts),
+                                  _p(offsets), _p(err_flag), _stream())
+
+
+def shard_permute_ids_(ids: torch.Tensor, V: int, n_shards: int, shard_rows: int,
+                       err_flag: torch.Tensor | None = None) -> torch.Tensor:
+    """In place: global row ids r -> (r % n_shards) * shard_rows + r // n_shards, the cyclic
+    row-sharding space in which shard j's rows are one block (ctr_shard_permute_ids); ids
+    outside [0, V) raise CTR_EFLAG_INDEX in err_flag and map to row 0. int64 or int32."""
+    _dev(ids, "ids")
+    if ids.dtype not in (torch.int64, torch.int32) or not ids.is_contiguous():
+        raise TypeError("shard_permute_ids_: contiguous int64 / int32 ids expected")
+    lib.ctr_shard_permute_ids(_p(ids), int(ids.dtype == torch.int64), ids.numel(), int(V),
+                              int(n_shards), int(shard_rows), _p(err_flag), _stream())
+    return ids
 
 
 _STAGE_COPY = os.environ.get("CTR_STAGE_COPY", "1") != "0"  # A/B: the runtime's copies

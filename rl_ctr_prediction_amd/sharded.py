@@ -133,7 +133,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
     def __init__(self, model, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, process_group=None, seed: int | None = None,
                  count_group=None, device=None, exchange: str = "padded",
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, layout: str | None = None):
         """process_group: the ranks sharing the table (default: the world). count_group: a
         second communicator over the same ranks for the per-step capacity / counts
         agreement (it runs on the plan stream beside the data collectives). Default:
@@ -144,7 +144,15 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         capacity, the default) or "varsplit". force_collectives: at world size 1, send every
         exchange through the collectives of a one-rank process group (dist initialised,
         e.g. RCCL on one GPU) instead of local copies — the N > 1 launch sequence, RCCL
-        kernels and their graph capture included, on one device (tests)."""
+        kernels and their graph capture included, on one device (tests). layout: "cyclic"
+        (the default; CTR_SHARD_LAYOUT overrides) — global row r lives on rank r % N as its
+        local row r // N — or "blocks" — rank r owns the contiguous rows [r*Vs, (r+1)*Vs).
+        The reference's encoders number the feature ids field by field (creat_data.py's field
+        offsets), so the high-cardinality fields fill the last row blocks: measured on the
+        Criteo-shape C3 batches at N = 8 (gloo rehearsal, profiles/r06_n8_rehearsal.jsonl),
+        blocks gave one owner ~85 % of every batch's unique rows and an exchange capacity of
+        41,984 rows per pair against ~7,600 rows per owner on average (82 % padding); cyclic
+        ownership spreads every field over every rank."""
         self.rank, self.world_size = world()
         V = model.feature_embedding.weight.shape[0]
         if V < self.world_size:
@@ -152,8 +160,16 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if exchange not in ("padded", "varsplit"):
             raise ValueError(f"exchange must be 'padded' or 'varsplit', not {exchange!r}")
         self.exchange = exchange
+        layout = layout or os.environ.get("CTR_SHARD_LAYOUT", "cyclic")
+        if layout not in ("cyclic", "blocks"):
+            raise ValueError(f"layout must be 'cyclic' or 'blocks', not {layout!r}")
+        self.layout = layout
         self.shard_rows = -(-V // self.world_size)
         self._V_full = V
+        # cyclic at N > 1: the batch ids are permuted (ctr_shard_permute_ids) into the space
+        # where each rank's rows are one block again; at N = 1 both layouts are the identity
+        self._permute = layout == "cyclic" and self.world_size > 1
+        self._V_plan = self.shard_rows * self.world_size if self._permute else V
         self._shard_model(model, device)
         super().__init__(model, lr=lr, weight_decay=weight_decay, betas=betas, eps=eps,
                          process_group=process_group, seed=seed, optimizer_mode="deferred")
@@ -227,14 +243,13 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if device is None:
             device = E.device if E.is_cuda else torch.device("cuda", torch.cuda.current_device())
         device = torch.device(device)
-        lo = min(self.rank * self.shard_rows, self._V_full)
-        hi = min(lo + self.shard_rows, self._V_full)
+        n_r = self._rows_of(self.rank)
         tabs = [E] + ([model.linear.weight] if hasattr(model, "linear") else [])
         self._spare = {}
         for p in tabs:
-            buf = torch.zeros((hi - lo + 1,) + tuple(p.shape[1:]), dtype=p.dtype, device=device)
-            buf[:hi - lo].copy_(p.data[lo:hi])  # the full table's storage goes with .data
-            p.data = buf[:hi - lo]
+            buf = torch.zeros((n_r + 1,) + tuple(p.shape[1:]), dtype=p.dtype, device=device)
+            buf[:n_r].copy_(self._cut(p.data))  # the full table's storage goes with .data
+            p.data = buf[:n_r]
             self._spare[id(p)] = buf
         model.to(device)
         self._sharded_params = tabs
@@ -256,7 +271,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 the reference's): [row_lo, row_hi, V]."""
                 t = ref()
                 if t is not None:
-                    local_metadata["ctr_rows"] = [t.row_lo, t.row_hi, t._V_full]
+                    local_metadata["ctr_rows"] = t.shard_meta()
 
             def load_rows(state_dict, prefix, local_metadata, strict, missing, unexpected,
                           errors):
@@ -273,22 +288,54 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                     if v is None or v.dim() < 1:
                         continue
                     if v.shape[0] == t._V_full != t.V_tab:
-                        state_dict[prefix + name] = v[t.row_lo:t.row_hi]
+                        state_dict[prefix + name] = t._cut(v)
                         continue
                     got = local_metadata.get("ctr_rows")
-                    want = [t.row_lo, t.row_hi, t._V_full]
+                    want = t.shard_meta()
                     if got is None or list(got) != want:
                         raise RuntimeError(
                             f"ShardedCTRTrainer: {prefix + name} holds {v.shape[0]} rows with "
-                            f"row range {got} in its metadata; this rank owns rows "
-                            f"[{want[0]}, {want[1]}) of {want[2]} — load this rank's own "
-                            "state_dict() or a full-size table (full_state_dict())")
+                            f"row range {got} in its metadata; this rank owns the rows {want} "
+                            "— load this rank's own state_dict() or a full-size table "
+                            "(full_state_dict())")
             model.register_forward_pre_hook(no_forward)
             model._register_state_dict_hook(save_rows)
             model._register_load_state_dict_pre_hook(load_rows)
 
     def _vocab_size(self, E) -> int:
         return self._V_full
+
+    def _rows_of(self, r: int) -> int:
+        """Rows of the table rank r owns."""
+        V, n = self._V_full, self.world_size
+        if self.layout == "cyclic":
+            return max(0, (V - r + n - 1) // n)
+        lo = min(r * self.shard_rows, V)
+        return min(lo + self.shard_rows, V) - lo
+
+    def _cut(self, full: torch.Tensor, r: int | None = None) -> torch.Tensor:
+        """Rank r's rows (default: this rank's) of a full-size table, in local order."""
+        r = self.rank if r is None else r
+        if self.layout == "cyclic":
+            return full[r::self.world_size]
+        lo = min(r * self.shard_rows, self._V_full)
+        return full[lo:lo + self._rows_of(r)]
+
+    def shard_meta(self) -> list:
+        """The shard's identity as saved in the state dict's metadata ("ctr_rows"):
+        ["cyclic", rank, N, V] or, for the blocks layout, [row_lo, row_hi, V]."""
+        if self.layout == "cyclic":
+            return ["cyclic", self.rank, self.world_size, self._V_full]
+        lo = min(self.rank * self.shard_rows, self._V_full)
+        return [lo, lo + self._rows_of(self.rank), self._V_full]
+
+    def _plan_ids(self, x: torch.Tensor) -> torch.Tensor:
+        """The ids the plans are built over: x itself, or (cyclic, N > 1) a permuted copy."""
+        if not self._permute:
+            return x
+        xp = x.contiguous().clone() if x.is_cuda else x.to(self.device)
+        return hip_ops.shard_permute_ids_(xp, self.V, self.world_size, self.shard_rows,
+                                          err_flag=self.err)
 
     def _own_rows(self, t: torch.Tensor) -> torch.Tensor:
         """The shard's buffer, spare row included (the Parameter is its first V_tab rows)."""
@@ -313,8 +360,11 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         return b
 
     def _table_rows(self) -> tuple[int, int]:
-        lo = min(self.rank * self.shard_rows, self.V)
-        return lo, min(lo + self.shard_rows, self.V)
+        """The rank's rows as a range of the plan's id space (the permuted one, cyclic N > 1):
+        [rank * Vs, rank * Vs + rows)."""
+        lo = self.rank * self.shard_rows if self._permute else min(self.rank * self.shard_rows,
+                                                                   self.V)
+        return lo, lo + self._rows_of(self.rank)
 
     def optimizer_state_dict(self) -> dict:
         """The shard's moments (the spare row is internal): only the table parameters'
@@ -579,7 +629,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         slot.ev.record()
 
     def _plan_launch(self, slot: InputSlot) -> None:
-        slot.plan.build(slot.ids, self.V, err_flag=self.err)
+        if self._permute:  # cyclic rows: the slot's ids into the per-owner block space
+            hip_ops.shard_permute_ids_(slot.ids, self.V, self.world_size, self.shard_rows,
+                                       err_flag=self.err)
+        slot.plan.build(slot.ids, self._V_plan, err_flag=self.err)
         # the forward's ids over the compact table, ahead with the plan (off the step's path)
         slot.plan.slot_to_unique(out=slot.slot2u)
         if self.world_size <= 15:  # the counts and their maximum in one launch
@@ -662,7 +715,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # 1. row ids out: each owner's run, padded with its spare row
         t = self._mark("exchange")
         hip_ops.shard_pack_ids(plan, self.shard_rows, self.V, n, C, xb.send_ids, xb.counts,
-                               xb.offsets, err_flag=self.err)
+                               xb.offsets, err_flag=self.err, cyclic=self._permute)
         alltoall_equal(xb.recv_ids, xb.send_ids, self.group, force=f)
         self._span("exchange", t)
         # 2. owners: the plan over the requested rows (every source's run, ascending, the
@@ -861,7 +914,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             ps.wait_event(ev_start)
             x.record_stream(ps)
             with torch.cuda.stream(ps):
-                plan.build(x, self.V, err_flag=self.err)
+                plan.build(self._plan_ids(x), self._V_plan, err_flag=self.err)
                 plan.shard_counts(self.shard_rows, ws, out=counts)
         b.plan = plan
         with torch.cuda.stream(ps):
@@ -924,7 +977,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             with torch.cuda.stream(ps):  # allocated from the plan stream's pool: its writer
                 P = self._plan_for(n)
                 c = torch.empty(ws, dtype=torch.int64, device=self.device)
-                P.build(n, self.V, err_flag=self.err)
+                P.build(self._plan_ids(n), self._V_plan, err_flag=self.err)
                 P.shard_counts(self.shard_rows, ws, out=c)
                 ev = torch.cuda.Event()
                 ev.record(ps)
@@ -950,21 +1003,23 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         def gather(tab, width):
             send = torch.zeros(self.shard_rows, width, dtype=tab.dtype, device=tab.device)
             send[:self.V_tab] = tab.reshape(self.V_tab, width)
+            n = self.world_size
             if dev.type == "cuda" and not gloo:
-                out = torch.empty(self.shard_rows * self.world_size, width, dtype=tab.dtype,
-                                  device=dev)
+                out = torch.empty(self.shard_rows * n, width, dtype=tab.dtype, device=dev)
                 dist.all_gather_into_tensor(out, send, group=self.group)
+                if self.layout == "cyclic":  # row q*N + r = shard r's local row q
+                    return out.view(n, self.shard_rows, width).transpose(0, 1).reshape(
+                        -1, width)[:self.V].contiguous()
                 return out[:self.V]
             out = torch.empty(self.V, width, dtype=tab.dtype, device=dev)
             buf = send.cpu() if gloo else torch.empty_like(send)
-            for r in range(self.world_size):  # one shard in flight at a time
+            for r in range(n):  # one shard in flight at a time
                 src = dist.get_global_rank(self.group, r) if self.group is not None else r
                 if r == self.rank:
                     buf.copy_(send)
                 dist.broadcast(buf, src=src, group=self.group)
-                lo = r * self.shard_rows
-                cnt = max(0, min(self.shard_rows, self.V - lo))
-                out[lo:lo + cnt].copy_(buf[:cnt])
+                cnt = self._rows_of(r)
+                self._cut(out, r).copy_(buf[:cnt])
             return out
 
         return gather(E_loc, self.K), (gather(w_loc, 1) if w_loc is not None else None)

@@ -312,6 +312,19 @@ class FusedCTRTrainer:
         # in one step and none in the next)
         self._stage_seq = 0
         self._extra_plan_streams: list = []
+        # where a lookahead plan starts: after everything enqueued before the step that
+        # stages it (False), or after that whole step (True). Traced at C3 (round 5, kernel
+        # trace of the timed region): a plan that starts with the step lands beside the
+        # backward's weight-gradient GEMMs on every other step (its 26 column-sort blocks hold
+        # 26 CUs for ~125 us, dW0's one-block-per-CU grid then runs a second wave: 84 -> 132
+        # us, the step 410 -> 462 us); started after the step it runs beside the next step's
+        # catch-up and gather (HBM- and latency-bound, no slowdown measured) and is ready a
+        # whole step before it is needed. CTR_PLAN_AFTER_STEP=0/1 overrides the default
+        # (on for the MLP kinds, whose steps are long against the plan; FM steps at C2 are
+        # about the plan's length)
+        env = os.environ.get("CTR_PLAN_AFTER_STEP")
+        self.plan_after_step = (env == "1") if env in ("0", "1") else self.kind in _MLP_KINDS
+        self._ev_end = None
         # cross-step pipelining of the MLP kinds' weight-gradient tail (one process, deferred
         # mode): the largest weight gradient dW0 = dH1^T X and the MLP weights' Adam of step t
         # run at the START of step t+1's graph, on the side stream beside its catch-up and
@@ -631,6 +644,11 @@ class FusedCTRTrainer:
             loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan,
                                 pipe=self._pipe_state(slot))
             self._after_step()
+        if todo and self.plan_after_step:  # the staged plans start after this whole step
+            if self._ev_end is None:
+                self._ev_end = torch.cuda.Event()
+            self._ev_end.record(main)
+            ev_start = self._ev_end
         for n, k in todo:
             self._stage_ahead(n, k, shape, slot, ev_start, main, ny.get(k))
         return loss

@@ -992,3 +992,42 @@ def test_shard_row_grads_capacity_overflow_stays_in_chunk(cuda, mode):
             assert bool((g[j, C * K + m:] == sentinel).all()), j
         else:
             assert bool((g[j, C * K:] == sentinel).all()), j
+
+
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_shard_permute_ids_and_cyclic_pack(cuda, dtype):
+    """Cyclic row sharding: ctr_shard_permute_ids maps r -> (r % N) * Vs + r // N in place
+    (bit-exact vs numpy; ids outside [0, V) raise CTR_EFLAG_INDEX and map to row 0), the plan
+    over the permuted ids groups its unique rows by owner, and ctr_shard_pack_ids_layout
+    packs each owner's run as owner-local ids r // N padded with the owner's cyclic row count
+    ceil((V - j) / N) (its spare row)."""
+    from rl_ctr_prediction_amd import hip_ops as H
+    rng = np.random.default_rng(5)
+    V, N, B, F = 10_007, 4, 300, 7
+    Vs = -(-V // N)
+    x = rng.integers(0, V, size=(B, F))
+    got = torch.tensor(x, dtype=dtype, device=cuda)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    H.shard_permute_ids_(got, V, N, Vs, err_flag=err)
+    want = (x % N) * Vs + x // N
+    assert np.array_equal(got.cpu().numpy(), want) and int(err) == 0
+    bad = torch.tensor([[0, V, -1, V - 1]], dtype=dtype, device=cuda)
+    H.shard_permute_ids_(bad, V, N, Vs, err_flag=err)
+    assert int(err) != 0
+    assert bad.cpu().tolist() == [[0, 0, 0, ((V - 1) % N) * Vs + (V - 1) // N]]
+    plan = H.SparsePlanBuffers(B * F, cuda).build(got, N * Vs)
+    U = plan.num_unique_host()
+    urows = plan.unique_rows[:U].cpu().numpy()
+    assert np.array_equal(urows, np.unique(want))
+    C = 512
+    send = torch.empty(N * C, dtype=torch.int32, device=cuda)
+    counts = torch.empty(N, dtype=torch.int32, device=cuda)
+    offsets = torch.empty(N, dtype=torch.int32, device=cuda)
+    H.shard_pack_ids(plan, Vs, V, N, C, send, counts, offsets, cyclic=True)
+    s = send.view(N, C).cpu().numpy()
+    orig = np.unique(x)
+    for j in range(N):
+        mine = orig[orig % N == j] // N
+        assert int(counts[j]) == len(mine)
+        assert np.array_equal(s[j, :len(mine)], mine), j
+        assert (s[j, len(mine):] == len(range(j, V, N))).all(), j
