@@ -39,8 +39,13 @@ typedef float pf32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
 
+// the software-pipelined stage of the k-contiguous x k-contiguous products with >= 4
+// 16-column groups per wave (fwd0's 64 x 160 tiling: B fragments of group tn+1 read under the
+// MFMAs of group tn, the DMA pieces spread between the groups): fwd0 69.2 -> 59.7 us
+// standalone at C3 (tools/gemm_planes_bench.py, profiles/r06_gemm_pipe.txt); fwd1's 32 x 32
+// waves (two groups) ran slower that way (17.4 -> 19.1 us) and keep the burst form
 #ifndef CTR_PL_PIPE
-#define CTR_PL_PIPE 0
+#define CTR_PL_PIPE 1
 #endif
 
 struct PlaneSrc {
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
 
   constexpr int IPW = IPWA + IPWB;
 #if CTR_PL_PIPE
-  if constexpr (!A_RC && !B_RC && KS == 1) {
+  if constexpr (!A_RC && !B_RC && KS == 1 && TN >= 4) {
     // Software-pipelined stage (both operands k-contiguous): the B fragments of 16-column
     // group tn+1 are read while the MFMAs of group tn run, and the stage's LDS-DMA pieces
     // for stage t+NS-1 are issued between the groups instead of in one burst at the

@@ -108,7 +108,8 @@ class InputSlot:
     reference trains on a new batch every iteration, all_main/pretrain_main.py:71-78)."""
 
     __slots__ = ("shape", "index", "ids", "y", "y_key", "plan", "ev", "plan_graph",
-                 "done_ev", "stream_i", "stage_stream", "cap", "counts", "slot2u", "gen")
+                 "done_ev", "stream_i", "stage_stream", "cap", "counts", "slot2u", "gen",
+                 "planned")
 
     def __init__(self, shape, index: int, device):
         B, F, dtype = shape
@@ -125,6 +126,7 @@ class InputSlot:
         self.cap = self.counts = None  # ShardedCTRTrainer: per-owner runs of the plan
         self.slot2u = None  # ShardedCTRTrainer: slot -> unique ordinal, built with the plan
         self.gen = 0  # ShardedCTRTrainer: staging generation (which contents the plan measured)
+        self.planned = True  # False: staged ids copied, plan not built yet (plan_in_graph)
 
 
 @dataclass
@@ -323,8 +325,18 @@ class FusedCTRTrainer:
         # (on for the MLP kinds, whose steps are long against the plan; FM steps at C2 are
         # about the plan's length)
         env = os.environ.get("CTR_PLAN_AFTER_STEP")
-        self.plan_after_step = (env == "1") if env in ("0", "1") else self.kind in _MLP_KINDS
+        self.plan_after_step = (env == "1") if env in ("0", "1") else False
         self._ev_end = None
+        # MLP kinds: the next batch's plan inside this step's graph, on the side list while
+        # dX runs (the window between dW1 and the dX join, idle otherwise); a staged batch is
+        # then only copied ahead. Traced at C3 (round 6, profiles/r06_c3_timelines.txt): a plan
+        # built on a plan stream lands wherever its queue lets it — beside dW0 on some steps
+        # (+50 us), beside the next catch-up / gather on others — so the steps' walls spread
+        # 394-460 us; in the step's own side list it has a fixed place
+        env = os.environ.get("CTR_PLAN_IN_GRAPH")
+        self.plan_in_graph = ((env == "1") if env in ("0", "1") else True) and (
+            self.kind in _MLP_KINDS)
+        self._next_plan = None  # the staged slot whose plan the step being launched builds
         # cross-step pipelining of the MLP kinds' weight-gradient tail (one process, deferred
         # mode): the largest weight gradient dW0 = dH1^T X and the MLP weights' Adam of step t
         # run at the START of step t+1's graph, on the side stream beside its catch-up and
@@ -621,37 +633,93 @@ class FusedCTRTrainer:
         if self._staged:  # staged for batches that did not come next: free their slots
             keep = {k for _, k in nk}
             for k in [k for k in self._staged if k not in keep]:
-                main.wait_event(self._staged.pop(k).ev)  # its plan-stream writes come first
+                ev = self._staged.pop(k).ev
+                if ev is not None:  # None: planned in a step graph (main's order)
+                    main.wait_event(ev)  # its plan-stream writes come first
         todo = [(n, k) for n, k in nk if k not in self._staged]
         have = slot is not None
         ev_start = None
         if todo:  # everything enqueued before this step (the last users of the slots)
             ev_start = self._start_event()
             ev_start.record(main)
-        if have:  # copied and planned ahead on the plan stream
-            main.wait_event(slot.ev)
-            slot.ev = None
+        # the next batch's plan in this step's graph (MLP kinds): its slot is only copied ahead
+        pig = (self.plan_in_graph and not self._pipe and self._side is not None
+               and self.deferred)
+        if have:  # copied (and planned) ahead
+            if slot.ev is not None:
+                main.wait_event(slot.ev)
+                slot.ev = None
+            if not slot.planned:  # copied ahead, no step planned it: build it here, first
+                self._plan_staged_now(slot, main)
         else:
             slot = self._acquire_slot(shape)
             slot.ids.copy_(x, non_blocking=True)
         if not (have and slot.y_key is not None and slot.y_key == self._xkey(y)):
             slot.y.copy_(y.reshape(-1), non_blocking=True)
         slot.y_key = None
-        if self.use_graphs and self.timing is None:
-            loss = self._graph_step(slot, mean_div, have)
-        else:
-            self.step_table.ensure(self.step_count + 1)
-            loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan,
-                                pipe=self._pipe_state(slot))
-            self._after_step()
+        nxt = None
+        if pig and nk:
+            n1, k1 = nk[0]
+            if k1 not in self._staged:  # stage (copy) it now: this step plans it
+                self._stage_ahead(n1, k1, shape, slot, ev_start, main, ny.get(k1), plan=False)
+                todo = [(n, k) for n, k in todo if k != k1]
+            nxt = self._staged[k1]
+            if nxt.planned:
+                nxt = None
+            elif nxt.ev is not None:
+                main.wait_event(nxt.ev)  # its ids copy
+                nxt.ev = None
+        self._next_plan = nxt
+        try:
+            if self.use_graphs and self.timing is None:
+                loss = self._graph_step(slot, mean_div, have)
+            else:
+                self.step_table.ensure(self.step_count + 1)
+                loss = self._launch(slot.ids, slot.y, mean_div, have, plan=slot.plan,
+                                    pipe=self._pipe_state(slot))
+                self._after_step()
+        finally:
+            self._next_plan = None
+        if nxt is not None:  # complete in main's order, after this step
+            nxt.planned = True
         if todo and self.plan_after_step:  # the staged plans start after this whole step
             if self._ev_end is None:
                 self._ev_end = torch.cuda.Event()
             self._ev_end.record(main)
             ev_start = self._ev_end
         for n, k in todo:
-            self._stage_ahead(n, k, shape, slot, ev_start, main, ny.get(k))
+            self._stage_ahead(n, k, shape, slot, ev_start, main, ny.get(k), plan=not pig)
         return loss
+
+    def _plan_staged_now(self, s: InputSlot, main) -> None:
+        """The plan of a slot staged (copied) ahead that no step graph planned, on its
+        staging stream (after its copy), replayed from its own plan graph once captured; the
+        main stream waits for it."""
+        ps = s.stage_stream if s.stage_stream is not None else self._plan_stream
+        torch.cuda.set_stream(ps)
+        try:
+            self._plan_build_slot(s, ps)
+            ev = self._slot_event(s)
+            ev.record(ps)
+        finally:
+            torch.cuda.set_stream(main)
+        main.wait_event(ev)
+        s.planned = True
+
+    def _plan_build_slot(self, s: InputSlot, ps) -> None:
+        """On the current stream ps: slot s's plan (its own captured plan graph once it
+        exists)."""
+        t = self._mark("plan")
+        if s.plan_graph is not None and self.timing is None:
+            s.plan_graph.replay()
+        else:
+            s.plan.build(s.ids, self.V)
+            if self.use_graphs and self.timing is None:
+                g = torch.cuda.CUDAGraph()
+                with graph_capture(g, pool=live_pool(self), stream=ps):
+                    s.plan.build(s.ids, self.V)  # captured, not executed
+                s.plan_graph = g
+        self._span("plan", t)
 
     def _ring(self, shape) -> list:
         r = self._rings.get(shape)
@@ -713,10 +781,11 @@ class FusedCTRTrainer:
         return s
 
     def _stage_ahead(self, nx: torch.Tensor, key, shape, current: InputSlot, ev_start,
-                     main, ny: torch.Tensor | None = None) -> None:
+                     main, ny: torch.Tensor | None = None, plan: bool = True) -> None:
         """Copy ids nx into a free slot and build its sparse plan there, on the slot's plan
         stream, concurrently with the step just enqueued (replayed from the slot's own
-        plan graph once captured)."""
+        plan graph once captured). plan=False: the copy only (plan_in_graph: the step
+        before the batch's own builds its plan inside its graph)."""
         s = self._acquire_slot(shape, exclude=current, ahead=True)
         ps = self._stage_stream(s)
         ps.wait_event(ev_start)
@@ -737,17 +806,9 @@ class FusedCTRTrainer:
                 if ny.is_cuda:
                     ny.record_stream(ps)
                 s.y_key = self._xkey(ny)
-            t = self._mark("plan")
-            if s.plan_graph is not None and self.timing is None:
-                s.plan_graph.replay()
-            else:
-                s.plan.build(s.ids, self.V)
-                if self.use_graphs and self.timing is None:
-                    g = torch.cuda.CUDAGraph()
-                    with graph_capture(g, pool=live_pool(self), stream=ps):
-                        s.plan.build(s.ids, self.V)  # captured, not executed
-                    s.plan_graph = g
-            self._span("plan", t)
+            s.planned = plan
+            if plan:
+                self._plan_build_slot(s, ps)
             ev = self._slot_event(s)
             ev.record(ps)
         finally:
@@ -855,8 +916,10 @@ class FusedCTRTrainer:
         mlp = getattr(self.model, "mlp", None)
         drops = tuple(float(mlp[i].p) for i in (2, 5)) if mlp is not None else ()
         pipe = self._pipe_state(slot)
+        nxt = self._next_plan
         key = (slot.shape, slot.index, mean_div, self.model.training, drops, have,
-               pipe[0], None if pipe[1] is None else (pipe[1][0].B, pipe[1][2]))
+               pipe[0], None if pipe[1] is None else (pipe[1][0].B, pipe[1][2]),
+               None if nxt is None else (nxt.shape, nxt.index))
         hit = self._graphs.get(key)
         if hit is None:
             # the real step (sizes every buffer), then the same launches captured
@@ -1172,6 +1235,11 @@ class FusedCTRTrainer:
             # Linear(300,200): dW1 = dH2^T H1, db1 = colsum dH2 (H1's ones column)
             self._gemm_planes(b.dh2p, b.h1p, True, True, H2, H1, B,
                               out=gv["mlp.3.weight"], last_col=gv["mlp.3.bias"])
+            nxt = self._next_plan
+            if nxt is not None:  # the next batch's plan, beside dX (plan_in_graph)
+                t = self._mark("plan")
+                nxt.plan.build(nxt.ids, self.V)
+                self._span("plan", t)
             if side is not None:  # from dX on
                 side.wait_event(b.ev_dx)
             # the column-sum pair here, ahead of dW0: seg_chunk takes the CUs before dW0
