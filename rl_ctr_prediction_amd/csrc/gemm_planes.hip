@@ -47,6 +47,9 @@ constexpr int kPBK = 32;  // k per LDS stage = one 16x16x32 MFMA
 #ifndef CTR_PL_PIPE
 #define CTR_PL_PIPE 1
 #endif
+#ifndef CTR_PL_PIPE2
+#define CTR_PL_PIPE2 0
+#endif
 
 struct PlaneSrc {
   const uint16_t* p;  // plane 0 (bf16 bits); planes `ps` elements apart
@@ -146,6 +149,14 @@ __device__ __forceinline__ int frag_rc_img_off(int cb, int lane, int j) {
 
 __device__ __forceinline__ pbf16x8 frag_kc_at(const char* p) {
   return *reinterpret_cast<const pbf16x8*>(p);
+}
+
+// the same read as an asm statement (waited for by hand, CTR_PL_PIPE2)
+__device__ __forceinline__ pbf16x8 frag_kc_asm(const char* p) {
+  pbf16x8 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const CTR_LDS char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return v;
 }
 
 // The transpose reads as inline asm (CTR_PL_TR_ASM, default): with the builtin, hipcc 7.2
@@ -438,6 +449,92 @@ __global__ __launch_bounds__(64 * WAVES_M* WAVES_N) void gemm_planes_kernel(Plan
   };
 
   constexpr int IPW = IPWA + IPWB;
+#if CTR_PL_PIPE2
+  if constexpr ((A_RC || B_RC) && KS == 1) {
+    // The pipelined stage for products with a k-strided operand: every fragment read is an
+    // asm statement (the compiler's wait pass cannot count the transpose reads, and its
+    // conservative lgkmcnt(0) for its own reads would drain them too), waited for by hand:
+    // the B fragments of group tn+1 are in flight (lgkmcnt(NBR)) under the MFMAs of group
+    // tn, and the next stage's DMA pieces are spread between the groups.
+    constexpr int NBR = 3 * (B_RC ? 2 : 1);
+    const int tlast = nt - 1;
+    auto issue_piece = [&](int j, int ts) {
+      char* st_ = smem + (ts % NS) * STAGE;
+      const int tsrc = min(ts, tlast);
+      if (j < IPWA)
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)SA.p + (int64_t)tsrc * stepA + offA[j]),
+                                         (CTR_LDS void*)(st_ + ldsA[j]), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)SB.p + (int64_t)tsrc * stepB + offB[j - IPWA]),
+                                         (CTR_LDS void*)(st_ + ldsB[j - IPWA]), 16, 0, 0);
+    };
+    if (nt > 0) {
+#pragma unroll
+      for (int s = 0; s < NS - 1; ++s)
+#pragma unroll
+        for (int j = 0; j < IPW; ++j) issue_piece(j, s);
+    }
+    for (int t = 0; t < nt; ++t) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IPW * (NS - 2)) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* st = smem + (t % NS) * STAGE;
+      if constexpr (NS <= 2) {  // a 2-deep ring: the next stage's pieces go out first
+#pragma unroll
+        for (int j = 0; j < IPW; ++j) issue_piece(j, t + NS - 1);
+      }
+      pbf16x8 af[TM][3], bf[2][3];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const char* img = st + p * A_PL;
+          af[i][p] = A_RC ? frag_rc_at(img + aoff[i][0], img + aoff[i][1])
+                          : frag_kc_asm(img + aoff[i][0]);
+        }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const char* img = st + 3 * A_PL + p * B_PL;
+        bf[0][p] = B_RC ? frag_rc_at(img + boff[0][0], img + boff[0][1])
+                        : frag_kc_asm(img + boff[0][0]);
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int cb = tn & 1;
+        if (tn + 1 < TN) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const char* img = st + 3 * A_PL + p * B_PL;
+            bf[cb ^ 1][p] = B_RC ? frag_rc_at(img + boff[tn + 1][0], img + boff[tn + 1][1])
+                                 : frag_kc_asm(img + boff[tn + 1][0]);
+          }
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NBR) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NS > 2) {  // deeper rings: the pieces spread between the groups
+          const int j0 = (IPW * tn) / TN, j1 = (IPW * (tn + 1)) / TN;
+#pragma unroll
+          for (int j = 0; j < IPW; ++j)
+            if (j >= j0 && j < j1) issue_piece(j, t + NS - 1);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          pf32x4 v = lo[i][tn];
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[cb][1], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][2], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bf[cb][0], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][1], v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[cb][0], v, 0, 0, 0);
+          lo[i][tn] = v;
+          acc[i][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[cb][0], acc[i][tn], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else
+#endif
 #if CTR_PL_PIPE
   if constexpr (!A_RC && !B_RC && KS == 1 && TN >= 4) {
     // Software-pipelined stage (both operands k-contiguous): the B fragments of 16-column

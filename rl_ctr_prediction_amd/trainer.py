@@ -327,15 +327,17 @@ class FusedCTRTrainer:
         env = os.environ.get("CTR_PLAN_AFTER_STEP")
         self.plan_after_step = (env == "1") if env in ("0", "1") else False
         self._ev_end = None
-        # MLP kinds: the next batch's plan inside this step's graph, on the side list while
-        # dX runs (the window between dW1 and the dX join, idle otherwise); a staged batch is
-        # then only copied ahead. Traced at C3 (round 6, profiles/r06_c3_timelines.txt): a plan
-        # built on a plan stream lands wherever its queue lets it — beside dW0 on some steps
-        # (+50 us), beside the next catch-up / gather on others — so the steps' walls spread
-        # 394-460 us; in the step's own side list it has a fixed place
+        # MLP kinds, opt-in (CTR_PLAN_IN_GRAPH=1): the next batch's plan inside this step's
+        # graph, on the side list between dW1 and the dX join; a staged batch is then only
+        # copied ahead. Traced at C3 (round 6, profiles/r06_c3_timelines.txt): a plan built on
+        # a plan stream lands wherever its queue lets it — beside dX (free), beside dW0 on some
+        # steps (+50 us), beside the next catch-up / gather on others — so the steps' walls
+        # spread 394-460 us. In the side list the column sort stretches to ~83 us beside dX
+        # and delays dW0 until after the scatter: every step 435-450 us (scatter 40 us alone
+        # instead of 84 beside dW0, dW0 66 alone instead of 85, but serial), C3 12.73 / 12.78
+        # / 12.92 vs 13.32 / 13.32 / 13.39 M ex/s off (alternating): off by default
         env = os.environ.get("CTR_PLAN_IN_GRAPH")
-        self.plan_in_graph = ((env == "1") if env in ("0", "1") else True) and (
-            self.kind in _MLP_KINDS)
+        self.plan_in_graph = (env == "1") and self.kind in _MLP_KINDS
         self._next_plan = None  # the staged slot whose plan the step being launched builds
         # cross-step pipelining of the MLP kinds' weight-gradient tail (one process, deferred
         # mode): the largest weight gradient dW0 = dH1^T X and the MLP weights' Adam of step t

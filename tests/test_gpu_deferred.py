@@ -250,8 +250,11 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         st = tr.optimizer_state_dict()["state"]
         out.append((losses, sd, st))
         if graphs:  # (slot, planned ahead) pairs of a ring of ahead + 1 slots (x the
-            # pipelined kinds' X plane buffer and pending-tail variants)
-            assert tr.captures <= 2 * (ahead + 1) * (3 if tr._pipe else 1)
+            # pipelined kinds' X plane buffer and pending-tail variants; x the slot whose
+            # plan the step builds in its graph — one of the ring or none — for the MLP kinds)
+            pig = tr.plan_in_graph and ahead > 0 and pla
+            assert tr.captures <= 2 * (ahead + 1) * (3 if tr._pipe else 1) * (
+                (ahead + 2) if pig else 1)
     for losses, sd, st in out[1:]:
         assert losses == out[0][0]
         for k in sd:
