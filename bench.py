@@ -5,7 +5,8 @@
 N>1 is launched by the driver as `python -m torch.distributed.run --nproc-per-node N ...`:
 one process per GPU, RCCL over xGMI, data parallel with row-sharded embedding tables
 (ShardedCTRTrainer: ids / rows / row gradients by all-to-all, dense gradients all-reduced;
---sharding replicated keeps full replicas with a sparse all-gather). Weak scaling: every
+--sharding replicated keeps full replicas with a sparse all-gather: a comparison mode, eager,
+one host read per step — DESIGN.md §6). Weak scaling: every
 rank trains its own B-example batches; value = all ranks' examples / max time.
 
 Workload (default c3 = BASELINE configs[2], the north-star target shape): DeepFM, 26
@@ -455,7 +456,8 @@ def main():
     ap.add_argument("--breakdown-steps", type=int, default=10,
                     help="un-timed steps with every kernel group instrumented (kernel table)")
     ap.add_argument("--sharding", default="auto", choices=["auto", "rows", "replicated"],
-                    help="N>1: row-sharded tables with all-to-all (auto) or replicated tables "
+                    help="N>1: row-sharded tables with all-to-all (auto) or, for comparison only "
+                         "(eager, a host read per step), replicated tables "
                          "with a sparse all-gather")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="sparse plans built this many batches ahead, concurrently with the "

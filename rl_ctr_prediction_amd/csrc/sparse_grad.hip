@@ -11,6 +11,16 @@
 // result is bitwise reproducible, which is what keeps data-parallel replicas identical.
 #include "adam_common.h"
 
+// FM rows: the per-slot term without the row's own embedding (g*s + d), the row term
+// -(sum g) * e added once per row where its sum completes — the embedding row is then read
+// once per unique row (the apply pass holds it anyway) instead of once per slot (at C3 the
+// 54 MB of random row reads in seg_chunk). The sums differ from the per-slot form by fp32
+// association only, within the oracle's gradient bar (tests/conftest.py: both terms are in
+// grad_condition). CTR_SEG_FM_DEFER=0 builds the per-slot form.
+#ifndef CTR_SEG_FM_DEFER
+#define CTR_SEG_FM_DEFER 1
+#endif
+
 namespace ctr {
 
 // Sorted positions per lane group: 16 when a row is >= 16 lane columns (K >= 64), else 4
@@ -34,6 +44,16 @@ struct VOps<float> {
 #pragma clang fp contract(off)
     return (g * s - g * e) + d;
   }
+  // the slot's term without its row: g*s + d (the row's -e * sum(g) is added once per row)
+  __device__ static float fm2(float g, float s, float d) {
+#pragma clang fp contract(off)
+    return g * s + d;
+  }
+  // a row's sum of fm2 terms A and its sum of g, c: A - c*e (the product rounded)
+  __device__ static float fin(float acc, float c, float e) {
+#pragma clang fp contract(off)
+    return acc - c * e;
+  }
 };
 template <>
 struct VOps<float4> {
@@ -48,6 +68,14 @@ struct VOps<float4> {
   __device__ static float4 fm(float g, float4 s, float4 e, float4 d) {
     return make_float4(VOps<float>::fm(g, s.x, e.x, d.x), VOps<float>::fm(g, s.y, e.y, d.y),
                        VOps<float>::fm(g, s.z, e.z, d.z), VOps<float>::fm(g, s.w, e.w, d.w));
+  }
+  __device__ static float4 fm2(float g, float4 s, float4 d) {
+    return make_float4(VOps<float>::fm2(g, s.x, d.x), VOps<float>::fm2(g, s.y, d.y),
+                       VOps<float>::fm2(g, s.z, d.z), VOps<float>::fm2(g, s.w, d.w));
+  }
+  __device__ static float4 fin(float4 acc, float c, float4 e) {
+    return make_float4(VOps<float>::fin(acc.x, c, e.x), VOps<float>::fin(acc.y, c, e.y),
+                       VOps<float>::fin(acc.z, c, e.z), VOps<float>::fin(acc.w, c, e.w));
   }
 };
 
@@ -66,6 +94,11 @@ struct SegArgs {
   const void* sum_e;
   const void* dx;
   const void* emb;
+  // FM with the row term deferred (CTR_SEG_FM_DEFER): per slot g*s + d, per row
+  // sum - (sum g) * e, e read once per row (emb by unique row, or by segment ordinal for a
+  // table compacted in unique order: emb_by_seg)
+  bool fm_defer;
+  bool emb_by_seg;
   // generic contribution (MODE_VALS)
   const void* vals;
   const float* vals_lin;
@@ -119,6 +152,17 @@ __device__ __forceinline__ void seg_emit(const SegArgs& a, int64_t u, int c, boo
   }
 }
 
+// a completed row sum of the deferred FM form: its row term, then written out
+template <typename VT>
+__device__ __forceinline__ void seg_final(const SegArgs& a, int64_t u, int c, bool col, VT acc,
+                                          float accl) {
+  if (a.fm_defer && col) {
+    const int64_t r = a.emb_by_seg ? u : (int64_t)a.unique_rows[u];
+    acc = VOps<VT>::fin(acc, accl, static_cast<const VT*>(a.emb)[r * a.KV + c]);
+  }
+  seg_emit<VT>(a, u, c, col, acc, accl);
+}
+
 enum { MODE_FM = 0, MODE_VALS = 1 };
 
 template <typename VT, int LPR, int MODE>
@@ -149,12 +193,16 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
         const float g = a.gz[b];
         gl[i] = g;
         if (col) {
-          const int32_t row = a.sorted_rows[pos];
           const VT s = static_cast<const VT*>(a.sum_e)[b * a.KV + c];
-          const VT e = static_cast<const VT*>(a.emb)[(int64_t)row * a.KV + c];
           const VT d = a.dx ? static_cast<const VT*>(a.dx)[(int64_t)slot * a.KV + c]
                             : VOps<VT>::zero();
-          val[i] = VOps<VT>::fm(g, s, e, d);
+          if (a.fm_defer) {  // the row's own term once per row (seg_final / the apply)
+            val[i] = VOps<VT>::fm2(g, s, d);
+          } else {
+            const int32_t row = a.sorted_rows[pos];
+            const VT e = static_cast<const VT*>(a.emb)[(int64_t)row * a.KV + c];
+            val[i] = VOps<VT>::fm(g, s, e, d);
+          }
         }
       } else {
         if (a.vals_lin) gl[i] = a.vals_lin[slot];
@@ -167,7 +215,10 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegArgs a) {
     const int32_t off0 = a.seg_offsets[u];
     const int32_t off1 = a.seg_offsets[u + 1];
     if (off0 / kChunk == (off1 - 1) / kChunk) {  // whole row inside this chunk: final
-      seg_emit<VT>(a, u, c, col, acc, accl);
+      if (a.apply)  // the apply pass adds the deferred row term (it holds the row)
+        seg_emit<VT>(a, u, c, col, acc, accl);
+      else
+        seg_final<VT>(a, u, c, col, acc, accl);
     } else {
       const int64_t k = gid * 2 + (first_run ? 0 : 1);
       if (col) static_cast<VT*>(a.part)[k * a.KV + c] = acc;
@@ -229,7 +280,7 @@ __global__ __launch_bounds__(256) void seg_combine_kernel(SegArgs a) {
       VOps<VT>::add(acc, VOps<VT>::shfl_xor(acc, o));
       accl += __shfl_xor(accl, o, kWave);
     }
-    if (g == 0) seg_emit<VT>(a, u, c, col, acc, accl);
+    if (g == 0) seg_final<VT>(a, u, c, col, acc, accl);
   }
 }
 
@@ -339,8 +390,11 @@ __global__ __launch_bounds__(256) void seg_combine_apply_kernel(SegArgs a) {
         gr = s_sum[wib][g * LPR + c];
         gl = s_lin[wib][g];
       }
-      if (P > 1 && a.out_keep) seg_emit<VT>(a, u, c, col, gr, gl);
-      deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, a.unique_rows[u], a.KV, c,
+      const int64_t r = a.unique_rows[u];
+      if (a.fm_defer && col)  // the row's term: e = the row as the forward read it (step-1)
+        gr = VOps<VT>::fin(gr, gl, a.E[r * a.KV + c]);
+      if ((P > 1 || a.fm_defer) && a.out_keep) seg_emit<VT>(a, u, c, col, gr, gl);
+      deferred_apply_row(a.E, a.mE, a.vE, a.w, a.mw, a.vw, a.last, r, a.KV, c,
                          col, gr, gl, step, a.tab, a.hp);
     }
     __builtin_amdgcn_wave_barrier();  // the slots are re-filled by the next iteration
@@ -487,6 +541,8 @@ extern "C" int ctr_fm_embedding_grad(const ctr_sparse_plan* plan, int F, int K, 
   a.sum_e = sum_e;
   a.dx = dx;
   a.emb = emb;
+  a.fm_defer = CTR_SEG_FM_DEFER;
+  a.emb_by_seg = plan->sorted_rows == plan->pos_seg;
   const bool al = ((uintptr_t)emb | (uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)grad_rows |
                    (uintptr_t)ws) % 16 == 0;
   return launch_seg(a, K, MODE_FM, as_stream(stream), al);
@@ -539,6 +595,8 @@ extern "C" int ctr_fm_embedding_grad_adam(const ctr_sparse_plan* plan, int F, in
   a.sum_e = sum_e;
   a.dx = dx;
   a.emb = table->emb;
+  a.fm_defer = CTR_SEG_FM_DEFER;
+  a.emb_by_seg = plan->sorted_rows == plan->pos_seg;
   CTR_REQUIRE(((uintptr_t)sum_e | (uintptr_t)dx | (uintptr_t)grad_rows | (uintptr_t)ws) % 16 == 0,
               "ctr_fm_embedding_grad_adam: 16-B aligned buffers required");
   return launch_seg(a, K, MODE_FM, as_stream(stream), true);
@@ -616,6 +674,8 @@ extern "C" int ctr_shard_row_grads(const ctr_sparse_plan* plan, int F, int K, co
     a.sum_e = sum_e;
     a.dx = dx;
     a.emb = emb;
+    a.fm_defer = CTR_SEG_FM_DEFER;
+    a.emb_by_seg = plan->sorted_rows == plan->pos_seg;
     return launch_seg(a, K, MODE_FM, as_stream(stream), true);
   }
   a.vals = vals;

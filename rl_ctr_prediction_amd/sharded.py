@@ -698,6 +698,15 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._after_step()
         return self._bufs.loss
 
+    def _xchg(self, out: torch.Tensor, send: torch.Tensor, coll: bool) -> torch.Tensor:
+        """The equal-split all-to-all of one exchange buffer into `out`, or (one process, no
+        forced collectives) `send` itself: a one-rank all-to-all is the identity, so the
+        readers take the send buffer and no copy is launched."""
+        if not coll:
+            return send
+        alltoall_equal(out, send, self.group, force=True)
+        return out
+
     def _launch_sharded(self, slot: InputSlot, mean_div: float, C: int) -> torch.Tensor:
         """Enqueue one fixed-capacity step (no host read, no size taken from the device:
         capturable for a given C)."""
@@ -716,7 +725,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         t = self._mark("exchange")
         hip_ops.shard_pack_ids(plan, self.shard_rows, self.V, n, C, xb.send_ids, xb.counts,
                                xb.offsets, err_flag=self.err, cyclic=self._permute)
-        alltoall_equal(xb.recv_ids, xb.send_ids, self.group, force=f)
+        recv_ids = self._xchg(xb.recv_ids, xb.send_ids, f)
         self._span("exchange", t)
         # 2. owners: the plan over the requested rows (every source's run, ascending, the
         # spare row as padding: ctr_sparse_plan_build_runs, 5 short launches instead of an
@@ -726,9 +735,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         # the rows up, gather them, send them back
         t = self._mark("plan")
         if n <= 8:  # n ascending runs of unique rows + spare-row padding: the runs plan
-            xb.gplan.build_runs(xb.recv_ids, n, Vo, self._runs_mask(Vo))
+            xb.gplan.build_runs(recv_ids, n, Vo, self._runs_mask(Vo))
         else:
-            xb.gplan.build(xb.recv_ids, Vo)
+            xb.gplan.build(recv_ids, Vo)
         self._span("plan", t)
         t = self._mark("catchup")
         hip_ops.adam_deferred_rows(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
@@ -738,10 +747,10 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         self._span("catchup", t)
         t = self._mark("exchange")
         # the rows and their linear weights: one gather, one all-to-all, one unpack
-        hip_ops.shard_gather_rows(self.E_tab, self.w_tab if has_lin else None, xb.recv_ids, n,
+        hip_ops.shard_gather_rows(self.E_tab, self.w_tab if has_lin else None, recv_ids, n,
                                   C, out=xb.rows_out)
-        alltoall_equal(xb.rows_in, xb.rows_out, self.group, force=f)
-        hip_ops.shard_rows_unpack(xb.rows_in, C, xb.counts, xb.offsets, xb.table,
+        rows_in = self._xchg(xb.rows_in, xb.rows_out, f)
+        hip_ops.shard_rows_unpack(rows_in, C, xb.counts, xb.offsets, xb.table,
                                   xb.lin_table if has_lin else None)
         T_lin = xb.lin_table.view(-1, 1) if has_lin else None
         self._span("exchange", t)
@@ -759,9 +768,9 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         if not self._grads_to_chunks or self.keep_grads:  # keep_grads: the compact sums stay
             hip_ops.shard_rows_pack(b.grad_rows, b.grad_lin if has_lin else None, C, xb.counts,
                                     xb.offsets, out=xb.g_out)
-        alltoall_equal(xb.g_recv, xb.g_out, self.group, force=f)
+        g_recv = self._xchg(xb.g_recv, xb.g_out, f)
         if not self._owner_direct:  # the owners' chunked sums read (source, position) rows
-            hip_ops.shard_rows_unpack(xb.g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
+            hip_ops.shard_rows_unpack(g_recv, C, xb.all_counts, xb.all_offsets, xb.g_in,
                                       xb.glin_in if has_lin else None)
         self._span("exchange", t)
         # 5. the owners' sums and Adam here, beside the weight-gradient stream (dW0 ...);
@@ -772,7 +781,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             # padding target) is skipped
             t = self._mark("scatter")
             hip_ops.adam_deferred_entries(self.E_tab, self.m_E, self.v_E, self.w_tab, self.m_w,
-                                          self.v_w, self.last, xb.gplan, xb.g_recv, None,
+                                          self.v_w, self.last, xb.gplan, g_recv, None,
                                           step_hint,
                                           self.step_table, self.betas, self.eps,
                                           self.weight_decay, skip_row=Vo - 1,
