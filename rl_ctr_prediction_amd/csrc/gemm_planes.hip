@@ -780,6 +780,10 @@ static const PlDef kPl[] = {
     // blocks): W0's strip is re-read by half as many blocks, 27 KB of fill per
     // 64 x 160 x 32 of work instead of 43
     {128, 160, 4, 2, 2, 1, 0.62},  // 29: 110 KB
+    // one N tile for N <= 224 (fwd1: N = 200): the A operand (H1's planes) is read once
+    // instead of once per 64-wide N tile; 16 x 112 per wave (TN = 7: the pipelined stage)
+    {32, 224, 2, 2, 3, 1, 0.60},   // 30: 147 KB, 4 waves
+    {64, 224, 4, 2, 2, 1, 0.60},   // 31: 110 KB, 8 waves
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -994,6 +998,8 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 27: CTR_PL_ALL4(192, 64, 4, 2, 2) break;
     case 28: CTR_PL_ALL4(320, 64, 2, 2, 2) break;
     case 29: CTR_PL_AONLY(128, 160, 4, 2, 2) break;
+    case 30: if (!a_rc && !b_rc) CTR_PL_K(32, 224, 2, 2, 3, false, false, 1); break;
+    case 31: CTR_PL_AONLY(64, 224, 4, 2, 2) break;
   }
 }
 #undef CTR_PL_AONLY
