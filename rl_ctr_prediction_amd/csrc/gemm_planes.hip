@@ -784,6 +784,9 @@ static const PlDef kPl[] = {
     // instead of once per 64-wide N tile; 16 x 112 per wave (TN = 7: the pipelined stage)
     {32, 224, 2, 2, 3, 1, 0.60},   // 30: 147 KB, 4 waves
     {64, 224, 4, 2, 2, 1, 0.60},   // 31: 110 KB, 8 waves
+    // one wave per SIMD holding a 64 x 80 tile (TM 4, TN 5: 4.4x fewer LDS fragment bytes
+    // per MFMA than 16 x 80), the pipelined stage hiding its own reads
+    {128, 160, 2, 2, 2, 1, 0.60},  // 32: 110 KB, 4 waves
 };
 constexpr int kNumPl = sizeof(kPl) / sizeof(kPl[0]);
 
@@ -1000,6 +1003,7 @@ static void pl_launch(const PlCfg& c, const PlanesArgs& a, bool a_rc, bool b_rc,
     case 29: CTR_PL_AONLY(128, 160, 4, 2, 2) break;
     case 30: if (!a_rc && !b_rc) CTR_PL_K(32, 224, 2, 2, 3, false, false, 1); break;
     case 31: CTR_PL_AONLY(64, 224, 4, 2, 2) break;
+    case 32: CTR_PL_AONLY(128, 160, 2, 2, 2) break;
   }
 }
 #undef CTR_PL_AONLY
