@@ -171,24 +171,30 @@ def test_row_sharded_exchange_gloo(world):
 
 
 # ------------------------------------------------- fixed-capacity (padded) exchange ----
-def _padded_worker(rank, world, port, q):
+def _padded_worker(rank, world, port, q, layout="blocks"):
     """ShardedCTRTrainer's fixed-capacity protocol with numpy standing in for the GPU
-    kernels (ctr_shard_pack_ids / ctr_shard_runs_copy): capacity agreed by an all-reduce MAX,
-    equal-split all-to-alls of ids, rows and gradients, padding entries on each owner's spare
-    row (index = its row count)."""
+    kernels (ctr_shard_permute_ids / ctr_shard_pack_ids_layout / ctr_shard_runs_copy):
+    capacity agreed by an all-reduce MAX, equal-split all-to-alls of ids, rows and gradients,
+    padding entries on each owner's spare row (index = its row count). layout "cyclic": rank r
+    owns the rows r::N, the ids permuted to (r % N) * Vs + r // N before the plan, so each
+    owner's unique rows are again one ascending run."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from rl_ctr_prediction_amd.distributed import alltoall_equal
         V, K = 1000, 4
         shard = -(-V // world)
-        lo, hi = rank * shard, min(V, (rank + 1) * shard)
+        cyc = layout == "cyclic"
         table = np.arange(V * K, dtype=np.float32).reshape(V, K)
-        mine = np.concatenate([table[lo:hi], np.full((1, K), -7, np.float32)])  # + spare row
+        own = table[rank::world] if cyc else table[rank * shard:min(V, (rank + 1) * shard)]
+        n_own = own.shape[0]
+        mine = np.concatenate([own, np.full((1, K), -7, np.float32)])  # + spare row
         rng = np.random.default_rng(7 + rank)
         ids = rng.integers(0, V, size=500 + 111 * rank)
         ids[:50] = 3
-        uniq = np.unique(ids)
+        keys = (ids % world) * shard + ids // world if cyc else ids
+        uniq = np.unique(keys)
+        orig = (uniq % shard) * world + uniq // shard if cyc else uniq  # back to global rows
         owner = uniq // shard
         counts = np.bincount(owner, minlength=world)
         offsets = np.concatenate([[0], np.cumsum(counts)[:-1]])
@@ -197,39 +203,42 @@ def _padded_worker(rank, world, port, q):
         C = int(-(-int(cap) // 64) * 64)
         send = np.empty(world * C, np.int32)
         for j in range(world):
-            spare = min(shard, V - j * shard)
+            spare = len(range(j, V, world)) if cyc else min(shard, V - j * shard)
             run = uniq[offsets[j]:offsets[j] + counts[j]] - j * shard
             send[j * C:(j + 1) * C] = np.concatenate([run, np.full(C - counts[j], spare)])
         recv = torch.empty(world * C, dtype=torch.int32)
         alltoall_equal(recv, torch.tensor(send))
         loc = recv.numpy()
-        assert ((loc >= 0) & (loc <= hi - lo)).all()
+        assert ((loc >= 0) & (loc <= n_own)).all()
         rows_in = torch.empty(world * C, K)
         alltoall_equal(rows_in, torch.tensor(mine[loc]))
         got = np.concatenate([rows_in.numpy()[j * C:j * C + counts[j]] for j in range(world)])
-        np.testing.assert_array_equal(got, table[uniq])          # unpacked, compact order
-        cnt = np.array([(ids == u).sum() for u in uniq], dtype=np.float32)
+        np.testing.assert_array_equal(got, table[orig])          # unpacked, compact order
+        cnt = np.array([(ids == u).sum() for u in orig], dtype=np.float32)
         g = np.repeat((cnt * (rank + 1))[:, None], K, axis=1)
         g_pad = np.zeros((world * C, K), np.float32)
         for j in range(world):
             g_pad[j * C:j * C + counts[j]] = g[offsets[j]:offsets[j] + counts[j]]
         g_in = torch.empty(world * C, K)
         alltoall_equal(g_in, torch.tensor(g_pad))
-        sums = np.zeros((hi - lo + 1, K), np.float32)
+        sums = np.zeros((n_own + 1, K), np.float32)
         np.add.at(sums, loc, g_in.numpy())
         assert (sums[-1] == 0).all()                               # padding: zero gradients
         nz = np.nonzero(sums[:-1, 0])[0]
-        q.put((rank, nz + lo, sums[nz]))
+        rows = nz * world + rank if cyc else nz + rank * shard     # local -> global rows
+        q.put((rank, rows, sums[nz]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 5])
-def test_padded_exchange_gloo(world):
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (5, "blocks"), (3, "cyclic"),
+                                          (8, "cyclic")])
+def test_padded_exchange_gloo(world, layout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_padded_worker, args=(r, world, port, q, layout))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r[0], r[1:]) for r in collect_ranks(procs, q, world))
@@ -246,6 +255,10 @@ def test_padded_exchange_gloo(world):
         np.add.at(expect, ids, rank + 1)
     for rank in range(world):
         rows, sums = res[rank]
-        np.testing.assert_array_equal(rows, np.nonzero(expect[rank * shard:(rank + 1) * shard])[0]
-                                      + rank * shard)
+        if layout == "cyclic":
+            mine = np.arange(rank, V, world)
+            want = mine[expect[mine] != 0]
+        else:
+            want = np.nonzero(expect[rank * shard:(rank + 1) * shard])[0] + rank * shard
+        np.testing.assert_array_equal(rows, want)
         np.testing.assert_allclose(sums[:, 0], expect[rows])
