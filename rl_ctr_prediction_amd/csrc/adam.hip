@@ -21,17 +21,15 @@
 // (tests/test_gpu_deferred.py).
 #include "adam_common.h"
 
+#include <cstdlib>
+
 namespace ctr {
 
-// The replay step of an absent row (g = 0 before weight decay) on four elements. Measured
-// and rejected on MI355X (C3 table / C5 shape): an explicit packed-fp32 form (v_pk_fma_f32 /
-// v_pk_mul_f32: 4.32 vs 4.42 ms at 20 replayed steps, 3.06 vs 2.64 at 1 step — hipcc
-// SLP-packs this scalar form already), and one reciprocal per element pair (1/d0 = d1 *
-// rcp(d0*d1): the flush 33.3-34.1 ms either way at C5 — the extra multiplies cancel the saved
-// reciprocal; the replay issues ~7 VALU instructions per element-step whatever their kind).
-__device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v, const AdamHP& h) {
-  adam_vec(p, make_float4(0.f, 0.f, 0.f, 0.f), m, v, h);
-}
+// (adam_replay_vec, the replay step of an absent row, is in adam_common.h. Measured and
+// rejected on MI355X before it: an inline-asm packed form (4.32 vs 4.42 ms at 20 replayed
+// steps, 3.06 vs 2.64 at 1 step), and one reciprocal per element pair (1/d0 = d1 *
+// rcp(d0*d1): the flush 33.3-34.1 ms either way at C5 — the extra multiplies cancel the
+// saved reciprocal).)
 
 // ------------------------------------------------------------------ dense -----------
 // step_ptr != NULL: the step's scalars come from the device step table (HIP-graph replay)
@@ -242,7 +240,6 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
       pw = w[r]; mws = mw[r]; vws = vw[r];
     }
     if (!APPLY && from >= target) continue;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int s = from + 1; s <= target; ++s) {
       if (s >= win0) {
         const float2 v = s_tab[s - win0];
@@ -251,7 +248,7 @@ __global__ __launch_bounds__(256) void deferred_rows_vec(
       } else {
         load_step(h, tab, s);
       }
-      adam_vec(pp, z4, mm, vv, h);
+      adam_replay_vec(pp, mm, vv, h);
       if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
     }
     if (APPLY) {
@@ -303,7 +300,6 @@ __global__ __launch_bounds__(256) void deferred_catchup_wave(
   const int g = lane / K4, c = lane % K4;
   const int step = *step_ptr;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x / kWave);
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x / kWave) + wib) * kWave; base < S;
        base += nwaves * kWave) {
     const int64_t s = base + lane;
@@ -343,7 +339,7 @@ __global__ __launch_bounds__(256) void deferred_catchup_wave(
         load_step(h, tab, t);
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
-          if (t > ff[u]) adam_vec(pp[u], z4, mm[u], vv[u], h);
+          if (t > ff[u]) adam_replay_vec(pp[u], mm[u], vv[u], h);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -471,7 +467,6 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
   const int c = lane % K4, r_in = lane / K4;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
   const int64_t n_tiles = (V + kWave - 1) / kWave;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   auto set_step = [&](int t) {
     if (LDS_TAB) {
       const float2 v = s_tab[t];
@@ -528,6 +523,149 @@ __global__ __launch_bounds__(256) void deferred_flush_tile(
         }
     }
     if (from_l < step) last[my] = step;
+  }
+}
+
+// The flush, software-pipelined (build option CTR_FLUSH_PIPE=1, K4 >= 8; measured slower,
+// kept for the record). The tile kernel's waves each load a batch, replay it, store it;
+// at 20 replayed steps the flush measured close to the SUM of its row traffic and its replay
+// (C3 table: 3.09 ms at 1 step, 4.33 at 20, 7.22 at 40), which suggested waves of a SIMD
+// falling into step. Here each wave keeps the NEXT batch's loads in flight while it replays
+// the current one: two register buffers of UNR float4 rows (UNR = 2 keeps four waves per
+// SIMD at K = 64). Loads are unconditional — a row already current reads row 0's cached
+// columns instead — so the compiler's in-order vmcnt counting waits for the current buffer
+// only; stores stay predicated. A tile's NB batches are unrolled, the first batch of the
+// next tile (and its rows' last[] / linear state, one tile ahead) is issued under the
+// current tile's last batch; the linear weight's chain rides in the replay loop of a
+// tile's first batch. Bitwise the tile kernel (tests/test_gpu_deferred.py), but slower:
+// C3 table 4.62-4.68 vs 4.28-4.32 ms at 20 steps, 8.14-8.29 vs 7.26-7.50 at 40 (grids
+// 512-4096 no better) — the replay per step costs more at UNR = 2, and the flush's
+// counters (r02_flush_pmc.txt: VALU busy ~95 % of SIMD cycles at 20 steps, at ~1.8 GHz)
+// say it is arithmetic-bound there, not waiting on its loads.
+#ifndef CTR_FLUSH_PIPE
+#define CTR_FLUSH_PIPE 0
+#endif
+#ifndef CTR_FLUSH_PIPE_UNR
+#define CTR_FLUSH_PIPE_UNR 2
+#endif
+
+template <int UNR>
+struct FlushBatch {
+  float4 p[UNR], m[UNR], v[UNR];
+  int from[UNR];
+  int64_t e[UNR];
+};
+
+struct FlushTileMeta {  // the lane's own row of a tile: last[] and the linear weight's state
+  int fl;
+  float lp, lm, lv;
+};
+
+template <int K4, int UNR, bool LDS_TAB>
+__global__ __launch_bounds__(256) void deferred_flush_pipe(
+    float4* __restrict__ E, float4* __restrict__ mE, float4* __restrict__ vE,
+    float* __restrict__ w, float* __restrict__ mw, float* __restrict__ vw, int64_t V,
+    int32_t* __restrict__ last, int step, const float* __restrict__ tab, AdamHP h) {
+  extern __shared__ __attribute__((aligned(16))) float2 s_tab[];
+  if (LDS_TAB) {
+    for (int i = threadIdx.x; i <= step; i += blockDim.x)
+      s_tab[i] = reinterpret_cast<const float2*>(tab)[i];
+    __syncthreads();
+  }
+  constexpr int RPI = kWave / K4;  // rows per wave-instruction
+  constexpr int NB = K4 / UNR;     // batches per 64-row tile
+  static_assert(K4 % UNR == 0 && NB % 2 == 0, "an even number of batches per tile");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = lane % K4, r_in = lane / K4;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  const int64_t n_tiles = (V + kWave - 1) / kWave;
+  const int64_t t_first = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (t_first >= n_tiles) return;  // wave-uniform, after the block's only barrier
+  const int64_t t_last = t_first + (n_tiles - 1 - t_first) / waves * waves;
+  auto set_step = [&](int t) {
+    if (LDS_TAB) {
+      const float2 v = s_tab[t];
+      h.neg_step_size = v.x;
+      h.inv_bc2_sqrt = v.y;
+    } else {
+      load_step(h, tab, t);
+    }
+  };
+  auto load_meta = [&](int64_t tile, FlushTileMeta& M) {
+    const int64_t my = tile * kWave + lane;
+    const bool ok = my < V;
+    const int64_t ms = ok ? my : 0;  // clamped: every lane loads a valid address
+    const int f = last[ms];
+    M.fl = ok ? f : step;            // lanes past V read as current
+    if (w) {
+      M.lp = w[ms];
+      M.lm = mw[ms];
+      M.lv = vw[ms];
+    }
+  };
+  auto issue = [&](int64_t tile, int bi, const FlushTileMeta& M, FlushBatch<UNR>& X) {
+    const int64_t base = tile * kWave;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int r = (bi * UNR + u) * RPI + r_in;
+      X.from[u] = __shfl(M.fl, r, kWave);
+      X.e[u] = (base + r) * K4 + c;
+      const int64_t el = X.from[u] < step ? X.e[u] : c;  // current rows: row 0, cached
+      X.p[u] = E[el];
+      X.m[u] = mE[el];
+      X.v[u] = vE[el];
+    }
+  };
+  auto replay_store = [&](int64_t tile, bool first, FlushTileMeta& M, FlushBatch<UNR>& X) {
+    int f0 = step;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) f0 = min(f0, X.from[u]);
+    const int fl_lin = (first && w) ? M.fl : step;
+    f0 = min(f0, fl_lin);
+    for (int s = f0 + 1; s <= step; ++s) {
+      set_step(s);
+      if (s > fl_lin) adam_elem(M.lp, 0.f, M.lm, M.lv, h);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (s > X.from[u]) adam_replay_vec(X.p[u], X.m[u], X.v[u], h);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (X.from[u] < step) {
+        E[X.e[u]] = X.p[u];
+        mE[X.e[u]] = X.m[u];
+        vE[X.e[u]] = X.v[u];
+      }
+    if (first && M.fl < step) {  // fl < step only for rows below V
+      const int64_t my = tile * kWave + lane;
+      if (w) {
+        w[my] = M.lp;
+        mw[my] = M.lm;
+        vw[my] = M.lv;
+      }
+      last[my] = step;
+    }
+  };
+  FlushBatch<UNR> X0, X1;
+  FlushTileMeta cur, nxt;
+  load_meta(t_first, cur);
+  load_meta(t_first + waves <= t_last ? t_first + waves : t_last, nxt);
+  issue(t_first, 0, cur, X0);
+  for (int64_t tile = t_first; tile <= t_last; tile += waves) {
+    const int64_t nt = tile + waves <= t_last ? tile + waves : t_last;  // clamped: the last
+    // tile's prefetch re-reads a batch it never replays
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi) {
+      FlushBatch<UNR>& now = (bi & 1) ? X1 : X0;
+      FlushBatch<UNR>& ahead = (bi & 1) ? X0 : X1;
+      if (bi + 1 < NB)
+        issue(tile, bi + 1, cur, ahead);
+      else
+        issue(nt, 0, nxt, ahead);
+      replay_store(tile, bi == 0, cur, now);
+    }
+    cur = nxt;
+    load_meta(nt + waves <= t_last ? nt + waves : t_last, nxt);
   }
 }
 
@@ -768,7 +906,6 @@ __global__ __launch_bounds__(256) void deferred_entries_vec(
     }
     if (out) out[u * K4 + c] = g;
     if (out_lin && c == 0) out_lin[u] = gl;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int t = from + 1; t <= target; ++t) {
       if (t >= win0) {
         const float2 v = s_tab[t - win0];
@@ -777,7 +914,7 @@ __global__ __launch_bounds__(256) void deferred_entries_vec(
       } else {
         load_step(h, tab, t);
       }
-      adam_vec(pp, z4, mm, vv, h);
+      adam_replay_vec(pp, mm, vv, h);
       if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
     }
     load_step(h, tab, step);
@@ -926,7 +1063,36 @@ extern "C" int ctr_adam_deferred_flush(float* emb, float* m_emb, float* v_emb, f
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_tiles, 4), 8192));
     const bool lds = step < kMaxLdsSteps;
     const size_t lds_bytes = lds ? (size_t)(step + 1) * sizeof(float2) : 0;
-#define CTR_DEF_FLUSH(K4_, UNR_)                                                                 \
+    if (CTR_FLUSH_PIPE && K4 >= 8) {
+      // one generation of resident waves less a little (a wave's first batch is its only
+      // unhidden load): 256 CUs x 4 blocks of 4 waves at <= 128 VGPRs; CTR_FLUSH_GRID tunes
+      static const int64_t pipe_grid = [] {
+        const char* s = std::getenv("CTR_FLUSH_GRID");
+        return s ? std::max<int64_t>(1, std::atoll(s)) : int64_t(1024);
+      }();
+      const unsigned pgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_tiles, 4), pipe_grid));
+#define CTR_DEF_PIPE(K4_)                                                                     \
+  if (lds)                                                                                    \
+    hipLaunchKernelGGL((deferred_flush_pipe<K4_, CTR_FLUSH_PIPE_UNR, true>), pgrid, 256,      \
+                       lds_bytes, st, reinterpret_cast<float4*>(emb),                         \
+                       reinterpret_cast<float4*>(m_emb), reinterpret_cast<float4*>(v_emb), lin, \
+                       m_lin, v_lin, V, last, (int)step, step_table, h);                      \
+  else                                                                                        \
+    hipLaunchKernelGGL((deferred_flush_pipe<K4_, CTR_FLUSH_PIPE_UNR, false>), pgrid, 256, 0,  \
+                       st, reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),  \
+                       reinterpret_cast<float4*>(v_emb), lin, m_lin, v_lin, V, last,          \
+                       (int)step, step_table, h)
+      switch (K4) {
+        case 8: CTR_DEF_PIPE(8); break;
+        case 16: CTR_DEF_PIPE(16); break;
+        case 32: CTR_DEF_PIPE(32); break;
+        case 64: CTR_DEF_PIPE(64); break;
+      }
+#undef CTR_DEF_PIPE
+      CTR_LAUNCH_CHECK("deferred_flush_pipe");
+      return CTR_OK;
+    }
+#define CTR_DEF_FLUSH(K4_, UNR_)                                                           \
   if (lds)                                                                                      \
     hipLaunchKernelGGL((deferred_flush_tile<K4_, UNR_, true>), grid, 256, lds_bytes, st,        \
                        reinterpret_cast<float4*>(emb), reinterpret_cast<float4*>(m_emb),        \

@@ -47,6 +47,39 @@ __device__ __forceinline__ void adam_vec(float4& p, float4 g, float4& m, float4&
   adam_elem(p.w, g.w, m.w, v.w, h);
 }
 
+// The replay step of an absent row (g = 0 before weight decay) on four elements: adam_elem's
+// arithmetic exactly (same IEEE operations in the same order, so bitwise adam_vec with a zero
+// gradient), written on float pairs so that every non-transcendental operation is one
+// v_pk_* instruction — the denominator's fma included, which hipcc's SLP pass leaves scalar
+// in adam_vec because the square roots arrive as two scalars. The replay is the flush's
+// bound (VALU at ~90 % of SIMD cycles at 20 replayed steps, r02_flush_pmc.txt):
+// tools/replay_ubench.hip measured 37.3 vs 43.3 SIMD cycles per wave-element-step.
+typedef float ctr_f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void adam_replay_pair(float& p0, float& p1, float& m0, float& m1,
+                                                 float& v0, float& v1, const AdamHP& h) {
+#pragma clang fp contract(off)
+  const ctr_f2 p = {p0, p1}, m = {m0, m1}, v = {v0, v1};
+  const ctr_f2 wd = {h.wd, h.wd}, w1 = {h.w1, h.w1}, w2 = {h.w2, h.w2};
+  const ctr_f2 b2 = {h.beta2, h.beta2}, ib = {h.inv_bc2_sqrt, h.inv_bc2_sqrt};
+  const ctr_f2 ep = {h.eps, h.eps}, ns = {h.neg_step_size, h.neg_step_size}, z = {0.f, 0.f};
+  const ctr_f2 g = __builtin_elementwise_fma(wd, p, z);             // grad.add(param, alpha=wd)
+  const ctr_f2 mn = __builtin_elementwise_fma(w1, g - m, m);        // lerp_
+  const ctr_f2 vn = __builtin_elementwise_fma(w2 * g, g, v * b2);   // mul_(b2).addcmul_
+  const ctr_f2 sq = {__builtin_amdgcn_sqrtf(vn.x), __builtin_amdgcn_sqrtf(vn.y)};
+  const ctr_f2 d = __builtin_elementwise_fma(sq, ib, ep);
+  const ctr_f2 rc = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const ctr_f2 pn = __builtin_elementwise_fma(ns * mn, rc, p);      // addcdiv_
+  p0 = pn.x; p1 = pn.y;
+  m0 = mn.x; m1 = mn.y;
+  v0 = vn.x; v1 = vn.y;
+}
+
+__device__ __forceinline__ void adam_replay_vec(float4& p, float4& m, float4& v, const AdamHP& h) {
+  adam_replay_pair(p.x, p.y, m.x, m.y, v.x, v.y, h);
+  adam_replay_pair(p.z, p.w, m.z, m.w, v.z, v.w, h);
+}
+
 // step_tab[2t] = -lr/(1-beta1^t), step_tab[2t+1] = 1/sqrt(1-beta2^t)  (host doubles -> f32)
 __device__ __forceinline__ void load_step(AdamHP& h, const float* __restrict__ tab, int s) {
   const float2 v = reinterpret_cast<const float2*>(tab)[s];
@@ -80,10 +113,9 @@ __device__ __forceinline__ void deferred_apply_loaded(
     float4 vv, float pw, float mws, float vws) {
   const int64_t e = r * KV + c;
   const bool own_lin = w && c == 0;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int s = from + 1; s < step; ++s) {
     load_step(h, tab, s);
-    if (col) adam_vec(pp, z4, mm, vv, h);
+    if (col) adam_replay_vec(pp, mm, vv, h);
     if (own_lin) adam_elem(pw, 0.f, mws, vws, h);
   }
   load_step(h, tab, step);

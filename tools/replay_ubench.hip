@@ -36,6 +36,27 @@ __device__ __forceinline__ void replay1(float& p, float& m, float& v, const Adam
   }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// VAR 3: two elements at a time with every non-transcendental op packed, the denominator's
+// fma included (adam_elem leaves it scalar: the square roots arrive as two scalars).
+__device__ __forceinline__ void replay2(float& p0, float& p1, float& m0, float& m1, float& v0,
+                                        float& v1, const AdamHP& h) {
+#pragma clang fp contract(off)
+  const f2v p = {p0, p1}, m = {m0, m1}, v = {v0, v1};
+  const f2v wd = {h.wd, h.wd}, w1 = {h.w1, h.w1}, w2 = {h.w2, h.w2}, b2 = {h.beta2, h.beta2};
+  const f2v ib = {h.inv_bc2_sqrt, h.inv_bc2_sqrt}, ep = {h.eps, h.eps};
+  const f2v ns = {h.neg_step_size, h.neg_step_size}, z = {0.f, 0.f};
+  const f2v g = __builtin_elementwise_fma(wd, p, z);
+  const f2v mn = __builtin_elementwise_fma(w1, g - m, m);
+  const f2v vn = __builtin_elementwise_fma(w2 * g, g, v * b2);
+  const f2v sq = {__builtin_amdgcn_sqrtf(vn.x), __builtin_amdgcn_sqrtf(vn.y)};
+  const f2v d = __builtin_elementwise_fma(sq, ib, ep);
+  const f2v rc = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const f2v pn = __builtin_elementwise_fma(ns * mn, rc, p);
+  p0 = pn.x; p1 = pn.y; m0 = mn.x; m1 = mn.y; v0 = vn.x; v1 = vn.y;
+}
+
 template <int VAR, int NCH>
 __global__ __launch_bounds__(256) void replay_kernel(float* __restrict__ out, int steps,
                                                      const float2* __restrict__ tab, AdamHP h) {
@@ -54,8 +75,14 @@ __global__ __launch_bounds__(256) void replay_kernel(float* __restrict__ out, in
     const float2 t = s_tab[s];
     h.neg_step_size = t.x;
     h.inv_bc2_sqrt = t.y;
+    if constexpr (VAR == 3) {
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) replay1<VAR>(p[i], m[i], v[i], h);
+      for (int i = 0; i < NCH; i += 2)
+        replay2(p[i], p[i + 1], m[i], m[i + 1], v[i], v[i + 1], h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) replay1<VAR>(p[i], m[i], v[i], h);
+    }
   }
   float acc = 0.f;
 #pragma unroll
@@ -95,7 +122,7 @@ int main() {
   hipMalloc(&tab, sizeof(float2) * (steps + 1));
   hipMemcpy(tab, htab.data(), sizeof(float2) * (steps + 1), hipMemcpyHostToDevice);
   AdamHP h = make_hp(1e-3, 1.0, 0.9, 0.999, 1e-8, 1e-5);
-  const int blocks = 256 * 8;
+  const int blocks = 256 * 8;  // every launch below uses at most this many blocks
   float* out;
   hipMalloc(&out, sizeof(float) * blocks * 256);
   run<0, 16>("shipped adam_elem", out, tab, h, blocks, steps);
@@ -104,7 +131,8 @@ int main() {
   run<1, 16>("no transcendentals", out, tab, h, blocks, steps);
   run<2, 16>("same, explicit", out, tab, h, blocks, steps);
   run<0, 16>("shipped, 4 blk/CU", out, tab, h, 256 * 4, steps);
-  run<0, 16>("shipped, 16 blk/CU", out, tab, h, 256 * 16, steps);
+  run<3, 16>("packed denominator", out, tab, h, blocks, steps);
+  run<3, 8>("packed denominator", out, tab, h, blocks, steps);
   hipFree(out);
   hipFree(tab);
   return 0;
