@@ -58,6 +58,14 @@ const char* ctr_last_error(void);
 /* Number of visible HIP devices (0 on a host without a GPU); never initialises a context
  * beyond hipGetDeviceCount. */
 int ctr_device_count(void);
+/* A stream whose kernels run only on the CUs set in mask[0 .. n_words) (bit c % 32 of word
+ * c / 32 = CU c in the driver's numbering; hipExtStreamCreateWithCUMask), and its release.
+ * The mask holds for launches on that stream, eager or as the root of a graph launched on
+ * it, not for a graph branch forked onto it (tools/cumask_probe.hip). Used by the
+ * weight-gradient side stream experiment (CTR_WGRAD_CU_FRAC); no reference
+ * counterpart. */
+int ctr_stream_create_cu_masked(const uint32_t* mask, int n_words, ctr_stream_t* out);
+int ctr_stream_destroy(ctr_stream_t stream);
 
 /* ---------------------------------------------------------------- A3: gather ---------
  * out[i, :] = table[idx[i], :]  — nn.Embedding.forward.

@@ -177,6 +177,8 @@ SIGNATURES = {
     "ctr_shard_pack_ids_layout": (_i32, [_plan_p, _i64, _i64, _i32, _i32, _i64, _vp, _vp, _vp,
                                          _vp, _vp]),
     "ctr_shard_permute_ids": (_i32, [_vp, _i32, _i64, _i64, _i32, _i64, _vp, _vp]),
+    "ctr_stream_create_cu_masked": (_i32, [_vp, _i32, _vp]),
+    "ctr_stream_destroy": (_i32, [_vp]),
     "ctr_shard_runs_copy": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i32, _vp]),
     "ctr_batch_stage_copy": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp]),
     "ctr_sparse_plan_runs_workspace_bytes": (_i64, [_i32, _i64, _i64]),

@@ -598,6 +598,28 @@ def shard_permute_ids_(ids: torch.Tensor, V: int, n_shards: int, shard_rows: int
     return ids
 
 
+def cu_mask_words(n_cus: int, frac: float) -> list[int]:
+    """A CU mask keeping q/8 of n_cus CUs (q = round(8 * frac), 1..8), every XCD its share
+    whether the driver numbers CUs XCD by XCD (XCD = c // (n_cus / 8)) or round robin over
+    the XCDs (XCD = c % 8): CU c is kept when (c % 8 + c // (n_cus / 8)) % 8 < q."""
+    q = max(1, min(8, round(8 * frac)))
+    per = max(1, n_cus // 8)
+    words = [0] * ((n_cus + 31) // 32)
+    for c in range(n_cus):
+        if (c % 8 + c // per) % 8 < q:
+            words[c // 32] |= 1 << (c % 32)
+    return words
+
+
+def cu_masked_stream(words: list[int], device=None) -> torch.cuda.ExternalStream:
+    """A torch stream over a HIP stream whose kernels run only on the CUs set in `words`
+    (ctr_stream_create_cu_masked). It lives as long as the process."""
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    out = ctypes.c_void_p()
+    lib.ctr_stream_create_cu_masked(ctypes.addressof(arr), len(words), ctypes.addressof(out))
+    return torch.cuda.ExternalStream(out.value, device=device)
+
+
 _STAGE_COPY = os.environ.get("CTR_STAGE_COPY", "1") != "0"  # A/B: the runtime's copies
 
 

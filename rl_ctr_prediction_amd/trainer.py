@@ -288,6 +288,17 @@ class FusedCTRTrainer:
         self._wgrad_stream = None
         if self.kind in _MLP_KINDS:
             self._wgrad_stream = self._side if self._side is not None else self._new_stream()
+            # experiment: the weight-gradient stream on a fraction of the
+            # CUs, so dW0 leaves the rest to the scatter beside it. The mask holds for eager
+            # launches only — a graph branch forked onto a masked stream runs on every CU
+            # (tools/cumask_probe.hip) — so it was measured with graphs off: C3 5.2-5.8 vs
+            # 13.1-13.3 M ex/s unmasked, the masked queue's kernels no longer overlapping the
+            # main queue's (profiles/r06_cumask.txt). Not a default.
+            frac = os.environ.get("CTR_WGRAD_CU_FRAC")
+            if frac:
+                n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+                self._wgrad_stream = hip_ops.cu_masked_stream(
+                    hip_ops.cu_mask_words(n_cus, float(frac)), device=self.device)
         # the MLP weights' planes: rewritten by the dense Adam with every update
         # (ctr_adam_dense_planes), re-split from the fp32 parameters (the source of truth:
         # state_dict / load_state_dict see fp32) whenever those changed outside the trainer

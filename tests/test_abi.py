@@ -49,7 +49,7 @@ def test_python_binding_matches_header(built_lib):
     from rl_ctr_prediction_amd._lib import exported_symbols, lib
     assert set(exported_symbols()) == _header_functions()
     dll = lib.load()  # loads on a GPU-less host; resolves every symbol with argtypes
-    assert dll.ctr_abi_version() == 12
+    assert dll.ctr_abi_version() == 13
     assert dll.ctr_device_count() >= 0
 
 

@@ -55,6 +55,7 @@ int main() {
   for (uint32_t w : got) bits += __builtin_popcount(w);
   printf("masked stream: %d of %d CUs in its mask\n", bits, ncu);
 
+  bool verbose = false;
   auto run = [&](const char* name, auto launch) -> int {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -68,6 +69,11 @@ int main() {
     CK(hipEventSynchronize(b));
     CK(hipMemcpy(h.data(), d_out, blocks * sizeof(unsigned), hipMemcpyDeviceToHost));
     printf("%-44s distinct CUs %4d\n", name, distinct(h));
+    if (verbose) {  // the ids (__smid: XCC << (SE bits + CU bits) | SE << CU bits | CU)
+      std::set<unsigned> ids(h.begin(), h.end());
+      for (unsigned id : ids) printf(" %x", id);
+      printf("\n");
+    }
     return 0;
   };
 
@@ -76,12 +82,14 @@ int main() {
         return hipGetLastError() != hipSuccess;
       }))
     return 1;
+  verbose = true;
   if (run("eager, masked stream", [&] {
         where_kernel<<<blocks, 256, 0, masked>>>(d_out, sink, iters);
         return hipGetLastError() != hipSuccess;
       }))
     return 1;
 
+  verbose = false;
   hipGraph_t graph;
   hipGraphExec_t exec;
   CK(hipStreamBeginCapture(masked, hipStreamCaptureModeGlobal));
