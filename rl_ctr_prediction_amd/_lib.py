@@ -270,6 +270,7 @@ class _Lib:
         fn = self.raw(name)
         res = SIGNATURES[name][0]
         if res is not _i32 or name in ("ctr_abi_version", "ctr_device_count"):
+            self.__dict__[name] = fn
             return fn
 
         def checked(*args):
@@ -280,6 +281,7 @@ class _Lib:
             return rc
 
         checked.__name__ = name
+        self.__dict__[name] = checked  # later lookups skip __getattr__ (host cost per call)
         return checked
 
 

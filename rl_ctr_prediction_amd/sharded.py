@@ -408,7 +408,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         mean_div = float(global_batch if global_batch is not None else B * ws)
         self._sync_weight_planes()
         self._bound_staleness()
-        main, ps = torch.cuda.current_stream(), self._plan_stream
+        main, ps = hip_ops.current_stream(), self._plan_stream
         shape = (B, F, x.dtype)
         xkey = self._xkey(x)
         t_call = self._calls
@@ -528,7 +528,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         a = self._now
         if a is None:
             a = self._now = _Agreement(1, self.device)
-        cs, main = self._cap_stream, torch.cuda.current_stream()
+        cs, main = self._cap_stream, hip_ops.current_stream()
         cs.wait_event(slot.ev)
         torch.cuda.set_stream(cs)
         try:
@@ -557,7 +557,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
             if s is not None:
                 cs.wait_event(s.ev)
                 known.append((j, s))
-        main = torch.cuda.current_stream()
+        main = hip_ops.current_stream()
         torch.cuda.set_stream(cs)
         try:
             if len(known) < self.LOOKAHEAD:
@@ -613,7 +613,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
                 # while this thread captures: a thread-local capture, as the step's
                 mode = "thread_local" if self._coll else "global"
                 try:
-                    with graph_capture(g, pool=live_pool(self), stream=torch.cuda.current_stream(),
+                    with graph_capture(g, pool=live_pool(self), stream=hip_ops.current_stream(),
                                        capture_error_mode=mode):
                         self._plan_launch(slot)  # captured, not executed
                 except RuntimeError as e:
@@ -903,7 +903,7 @@ class ShardedCTRTrainer(FusedCTRTrainer):
         has_lin = self.w_tab is not None
         self._sync_weight_planes()
         self._bound_staleness()
-        main, ps = torch.cuda.current_stream(), self._plan_stream
+        main, ps = hip_ops.current_stream(), self._plan_stream
         xkey = self._xkey(x)
         ahead = [] if next_x is None else (
             [next_x] if isinstance(next_x, torch.Tensor) else list(next_x))

@@ -641,7 +641,7 @@ class FusedCTRTrainer:
                     nk.append((n, k))
                     if j < len(ys_) and ys_[j] is not None and ys_[j].numel() == n.shape[0]:
                         ny[k] = ys_[j]
-        main = torch.cuda.current_stream()
+        main = hip_ops.current_stream()
         slot = self._staged.pop(xkey, None)
         if self._staged:  # staged for batches that did not come next: free their slots
             keep = {k for _, k in nk}
@@ -989,7 +989,7 @@ class FusedCTRTrainer:
             # that node's hardware queue and the others start new queues; every fork / join
             # on the step's critical path costs ~5-12 us (rocprofv3 timelines) — so the
             # critical path is always enqueued before the branch that forks off it.
-            main = torch.cuda.current_stream()
+            main = hip_ops.current_stream()
             ev0 = torch.cuda.Event()
             ev0.record(main)  # x ready; previous step's plan users and Adam done
             ev_plan = torch.cuda.Event()
@@ -1058,7 +1058,7 @@ class FusedCTRTrainer:
         if self.kind == "FM" and not tail:  # MLP kinds: on the weight-gradient stream
             hip_ops.tensor_sum(gz, out=gv["bias"].view(1))
         if self._side is not None and not have_plan:
-            torch.cuda.current_stream().wait_event(ev_plan)  # the plan
+            hip_ops.current_stream().wait_event(ev_plan)  # the plan
         t = self._mark("scatter")
         sparse_rowmap = self.rowmap if (ws == 1 and not self.deferred) else None
         # one process, deferred Adam: the row sums are applied where they complete
@@ -1191,7 +1191,7 @@ class FusedCTRTrainer:
             hip_ops.split_planes(X, out=b.xp)
         self._span("gather", t)
         if getattr(b, "ev_tail", None) is not None:  # the previous step's MLP Adam
-            torch.cuda.current_stream().wait_event(b.ev_tail)
+            hip_ops.current_stream().wait_event(b.ev_tail)
         # Linear(F*K,300)+ReLU+Dropout: H1 (fp32 for the mask, planes for the next GEMMs)
         self._gemm_planes(b.xp, w0p, False, False, B, H1, W, out=b.h1, out_planes=b.h1p,
                           epi=hip_ops.EPI_BIAS_RELU_DROP if p0 > 0 else hip_ops.EPI_BIAS_RELU,
@@ -1268,7 +1268,7 @@ class FusedCTRTrainer:
     def _join_wgrad(self) -> None:
         """The dense-parameter gradients are complete on the current stream after this."""
         if self._wgrad_stream is not None:
-            torch.cuda.current_stream().wait_stream(self._wgrad_stream)
+            hip_ops.current_stream().wait_stream(self._wgrad_stream)
 
     def _exchange(self, b: _Bufs):
         """Sum embedding-row gradients over ranks (deterministic, identical everywhere)."""
