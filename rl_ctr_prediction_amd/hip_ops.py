@@ -614,7 +614,8 @@ def shard_permute_ids_(ids: torch.Tensor, V: int, n_shards: int, shard_rows: int
 def cu_mask_words(n_cus: int, frac: float) -> list[int]:
     """A CU mask keeping q/8 of n_cus CUs (q = round(8 * frac), 1..8), every XCD its share
     whether the driver numbers CUs XCD by XCD (XCD = c // (n_cus / 8)) or round robin over
-    the XCDs (XCD = c % 8): CU c is kept when (c % 8 + c // (n_cus / 8)) % 8 < q."""
+    the XCDs (XCD = c % 8): CU c is kept when (c % 8 + c // (n_cus / 8)) % 8 < q (exactly
+    balanced when n_cus is a multiple of 64, as MI355X's 256)."""
     q = max(1, min(8, round(8 * frac)))
     per = max(1, n_cus // 8)
     words = [0] * ((n_cus + 31) // 32)

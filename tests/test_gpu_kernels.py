@@ -1031,3 +1031,28 @@ def test_shard_permute_ids_and_cyclic_pack(cuda, dtype):
         assert int(counts[j]) == len(mine)
         assert np.array_equal(s[j, :len(mine)], mine), j
         assert (s[j, len(mine):] == len(range(j, V, N))).all(), j
+
+
+def test_cu_masked_stream_runs_kernels(cuda):
+    """ctr_stream_create_cu_masked: a stream on half the CUs (hip_ops.cu_masked_stream) runs
+    the library's kernels with the same results as the default stream (the permute kernel,
+    bit-exact), and ctr_stream_destroy releases a stream it made."""
+    from rl_ctr_prediction_amd import hip_ops as H
+    from rl_ctr_prediction_amd._lib import lib
+    n_cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    st = H.cu_masked_stream(H.cu_mask_words(n_cus, 0.5), device=cuda)
+    V, N = 1000, 3
+    Vs = -(-V // N)
+    ids = torch.randint(0, V, (4096,), device=cuda, generator=torch.Generator(cuda).manual_seed(5))
+    ref = H.shard_permute_ids_(ids.clone(), V, N, Vs)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        got = H.shard_permute_ids_(ids.clone(), V, N, Vs)
+    st.synchronize()
+    assert torch.equal(got, ref)
+    import ctypes
+    h = ctypes.c_void_p()
+    words = (ctypes.c_uint32 * 1)(0xFFFF)
+    lib.ctr_stream_create_cu_masked(ctypes.addressof(words), 1, ctypes.addressof(h))
+    assert h.value
+    lib.ctr_stream_destroy(h.value)
