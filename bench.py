@@ -829,8 +829,10 @@ def main():
         chunk = H.rows_chunk(C, K, lin)
         dense_n = int(trainer.flat_grad.numel())
         result["sharding"] = {
-            "shard_rows": int(trainer.V_tab), "row_range": [int(trainer.row_lo),
-                                                           int(trainer.row_hi)],
+            # rows: ["cyclic", rank, N, V] (this rank owns global rows rank::N) or, for the
+            # blocks layout, [row_lo, row_hi, V] (sharded.shard_meta)
+            "shard_rows": int(trainer.V_tab), "layout": trainer.layout,
+            "rows": trainer.shard_meta(),
             "capacity_rows": C, "chunk_floats": int(chunk),
             "exchange_bytes_per_step": {
                 "ids_alltoall": world * C * 4, "rows_alltoall": world * chunk * 4,
@@ -843,12 +845,12 @@ def main():
             "captures": getattr(trainer, "captures", None),
             "host_reads_blocking": trainer.cap_blocking, "host_reads": trainer.cap_reads}
         if world > 1:  # every rank's shard and capacity, gathered to rank 0 for the line
-            mine = [trainer.V_tab, trainer.row_lo, trainer.row_hi, C, U]
+            mine = [trainer.V_tab, trainer.shard_meta(), C, U]
             allr = [None] * world
             dist.all_gather_object(allr, mine)
             result["sharding"]["per_rank"] = [
-                {"rank": r, "shard_rows": a[0], "row_range": [a[1], a[2]], "capacity_rows": a[3],
-                 "unique_rows_last_batch": a[4]} for r, a in enumerate(allr)]
+                {"rank": r, "shard_rows": a[0], "rows": a[1], "capacity_rows": a[2],
+                 "unique_rows_last_batch": a[3]} for r, a in enumerate(allr)]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(cfg, host_batches)
