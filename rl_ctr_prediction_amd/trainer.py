@@ -338,7 +338,7 @@ class FusedCTRTrainer:
         env = os.environ.get("CTR_PLAN_AFTER_STEP")
         self.plan_after_step = (env == "1") if env in ("0", "1") else False
         self._ev_end = None
-        # MLP kinds, opt-in (CTR_PLAN_IN_GRAPH=1): the next batch's plan inside this step's
+        # opt-in (CTR_PLAN_IN_GRAPH=1): the next batch's plan inside this step's
         # graph, on the side list between dW1 and the dX join; a staged batch is then only
         # copied ahead. Traced at C3 (round 6, profiles/r06_c3_timelines.txt): a plan built on
         # a plan stream lands wherever its queue lets it — beside dX (free), beside dW0 on some
@@ -346,9 +346,12 @@ class FusedCTRTrainer:
         # spread 394-460 us. In the side list the column sort stretches to ~83 us beside dX
         # and delays dW0 until after the scatter: every step 435-450 us (scatter 40 us alone
         # instead of 84 beside dW0, dW0 66 alone instead of 85, but serial), C3 12.73 / 12.78
-        # / 12.92 vs 13.32 / 13.32 / 13.39 M ex/s off (alternating): off by default
+        # / 12.92 vs 13.32 / 13.32 / 13.39 M ex/s off (alternating): off by default. FM (the
+        # plan on the side list beside the gather and scatter, joined before the tail: one
+        # graph launch per step instead of two) at C2: 37.9 / 40.0 / 47.7 / 39.8 vs 49.3 /
+        # 55.4 / 49.2 / 55.7 M ex/s off — the join costs the GPU more than the launch saves
         env = os.environ.get("CTR_PLAN_IN_GRAPH")
-        self.plan_in_graph = (env == "1") and self.kind in _MLP_KINDS
+        self.plan_in_graph = (env == "1") and self.kind in _MLP_KINDS + ("FM",)
         self._next_plan = None  # the staged slot whose plan the step being launched builds
         # cross-step pipelining of the MLP kinds' weight-gradient tail (one process, deferred
         # mode): the largest weight gradient dW0 = dH1^T X and the MLP weights' Adam of step t
@@ -982,6 +985,7 @@ class FusedCTRTrainer:
         gv = self.grad_views
         step_hint = self.step_count + 1
         self._ev_wplanes = None
+        ev_nplan = None  # FM plan_in_graph: the next batch's plan, joined before the tail
         if self._side is not None:
             # the sparse plan is only needed from the scatter on: build it on a side stream
             # while the catch-up (plan-free, from the ids) and the forward run here.
@@ -1034,6 +1038,18 @@ class FusedCTRTrainer:
                     b.ev_tail.record()
             if not self.plan_first:
                 plan()
+            nxt = self._next_plan
+            if nxt is not None and self.kind not in _MLP_KINDS:
+                # FM (plan_in_graph): the next batch's plan on the side list, beside this
+                # step's gather and scatter, joined before the step's tail: one graph launch
+                # per step instead of a step graph and a plan graph
+                self._side.wait_event(ev0)
+                with torch.cuda.stream(self._side):
+                    t_p = self._mark("plan")
+                    nxt.plan.build(nxt.ids, self.V)
+                    self._span("plan", t_p)
+                    ev_nplan = torch.cuda.Event()
+                    ev_nplan.record()
         else:
             t_plan = self._mark("plan")
             b.plan.build(x, self.V)  # rows of this batch (needed before the forward when deferred)
@@ -1106,6 +1122,8 @@ class FusedCTRTrainer:
                                    self.eps, self.weight_decay, step_dev=self.step_cur,
                                    table=self.step_table)
         self._span("adam", t)
+        if ev_nplan is not None:
+            hip_ops.current_stream().wait_event(ev_nplan)
         # the dense Adam where the dense gradient completes: on the weight-gradient stream
         # at one process (beside the embedding apply), after the exchange otherwise
         if tail:

@@ -221,11 +221,14 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
     out = []
     # (batches ahead, HIP graphs, plan lookahead, labels staged too: None / the batch's own
     # (its step skips the label copy) / a decoy (its step must copy its own y))
-    for ahead, graphs, pla, ymode in ((0, True, False, None), (1, True, True, None),
-                                      (2, True, True, None), (2, False, True, None),
-                                      (2, True, False, None), (1, False, True, None),
-                                      (2, True, True, "own"), (1, False, True, "own"),
-                                      (2, True, True, "decoy")):
+    # (+ pig: the next batch's plan built inside the step's graph, plan_in_graph)
+    for ahead, graphs, pla, ymode, pig_on in (
+            (0, True, False, None, False), (1, True, True, None, False),
+            (2, True, True, None, False), (2, False, True, None, False),
+            (2, True, False, None, False), (1, False, True, None, False),
+            (2, True, True, "own", False), (1, False, True, "own", False),
+            (2, True, True, "decoy", False), (2, True, True, None, True),
+            (1, True, True, "own", True), (2, False, True, None, True)):
         torch.manual_seed(8)
         with torch.device(cuda):
             m = {"FM": lambda: P.FM(V, K), "DeepFM": lambda: P.DeepFM(V, F, K),
@@ -235,6 +238,7 @@ def test_plan_lookahead_bitwise(cuda, kind, V, K, B):
         tr = P.FusedCTRTrainer(m, lr=1e-3, weight_decay=1e-5, seed=7)
         tr.use_graphs = graphs
         tr.plan_lookahead = pla  # default: FM only; exercised for every kind here
+        tr.plan_in_graph = pig_on
         losses = []
         for j, (i, n) in enumerate(order):
             nxt = xs[n] if (ahead and n is not None) else None
