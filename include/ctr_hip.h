@@ -199,8 +199,9 @@ int ctr_gemm_planes_lastcol(int a_rc, int b_rc, int64_t M, int64_t N, int64_t K,
  * ctr_fm_forward_planes: ctr_fm_forward (no BCE head; DeepFM's FM part) whose flattened
  *   embeddings (emb_out [B, F*K]) are written as planes; needs K % 4 == 0, (K/4) | 64,
  *   F <= 64. Replaces: p_model.py:303,320 (the two gathers of DeepFM.forward).
- * ctr_deepfm_head_planes: ctr_deepfm_head with labels, writing dh_pre [B, H] in fp32 and
- *   as planes (the dH1 / dW1 GEMM operand). Replaces: p_model.py:290-293,322 backward. */
+ * ctr_deepfm_head_planes: ctr_deepfm_head with labels, writing dh_pre [B, H] in fp32 (dh_pre
+ *   may be NULL: the planes only) and as planes (the dH1 / dW1 GEMM operand). Replaces:
+ *   p_model.py:290-293,322 backward. */
 int ctr_fm_forward_planes(const void* idx, int idx_type, int64_t B, int F, int K, int64_t V,
                           const float* emb, const float* lin, const float* bias, float* z,
                           float* sum_e, const ctr_planes* emb_planes, int32_t* err_flag,

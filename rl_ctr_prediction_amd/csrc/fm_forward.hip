@@ -238,11 +238,11 @@ __global__ __launch_bounds__(256) void deepfm_head_kernel(
     if (loss_out && y) loss_out[b] = l;
     if (gz_out && y) gz_out[b] = g;
   }
-  if (dh_pre && y) {
-    float* d = dh_pre + b * H;
+  if ((dh_pre || dpl) && y) {  // dh_pre NULL: the planes only (no reader of the fp32 copy)
+    float* d = dh_pre ? dh_pre + b * H : nullptr;
     auto put = [&](int j, float hj, float wj) {
       const float v = hj > 0.f ? (g * wj) * drop_scale : 0.f;
-      d[j] = v;
+      if (d) d[j] = v;
       if (dpl) {  // dH2's planes for the dH1 / dW1 GEMMs (csrc/gemm_planes.hip)
         uint16_t h3[3];
         psplit1(v, h3);
@@ -475,7 +475,7 @@ extern "C" int ctr_deepfm_head_planes(const float* h, int64_t B, int H, const fl
                                       float mean_div, float drop_scale, float* z, float* p,
                                       float* loss_elem, float* gz, float* dh_pre,
                                       const ctr_planes* dh_planes, ctr_stream_t stream) {
-  CTR_REQUIRE(h && w_out && b_out && z_fm && labels && dh_pre && dh_planes && dh_planes->data,
+  CTR_REQUIRE(h && w_out && b_out && z_fm && labels && dh_planes && dh_planes->data,
               "ctr_deepfm_head_planes: null pointer");
   CTR_REQUIRE(B >= 0 && H > 0 && mean_div > 0.f, "ctr_deepfm_head_planes: bad sizes");
   CTR_REQUIRE(dh_planes->rows >= B && dh_planes->cols >= H && dh_planes->ld >= H,
