@@ -139,7 +139,6 @@ class _Bufs:
     h1: torch.Tensor | None = None
     h2: torch.Tensor | None = None
     head: dict | None = None
-    dh1: torch.Tensor | None = None
     dx: torch.Tensor | None = None
     # exact three-plane bf16 splits (hip_ops.Planes) of the MLP GEMM operands, written by
     # their producers; the GEMMs read them in the stored orientation (csrc/gemm_planes.hip)
